@@ -1,0 +1,339 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE.
+
+Run in the build container only (needs /root/reference, read-only):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+
+The reference is imported from /root/reference with a minimal harness
+(SURVEY.md 8(c)): stub modules for the absent torchvision/torchmetrics (not on
+the loss-math path), and ``model.graph.load_graph`` replaced by a reader of our
+JSON adjacency files (pinned equal to the reference gpickles by
+tests/test_graph.py) -- nothing from the reference is unpickled.  Weights come
+from ``oracle.step.formula_state_dict`` (a deterministic function of the
+parameter name and element index) and are loaded with ``load_state_dict``.
+
+Outputs are small .npz files (data only: inputs and expected outputs).  The
+oracle is checked against them by tests/test_oracle_goldens.py, and the HIP
+build by the GPU parity tests.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+os.environ['PYTHONDONTWRITEBYTECODE'] = '1'
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import yaml  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+
+
+# ------------------------------------------------------------------ harness --
+def _install_stubs():
+    def mod(name, **attrs):
+        m = types.ModuleType(name)
+        m.__dict__.update(attrs)
+        sys.modules[name] = m
+        return m
+
+    ident = lambda *a, **k: (lambda x: x)  # noqa: E731
+    tv = mod('torchvision')
+    tv.utils = mod('torchvision.utils', make_grid=lambda *a, **k: None,
+                   save_image=lambda *a, **k: None)
+    tv.transforms = mod('torchvision.transforms', Resize=ident, ToTensor=ident,
+                        RandomHorizontalFlip=ident, Compose=ident)
+    tv.transforms.functional = mod('torchvision.transforms.functional')
+    tm = mod('torchmetrics')
+    tm.functional = mod('torchmetrics.functional',
+                        structural_similarity_index_measure=lambda *a, **k: None)
+
+
+class _Adj:
+    def __init__(self, adj):
+        self.adj = adj
+
+    def number_of_nodes(self):
+        return len(self.adj)
+
+    def neighbors(self, i):
+        return iter(self.adj[i])
+
+
+def _json_graph_loader(path):
+    # path = <dir>/stage_{s}.gpickle  ->  repo graphs/<dirname>/stage_{s}.json
+    d = os.path.basename(os.path.dirname(path))
+    f = os.path.basename(path).replace('.gpickle', '.json')
+    with open(os.path.join(REPO, 'graphs', d, f)) as fh:
+        return _Adj(json.load(fh)['adj'])
+
+
+def import_reference():
+    _install_stubs()
+    sys.path.insert(0, REF)
+    import model as ref_model  # noqa: E402
+    import model.graph as ref_graph  # noqa: E402
+    ref_graph.load_graph = _json_graph_loader
+    import train.loss as ref_loss  # noqa: E402
+    import train.utils as ref_utils  # noqa: E402
+    return ref_model, ref_loss, ref_utils
+
+
+# ------------------------------------------------------------------- inputs --
+def smooth_texture(b, c, h, w, seed=1234, sigma=2.0):
+    """Gaussian-blurred U[0,1) noise, renormalised to [0.05, 0.95]."""
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(b, c, h, w, generator=g)
+    r = int(3 * sigma)
+    t = torch.arange(-r, r + 1, dtype=torch.float32)
+    k = torch.exp(-t * t / (2 * sigma * sigma))
+    k = k / k.sum()
+    x = torch.nn.functional.conv2d(x.reshape(b * c, 1, h, w), k.view(1, 1, 1, -1),
+                                   padding=(0, r))
+    x = torch.nn.functional.conv2d(x, k.view(1, 1, -1, 1), padding=(r, 0))
+    x = x.reshape(b, c, h, w)
+    lo = x.amin(dim=(2, 3), keepdim=True)
+    hi = x.amax(dim=(2, 3), keepdim=True)
+    return 0.05 + 0.9 * (x - lo) / (hi - lo)
+
+
+def stereo_pair(b, h, w, seed=1234):
+    left = smooth_texture(b, 3, h, w, seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    dfield = smooth_texture(b, 1, h, w, seed + 2, sigma=6.0) * 0.1  # 0..0.1 * W
+    del g
+    sys.path.insert(0, REPO)
+    from oracle import loss as OL  # noqa: E402
+    right = OL.reconstruct(dfield, left)  # right sees left shifted by d
+    return left.contiguous(), right.contiguous(), dfield
+
+
+def pred_pyramid(b, h, w, seed, scale=0.3):
+    """4-level 4-channel prediction pyramid in (0, scale) like the disp head."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for i in range(4):
+        hh, ww = h // 2 ** i, w // 2 ** i
+        z = smooth_texture(b, 4, hh, ww, seed + 10 + i, sigma=1.5)
+        z = (z - 0.5) * 4 + 0.2 * torch.randn(b, 4, hh, ww, generator=g)
+        out.append(scale * torch.sigmoid(z))
+    return out
+
+
+# ------------------------------------------------------------------ goldens --
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **{k: (v.detach().cpu().numpy() if torch.is_tensor(v)
+                                     else np.asarray(v)) for k, v in arrays.items()})
+    print(f'wrote {path} ({os.path.getsize(path) / 1024:.1f} KB)')
+
+
+def gen_warp(ref_utils):
+    g = torch.Generator().manual_seed(7)
+    arrays = {}
+    for tag, (b, h, w) in {'small': (2, 4, 8), 'mid': (2, 32, 64)}.items():
+        img = torch.rand(b, 3, h, w, generator=g)
+        d = (torch.rand(b, 1, h, w, generator=g) - 0.5) * 0.6
+        arrays[f'{tag}_img'] = img
+        arrays[f'{tag}_disp'] = d
+        arrays[f'{tag}_out'] = ref_utils.reconstruct(d, img)
+        arrays[f'{tag}_out_zero'] = ref_utils.reconstruct(torch.zeros_like(d), img)
+        arrays[f'{tag}_left'] = ref_utils.reconstruct_left_image(d, img)
+        arrays[f'{tag}_right'] = ref_utils.reconstruct_right_image(d, img)
+    save('warp.npz', **arrays)
+
+
+def gen_loss(ref_loss, ref_utils, cfg, b=2, h=32, w=64, grads=True, name='loss.npz'):
+    left, right, _ = stereo_pair(b, h, w)
+    images = torch.cat([left, right], 1)
+    arrays = {'images': images}
+    pyr = ref_utils.scale_pyramid(images, 4)
+    for i, p in enumerate(pyr):
+        arrays[f'pyr{i}'] = p
+    for tex, seed in (('smooth', 21), ('rough', 22)):
+        preds = pred_pyramid(b, h, w, seed)
+        if tex == 'rough':
+            g = torch.Generator().manual_seed(99)
+            preds = [0.3 * torch.rand(p.shape, generator=g).clamp_min(1e-3) for p in preds]
+        for i, p in enumerate(preds):
+            arrays[f'{tex}_pred{i}'] = p
+        for lt in ('l1', 'bayesian', 'log_bayesian'):
+            lcfg = json.loads(json.dumps(cfg['loss']))
+            lcfg['error_loss_config']['loss_type'] = lt
+            lf = ref_loss.TukraUncertaintyLoss(**lcfg)
+            ps = [p.clone().requires_grad_(True) for p in preds]
+            recon = ref_utils.reconstruct_pyramid(ps, pyr)
+            if lt == 'l1':
+                for i, r in enumerate(recon):
+                    arrays[f'{tex}_recon{i}'] = r
+            dl, el = lf(pyr, ps, recon, 0, None)
+            arrays[f'{tex}_{lt}_disp_loss'] = dl.detach()
+            arrays[f'{tex}_{lt}_error_loss'] = el.detach()
+            if not grads:
+                continue
+            # separate gradients of the two returned scalars
+            ps2 = [p.clone().requires_grad_(True) for p in preds]
+            recon2 = ref_utils.reconstruct_pyramid(ps2, pyr)
+            dl2, el2 = lf(pyr, ps2, recon2, 0, None)
+            gd = torch.autograd.grad(dl2, ps2, retain_graph=True, allow_unused=True)
+            ge = torch.autograd.grad(el2, ps2, allow_unused=True)
+            for i in range(4):
+                arrays[f'{tex}_{lt}_gdisp{i}'] = gd[i] if gd[i] is not None else torch.zeros_like(preds[i])
+                arrays[f'{tex}_{lt}_gerr{i}'] = ge[i] if ge[i] is not None else torch.zeros_like(preds[i])
+            # per-term values (reference sub-modules, same loop as loss.py:541-550)
+            with torch.no_grad():
+                t = {'wssim': 0., 'consistency': 0., 'smoothness': 0., 'error': 0.}
+                rc = ref_utils.reconstruct_pyramid(preds, pyr)
+                for i, (im, p, r) in enumerate(zip(pyr, preds, rc)):
+                    d = p[:, :2]
+                    t['wssim'] += float(lf.wssim(im, r))
+                    t['consistency'] += float(lf.consistency(d))
+                    t['smoothness'] += float(lf.smoothness(d, im) / 2 ** i)
+                    t['error'] += float(lf.predictive_error(p, im, lf.wssim.previous_image_error))
+                    if lt == 'l1':
+                        arrays[f'{tex}_err{i}'] = lf.wssim.previous_image_error
+                for k, v in t.items():
+                    arrays[f'{tex}_{lt}_term_{k}'] = np.float64(v)
+    if not grads:
+        arrays = {k: v for k, v in arrays.items() if 'recon' not in k
+                  and not k.startswith('pyr') and 'err' not in k[-5:]}
+    save(name, **arrays)
+
+
+def _formula_weights(cfg, nodes_dir=None):
+    sys.path.insert(0, REPO)
+    from oracle import model as OM  # noqa: E402
+    from oracle import step as OS  # noqa: E402
+    graphs = OM.load_stage_graphs(cfg['model']['encoder'])
+    specs = OS.param_specs(cfg['model'], graphs)
+    return OS.formula_state_dict(specs), specs
+
+
+def _ref_model(ref_model, cfg):
+    mcfg = json.loads(json.dumps(cfg['model']))
+    mcfg['encoder']['load_graph'] = os.path.join(REF, 'graphs', 'nodes_5_seed_42') \
+        if mcfg['encoder'].get('nodes', 5) == 5 else \
+        os.path.join('/nonexistent', os.path.basename(mcfg['encoder']['load_graph']))
+    return ref_model.RandomlyConnectedModel(**mcfg)
+
+
+def gen_model(ref_model, cfg):
+    sd, specs = _formula_weights(cfg)
+    m = _ref_model(ref_model, cfg)
+    ref_keys = list(m.state_dict().keys())
+    assert ref_keys == [s[0] for s in specs], 'state_dict schema mismatch'
+    shapes_ok = all(tuple(m.state_dict()[k].shape) == tuple(s[1]) for k, s in zip(ref_keys, specs))
+    assert shapes_ok
+    m.load_state_dict(sd)
+    b, h, w = 2, 64, 128
+    left, right, _ = stereo_pair(b, h, w, seed=4321)
+    m.train()
+    with torch.no_grad():
+        d1, d2, d3, d4 = m(left, 0.3)
+    arrays = {'left': left, 'train_d1': d1, 'train_d2': d2, 'train_d3': d3, 'train_d4': d4}
+    arrays['running_mean_sum'] = sum(v.sum() for k, v in m.state_dict().items()
+                                     if k.endswith('running_mean'))
+    arrays['running_var_sum'] = sum(v.sum() for k, v in m.state_dict().items()
+                                    if k.endswith('running_var'))
+    m2 = _ref_model(ref_model, cfg)
+    m2.load_state_dict(sd)
+    m2.eval()
+    with torch.no_grad():
+        arrays['eval_d1'] = m2(left[:1], 0.3)
+    # encoder features at stage granularity (a localisation aid)
+    with torch.no_grad():
+        m3 = _ref_model(ref_model, cfg)
+        m3.load_state_dict(sd)
+        m3.train()
+        feats = m3.encoder(left)
+        for i, f in enumerate(feats):
+            arrays[f'feat{i}_sum'] = f.double().sum()
+            arrays[f'feat{i}_abssum'] = f.double().abs().sum()
+    arrays['schema'] = np.array(json.dumps([[s[0], list(s[1])] for s in specs]))
+    save('model_fwd.npz', **arrays)
+
+
+def gen_step(ref_model, ref_loss, ref_utils, cfg, loss_type, steps=3, tag=None):
+    sd, specs = _formula_weights(cfg)
+    m = _ref_model(ref_model, cfg)
+    m.load_state_dict(sd)
+    m.train()
+    lcfg = json.loads(json.dumps(cfg['loss']))
+    lcfg['error_loss_config']['loss_type'] = loss_type
+    lf = ref_loss.TukraUncertaintyLoss(**lcfg)
+    opt = torch.optim.Adam(m.parameters(), 1e-4)
+    b, h, w = 2, 64, 128
+    left, right, _ = stereo_pair(b, h, w, seed=555)
+    arrays = {'left': left, 'right': right}
+    scale = float(ref_utils.adjust_disparity(0))
+    arrays['scale'] = np.float64(scale)
+    for step in range(steps):
+        images = torch.cat([left, right], 1)
+        pyr = ref_utils.scale_pyramid(images, 4)
+        opt.zero_grad()
+        disps = m(left, scale)
+        recon = ref_utils.reconstruct_pyramid(disps, pyr)
+        dl, el = lf(pyr, disps, recon, step, None)
+        (dl + el).backward()
+        if step == 0:
+            for k, p in m.named_parameters():
+                arrays[f'gradnorm/{k}'] = p.grad.double().norm()
+            for i, d in enumerate(disps):
+                arrays[f'step0_disp{i}'] = d.detach()
+        opt.step()
+        arrays[f'disp_loss_{step}'] = dl.detach()
+        arrays[f'error_loss_{step}'] = el.detach()
+        if step == 0:
+            for k, v in m.state_dict().items():
+                if k.endswith('running_mean') or k.endswith('running_var'):
+                    arrays[f'bn/{k}'] = v.clone()
+                elif v.is_floating_point():
+                    arrays[f'param_sum/{k}'] = v.double().sum()
+                    arrays[f'param_abs/{k}'] = v.double().abs().sum()
+    save(f'step_{tag or loss_type}.npz', **arrays)
+
+
+def gen_nodes10(ref_model, cfg10):
+    sd, specs = _formula_weights(cfg10)
+    m = _ref_model(ref_model, cfg10)
+    assert list(m.state_dict().keys()) == [s[0] for s in specs]
+    m.load_state_dict(sd)
+    m.train()
+    left, _, _ = stereo_pair(1, 64, 128, seed=777)
+    with torch.no_grad():
+        d = m(left, 0.3)
+    save('nodes10_fwd.npz', left=left, train_d1=d[0], train_d4=d[3],
+         schema=np.array(json.dumps([[s[0], list(s[1])] for s in specs])))
+
+
+def main():
+    ref_model, ref_loss, ref_utils = import_reference()
+    torch.set_num_threads(8)
+    with open(os.path.join(REPO, 'config.yml')) as f:
+        cfg = yaml.safe_load(f)
+    with open(os.path.join(REPO, 'config_nodes10.yml')) as f:
+        cfg10 = yaml.safe_load(f)
+    which = sys.argv[1:] or ['warp', 'loss', 'model', 'step', 'nodes10']
+    if 'warp' in which:
+        gen_warp(ref_utils)
+    if 'loss' in which:
+        gen_loss(ref_loss, ref_utils, cfg)
+        gen_loss(ref_loss, ref_utils, cfg, 2, 64, 128, grads=False, name='loss_64x128.npz')
+    if 'model' in which:
+        gen_model(ref_model, cfg)
+    if 'step' in which:
+        gen_step(ref_model, ref_loss, ref_utils, cfg, 'bayesian')
+        gen_step(ref_model, ref_loss, ref_utils, cfg, 'l1', steps=1)
+    if 'nodes10' in which:
+        gen_nodes10(ref_model, cfg10)
+
+
+if __name__ == '__main__':
+    main()
