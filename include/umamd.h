@@ -1,0 +1,215 @@
+/*
+ * umamd -- MI355X (gfx950) kernels for the self-supervised depth+uncertainty
+ * training step of Probabilistic-Surgical-Vision/uncertainty-model.
+ *
+ * C ABI (drop-in boundary under the Python host layer in
+ * uncertainty-model_amd/umamd/).  Rules:
+ *   - plain pointers, sizes and enums only; no torch types;
+ *   - device pointers are caller-owned (PyTorch caching allocator); the
+ *     library never allocates or frees and never synchronises the host;
+ *   - every entry takes the HIP stream to launch on (torch's current stream);
+ *   - returns UM_OK (0) or an error code; um_last_error() gives a
+ *     thread-local message (entries are called from PyTorch's autograd thread).
+ *
+ * Tensor conventions: activations are NHWC with a pixel stride `ld`
+ * (elements between consecutive pixels; >= channels), element type UM_F32 or
+ * UM_BF16 as given by `dtype`; arithmetic is always f32.  Conv weights are
+ * repacked per step from the reference's NCHW f32 parameters
+ * ([K][C][R][R], reference nn.Conv2d) into [K][R][R][Cp] ("forward") and
+ * [Cp][R][R][K] ("transposed", for the data gradient), Cp = C rounded up to 8.
+ *
+ * Each entry cites the reference operation it replaces (file:line in the
+ * reference repository).
+ */
+#ifndef UMAMD_H
+#define UMAMD_H
+
+#include <hip/hip_runtime.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { UM_OK = 0, UM_ERR_ARG = 1, UM_ERR_HIP = 2 };
+enum { UM_F32 = 0, UM_BF16 = 1 };
+enum { UM_PAD_ZERO = 0, UM_PAD_REFLECT = 1 };
+enum {
+  UM_EPI_NONE = 0,           /* y = acc (+ bias)                               */
+  UM_EPI_STATS = 1,          /* y = acc + bias, per-block BN partial sums      */
+  UM_EPI_SIGMOID_SCALE = 2,  /* y(f32) = scale * sigmoid(acc + bias)           */
+  UM_EPI_RESIDUAL = 3        /* y = acc + bias + residual                      */
+};
+
+const char* um_last_error(void);
+int um_version(void);
+
+/* ---------------------------------------------------------------- conv ---
+ * Replaces nn.Conv2d forward/backward with its padding:
+ *   encoder ConvELUBlock: F.pad zero + Conv2d(k, stride)
+ *       reference model/layers/encoder.py:42-52
+ *   decoder ConvLayer: ReflectionPad2d(1) + Conv2d(3) / 1x1 without padding
+ *       reference model/layers/decoder.py:30-52
+ *   attention 1x1 K/Q/V/reprojection: reference model/layers/attention.py:37-40,66-76
+ * Implicit GEMM on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32).
+ */
+/* number of BN partial rows written by um_conv2d_fwd with UM_EPI_STATS for M output pixels and K channels */
+int um_conv_stats_parts(int M, int K);
+
+int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
+                  const void* wf, const float* bias, int K, int R, int stride,
+                  int pad, int pad_mode, int P, int Q, int ydtype, void* y,
+                  int ldy, int epilogue, float epi_scale, const void* residual,
+                  int ldr, float* stats_partials, hipStream_t stream);
+
+/* data gradient: dx[N,H,W,C] (= or +=) conv^T(dy[N,P,Q,K], wT) incl. the
+ * reflect-pad fold and the stride-2 scatter */
+int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx,
+                    int accumulate, const void* wT, int K, int R, int stride,
+                    int pad, int pad_mode, int P, int Q, const void* dy, int ldy,
+                    hipStream_t stream);
+
+/* weight gradient partial slabs [splits][K][R*R*C] (f32); splits from um_conv_wgrad_splits */
+int um_conv_wgrad_splits(int M, int K, int RRC);
+int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* x,
+                    int K, int R, int stride, int pad, int pad_mode, int P, int Q,
+                    const void* dy, int ldy, float* slabs, int splits,
+                    hipStream_t stream);
+/* sum slabs -> reference NCHW weight grad [Kreal][Creal][R][R] (f32), (+)= */
+int um_conv_wgrad_reduce(const float* slabs, int splits, int K, int Kreal, int R, int C,
+                         int Creal, float* dw, int accumulate, hipStream_t stream);
+
+/* repack f32 NCHW weight [K][Creal][R][R] -> wf [K][R][R][C] (row stride ldf
+ * elements) and wT [C][R][R][ldT] (column offset applied by the caller); C >= Creal, zero fill */
+int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C,
+                   void* wf, void* wT, int ldT, hipStream_t stream);
+
+/* per-channel column sums of y[M][C] (pixel stride ld) -> partial rows [parts][C] */
+int um_colsum_parts(int M);
+int um_colsum(int dtype, int M, int C, int ld, const void* y, float* partials,
+              hipStream_t stream);
+/* out[c] (+)= sum_p partials[p][c] (+ optional second partial set) */
+int um_reduce_rows(const float* partials, int parts, int C, int stride, float* out,
+                   int accumulate, hipStream_t stream);
+
+/* ------------------------------------------------------------------ BN ---
+ * Training-mode nn.BatchNorm2d + nn.ELU, reference model/layers/encoder.py:43-44,
+ * model/layers/decoder.py:82-84; SyncBatchNorm semantics when the host
+ * all-reduces the f64 per-channel sums between the phases
+ * (reference parallel_main.py:157).
+ */
+int um_bn_stats_reduce(const float* parts, int nparts, int C, double* out, hipStream_t stream);
+int um_bn_coeffs(const double* stats, double count, int C, const float* gamma,
+                 const float* beta, float eps, float momentum, float* running_mean,
+                 float* running_var, long long* num_batches_tracked, float* mean,
+                 float* invstd, float* scale, float* shift, hipStream_t stream);
+int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
+                  const float* shift, void* a, int lda, int apply_elu, hipStream_t stream);
+int um_bn_bwd_parts(long M);
+int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int ldda,
+                         const void* y, int ldy, const float* mean, const float* invstd,
+                         const float* scale, const float* shift, const float* add_nc,
+                         int apply_elu, float* parts, hipStream_t stream);
+int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamma,
+                     const float* invstd, const double* stats_local, float* dgamma,
+                     float* dbeta, int accumulate, float* k1, float* k2, float* k3,
+                     hipStream_t stream);
+int um_bn_elu_bwd_apply(int dtype, long M, int C, long HW, const void* da, int ldda,
+                        const void* y, int ldy, const float* mean, const float* invstd,
+                        const float* scale, const float* shift, const float* add_nc,
+                        int apply_elu, const float* k1, const float* k2, const float* k3,
+                        void* dy, int lddy, hipStream_t stream);
+
+/* ------------------------------------------------------- encoder misc ---
+ * NodeBlock merge, reference model/layers/encoder.py:115-124 (F3 index map
+ * passed in widx: input i weighted by sigmoid(w[widx[i]])).
+ */
+/* coefficient of input i: sigmoid(w[widx[i]]) if w, else coefs[i] (host array), else 1 */
+int um_merge_fwd(int dtype, int nsrc, const void* const* srcs, const int* widx,
+                 const float* w, const float* coefs, long count, void* dst, hipStream_t stream);
+int um_merge_parts(long count);
+int um_merge_bwd(int dtype, int nsrc, const void* const* srcs, void* const* dsrcs,
+                 const int* accumulate, const int* widx, const float* w, const float* coefs,
+                 long count, const void* dm, float* parts, hipStream_t stream);
+int um_merge_wgrad(const float* parts, int nparts, int nsrc, const int* widx,
+                   const float* w, float* dw, int nw, int accumulate, hipStream_t stream);
+int um_image_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp,
+                     void* out, hipStream_t stream);
+int um_axpy(int dtype, long n, float alpha, const void* x, void* y, hipStream_t stream);
+/* d/dlogit of scale*sigmoid(logit): disp head, reference model/layers/decoder.py:246 */
+int um_sigmoid_scale_bwd(int dtype, long M, int C, const float* d, int ldd, const float* dd,
+                         int lddd, float scale, void* dlogit, int ldo, hipStream_t stream);
+
+/* ----------------------------------------------------------- attention ---
+ * EfficientAttention core, reference model/layers/attention.py:42-76.
+ * qkv [N*S][ld]: K cols [0,C), Q [C,2C), V [2C,3C).
+ */
+long um_attn_ws_kstats(int N, int S, int C);
+long um_attn_ws_ctx(int N, int S, int C, int heads);
+long um_attn_ws_tiles(int N, int S, int C, int heads);
+int um_attn_fwd(int dtype, int N, int S, int C, int heads, const void* qkv, int ld,
+                float* kmax, float* ksum, float* ctx, float* ws, void* att, int ldo,
+                hipStream_t stream);
+int um_attn_bwd(int dtype, int N, int S, int C, int heads, const void* qkv, int ld,
+                const float* kmax, const float* ksum, const float* ctx, const void* datt,
+                int ldd, void* dqkv, int ldq, float* dks_ws, float* ws, float* dctx,
+                float* r, hipStream_t stream);
+
+/* ------------------------------------------------------------- decoder ---
+ * Decoder-stage concat/upsample/pixel-shuffle/SE, reference
+ * model/layers/decoder.py:90-136,210-249.
+ */
+enum { UM_CAT_COPY = 0, UM_CAT_UP2 = 1, UM_CAT_PSHUF = 2 };
+typedef struct {
+  const void* ptr;     /* source (NHWC, pixel stride ld) */
+  const float* scale;  /* optional per-(n,c) gate [N][C] */
+  int C, ld, op, coff, dtype, h, w; /* channels, stride, op, dst channel offset, dtype, src size */
+} um_cat_src;
+int um_concat_build(int dtype, int N, int H, int W, void* dst, int ld, int Ctot, int nsrc,
+                    const um_cat_src* srcs, hipStream_t stream);
+int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
+                      const um_cat_src* src, void* dsrc, int ldd, int dsrc_dtype,
+                      int accumulate, float* dscale, hipStream_t stream);
+int um_channel_mean(int dtype, int N, long S, int C, const void* x, int ld, float* out,
+                    hipStream_t stream);
+int um_se_mlp_fwd(int N, int C, int R, const float* pooled, const float* w1, const float* w2,
+                  float* z1, float* s, hipStream_t stream);
+int um_se_mlp_bwd(int N, int C, int R, const float* ds, const float* s, const float* z1,
+                  const float* pooled, const float* w1, const float* w2, float* dw1,
+                  float* dw2, float* dpool_scaled, float inv_S, hipStream_t stream);
+
+/* ---------------------------------------------------------------- loss ---
+ * Loss stack: scale_pyramid (reference train/utils.py:27-50), reconstruct
+ * (train/utils.py:65-109), TukraUncertaintyLoss forward/backward
+ * (train/loss.py:15-264,340-434,512-568).  Images NCHW f32 [N][6][H][W];
+ * predictions NHWC f32 [N][H][W][pld] (d_L, d_R, sigma_L, sigma_R).
+ * loss_type: 0 l1, 1 bayesian, 2 log_bayesian (train/loss.py:364-375).
+ */
+int um_pyramid_level(const float* x, int NC, int H, int W, float* out, int h, int w,
+                     hipStream_t stream);
+int um_warp(const float* img, int N, int C, int H, int W, const float* disp, long disp_sn,
+            long disp_sp, float sign, float* out, hipStream_t stream);
+int um_loss_parts(int N, int H, int W);
+int um_loss_fwd_scale(const float* img, const float* rec, const float* pred, int pld, int N,
+                      int H, int W, float alpha, int loss_type, float esw, float ecw,
+                      float* D, float* e, float* parts, hipStream_t stream);
+int um_loss_finalize(int nscales, const float* const* parts, const int* nparts,
+                     const double* npix, float w_wssim, float w_cons, float w_smooth,
+                     float w_err, float esw, float ecw, int loss_type, float* out,
+                     hipStream_t stream);
+int um_loss_bwd_scale(const float* img, const float* rec, const float* pred, int pld, int N,
+                      int H, int W, float alpha, int loss_type, float esw, float ecw,
+                      const float* e, const float* gout, float w_wssim, float w_cons,
+                      float w_smooth, float w_err, float smooth_div, float* dpred,
+                      hipStream_t stream);
+
+/* ---------------------------------------------------------------- adam ---
+ * torch.optim.Adam step, reference train/train.py:228-229.
+ */
+int um_adam_chunk(void);
+int um_adam_step(const void* table, const void* chunks, int nchunks, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, int step, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UMAMD_H */

@@ -1,0 +1,258 @@
+"""Kernel-level parity: each umamd autograd op (HIP) vs a plain-PyTorch fp32
+CPU reference of the same op, forward and backward.  Marked gpu."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _nhwc(x):  # NCHW cpu -> NHWC device
+    return x.permute(0, 2, 3, 1).contiguous().to(DEV)
+
+
+def _nchw(x):
+    return x.detach().permute(0, 3, 1, 2).float().cpu()
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+CONV_CASES = [
+    # (Cin, Cout, k, stride, pad_mode, H, W)
+    (8, 32, 7, 2, 'zero', 16, 24),
+    (32, 32, 7, 1, 'zero', 12, 20),
+    (32, 64, 5, 2, 'zero', 16, 16),
+    (64, 64, 3, 1, 'zero', 8, 12),
+    (40, 48, 3, 1, 'reflect', 10, 14),
+    (24, 40, 1, 1, 'zero', 6, 10),
+    (16, 8, 3, 1, 'reflect', 4, 6),
+]
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_conv_bn_elu(case, dtype):
+    from umamd import functional as U
+    from umamd._lib import PAD_REFLECT, PAD_ZERO
+    Cin, Cout, k, stride, mode, H, W = case
+    N = 2
+    pad = (k - 1) // 2
+    conv = nn.Conv2d(Cin, Cout, k, stride)
+    bn = nn.BatchNorm2d(Cout)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(N, Cin, H, W)
+    # CPU reference
+    xr = x.clone().requires_grad_(True)
+    cr, br = nn.Conv2d(Cin, Cout, k, stride), nn.BatchNorm2d(Cout)
+    cr.load_state_dict(conv.state_dict())
+    br.load_state_dict(bn.state_dict())
+    xp = F.pad(xr, (pad,) * 4, mode='reflect' if mode == 'reflect' else 'constant')
+    yr = F.elu(br(cr(xp)))
+    g = torch.randn_like(yr)
+    (yr * g).sum().backward()
+    # HIP
+    cd, bd = conv.to(DEV), bn.to(DEV)
+    xd = _nhwc(x).to(dtype).requires_grad_(True)
+    yd = U.conv_bn_elu(xd, cd, bd, pad, PAD_REFLECT if mode == 'reflect' else PAD_ZERO)
+    (yd.float() * _nhwc(g)).sum().backward()
+    tol = 1e-4 if dtype == torch.float32 else 5e-2
+    assert _rel(_nchw(yd), yr) < tol
+    assert _rel(_nchw(xd.grad), xr.grad) < tol * 5
+    assert _rel(cd.weight.grad, cr.weight.grad) < tol * 5
+    assert _rel(bd.weight.grad, br.weight.grad) < tol * 5
+    assert _rel(bd.bias.grad, br.bias.grad) < tol * 5
+    assert _rel(bd.running_mean, br.running_mean) < tol
+    assert _rel(bd.running_var, br.running_var) < tol
+    assert int(bd.num_batches_tracked) == 1
+
+
+def test_conv_first_layer_padded_channels():
+    """3-channel image -> 8-channel NHWC pad; weight packed with Creal=3."""
+    from umamd import functional as U
+    from umamd._lib import PAD_ZERO
+    conv = nn.Conv2d(3, 32, 7, 2)
+    bn = nn.BatchNorm2d(32)
+    x = torch.rand(2, 3, 32, 64)
+    yr = F.elu(bn(conv(F.pad(x, (3,) * 4))))
+    xd = U.image_to_nhwc(x.to(DEV), torch.float32)
+    yd = U.conv_bn_elu(xd, conv.to(DEV), bn.to(DEV), 3, PAD_ZERO)
+    assert _rel(_nchw(yd), yr) < 1e-4
+
+
+def test_merge():
+    from umamd import functional as U
+    w = torch.tensor([0.3, -0.7, 1.1, 0.2])
+    xs = [torch.randn(2, 4, 6, 16) for _ in range(4)]
+    wr = w.clone().requires_grad_(True)
+    xr = [x.clone().requires_grad_(True) for x in xs]
+    ref = torch.sigmoid(wr[0]) * xr[0]
+    for i, x in enumerate(xr[1:]):
+        ref = ref + torch.sigmoid(wr[i]) * x
+    g = torch.randn_like(ref)
+    (ref * g).sum().backward()
+    wd = w.to(DEV).requires_grad_(True)
+    xd = [x.to(DEV).requires_grad_(True) for x in xs]
+    out = U.merge(xd, wd, [0, 0, 1, 2])
+    (out * g.to(DEV)).sum().backward()
+    assert _rel(out, ref) < 1e-6
+    assert _rel(wd.grad, wr.grad) < 1e-5
+    assert wd.grad[3].item() == 0.0  # F3: last weight never used
+    for a, b in zip(xd, xr):
+        assert _rel(a.grad, b.grad) < 1e-6
+
+
+@pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 8), (512, 2, 4), (256, 4, 8)])
+def test_attention_block(C, H, W):
+    from oracle.model import efficient_attention
+    from umamd import functional as U
+    import importlib
+    att = importlib.import_module('model.layers.attention').EfficientAttention(C, C, C, 8)
+    x = torch.randn(2, C, H, W)
+    P = {k: v.clone().requires_grad_(True) for k, v in att.state_dict().items()}
+    xr = x.clone().requires_grad_(True)
+    yr = efficient_attention(xr, P, '', 8)
+    g = torch.randn_like(yr)
+    (yr * g).sum().backward()
+    ad = att.to(DEV)
+    xd = _nhwc(x).requires_grad_(True)
+    yd = U.attention_block(xd, ad)
+    (yd * _nhwc(g)).sum().backward()
+    assert _rel(_nchw(yd), yr) < 1e-5
+    assert _rel(_nchw(xd.grad), xr.grad) < 1e-4
+    for name in ('keys', 'queries', 'values', 'reprojection'):
+        for t in ('weight', 'bias'):
+            ref = P[f'{name}.{t}'].grad
+            got = getattr(getattr(ad, name), t).grad
+            if name == 'keys' and t == 'bias':
+                # softmax over pixels is shift invariant: true gradient 0
+                assert got.abs().max() < 1e-4 * (1 + ref.abs().max())
+                continue
+            assert _rel(got, ref) < 1e-4, (name, t)
+
+
+def _decoder_stage_case(cfg, N, h, w, with_gate, with_disp):
+    import importlib
+    from oracle.model import decoder_stage
+    DS = importlib.import_module('model.layers.decoder').DecoderStage
+    st = DS(**cfg)
+    for m in st.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            with torch.no_grad():
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(N, cfg['in_channels'], h // 2, w // 2)
+    f = torch.randn(N, cfg['feature_in_channels'], h, w)
+    sk = torch.randn(N, cfg['skip_in_channels'], h // 2, w // 2)
+    gate = torch.rand(N, cfg['skip_in_channels']) if with_gate else None
+    d = 0.3 * torch.rand(N, cfg.get('disp_channels', 2), h // 2, w // 2) if with_disp else None
+    return st, x, f, sk, gate, d
+
+
+@pytest.mark.parametrize('with_gate,with_disp,fC', [(False, False, 256), (True, True, 64),
+                                                      (True, True, 3)])
+def test_decoder_stage(with_gate, with_disp, fC):
+    from oracle.model import decoder_stage
+    cfg = dict(in_channels=64, feature_in_channels=fC, skip_in_channels=64,
+               upsample_channels=16, out_channels=32, skip_out_channels=32,
+               concat_disp=with_disp, calculate_disp=True, disp_channels=4)
+    N, h, w = 2, 16, 24
+    st, x, f, sk, gate, d = _decoder_stage_case(cfg, N, h, w, with_gate, with_disp)
+    P = {k: v.clone() for k, v in st.state_dict().items()}
+    for k in P:
+        if P[k].is_floating_point() and 'running' not in k:
+            P[k].requires_grad_(True)
+    xr, fr, skr = [t.clone().requires_grad_(True) for t in (x, f, sk)]
+    dr = d.clone().requires_grad_(True) if d is not None else None
+    gr = gate.clone().requires_grad_(True) if gate is not None else None
+    skin = skr * gr[:, :, None, None] if gate is not None else skr
+    out_r, skip_r, disp_r = decoder_stage(xr, fr, skin, dr, 0.3, P, '', cfg, True)
+    go, gs, gd = torch.randn_like(out_r), torch.randn_like(skip_r), torch.randn_like(disp_r)
+    ((out_r * go).sum() + (skip_r * gs).sum() + (disp_r * gd).sum()).backward()
+
+    from umamd.functional import image_to_nhwc
+    sd = st.to(DEV)
+    xd = _nhwc(x).requires_grad_(True)
+    fd = image_to_nhwc(f.to(DEV), torch.float32) if fC % 8 else _nhwc(f)
+    fd.requires_grad_(fC % 8 == 0)
+    skd = _nhwc(sk).requires_grad_(True)
+    gated = gate.to(DEV).requires_grad_(True) if gate is not None else None
+    dd = _nhwc(d).requires_grad_(True) if d is not None else None
+    out_d, (u1, s), disp_d = sd._fwd(xd, fd, (skd, gated) if gated is not None else skd, dd,
+                                     0.3)
+    skip_d = u1 * s[:, None, None, :]
+    ((out_d * _nhwc(go)).sum() + (skip_d * _nhwc(gs)).sum() +
+     (disp_d * _nhwc(gd)).sum()).backward()
+    assert _rel(_nchw(out_d), out_r) < 1e-4
+    assert _rel(_nchw(skip_d), skip_r) < 1e-4
+    assert _rel(_nchw(disp_d), disp_r) < 1e-4
+    assert _rel(_nchw(xd.grad), xr.grad) < 1e-3
+    assert _rel(_nchw(skd.grad), skr.grad) < 1e-3
+    if fC % 8 == 0:
+        assert _rel(_nchw(fd.grad), fr.grad) < 1e-3
+    if dd is not None:
+        assert _rel(_nchw(dd.grad), dr.grad) < 1e-3
+    if gated is not None:
+        assert _rel(gated.grad, gr.grad) < 1e-3
+    sdict = dict(sd.named_parameters())
+    for k, v in P.items():
+        if not (v.is_floating_point() and 'running' not in k) or v.grad is None:
+            continue
+        got = sdict[k].grad
+        if k.endswith('layers.0.layers.0.bias') and 'disp' not in k:
+            continue  # pre-BN bias: true gradient 0
+        assert got is not None, k
+        assert _rel(got, v.grad) < 2e-3, k
+
+
+def test_pyramid_and_warp_goldens():
+    from conftest import GOLDEN
+    import os
+    from umamd import lossfn as LF
+    z = np.load(os.path.join(GOLDEN, 'loss.npz'))
+    imgs = torch.from_numpy(z['images']).to(DEV)
+    pyr = LF.scale_pyramid(imgs, 4)
+    for i in range(4):
+        assert _rel(pyr[i], torch.from_numpy(z[f'pyr{i}'])) < 1e-6
+    w = np.load(os.path.join(GOLDEN, 'warp.npz'))
+    for tag in ('small', 'mid'):
+        img = torch.from_numpy(w[f'{tag}_img']).to(DEV)
+        d = torch.from_numpy(w[f'{tag}_disp']).to(DEV)
+        assert _rel(LF.reconstruct(d, img, 1.0), torch.from_numpy(w[f'{tag}_out'])) < 1e-5
+        assert _rel(LF.reconstruct(0 * d, img, 1.0), torch.from_numpy(w[f'{tag}_out_zero'])) < 1e-5
+        assert _rel(LF.reconstruct(d, img, -1.0), torch.from_numpy(w[f'{tag}_left'])) < 1e-5
+
+
+def test_adam_matches_torch():
+    from umamd.optim import Adam
+    ps = [torch.randn(37, 5), torch.randn(10000), torch.randn(3)]
+    gs = [[torch.randn_like(p) for p in ps] for _ in range(3)]
+    pr = [p.clone().requires_grad_(True) for p in ps]
+    pd = [p.clone().to(DEV).requires_grad_(True) for p in ps]
+    o1 = torch.optim.Adam(pr, 1e-3)
+    o2 = Adam(pd, 1e-3)
+    for step in range(3):
+        for p, g in zip(pr, gs[step]):
+            p.grad = g.clone()
+        for p, g in zip(pd, gs[step]):
+            p.grad = g.clone().to(DEV)
+        o1.step()
+        o2.step()
+    for a, b in zip(pd, pr):
+        assert _rel(a, b) < 1e-6

@@ -1,0 +1,413 @@
+// Efficient (linear) attention core, reference model/layers/attention.py:42-76.
+//
+// Layout: qkv[m = n*S + s][ld] holds K in columns [0,C), Q in [C,2C), V in
+// [2C,3C) (the three 1x1 convs run as one GEMM).  Heads h own channels
+// [h*d, (h+1)*d), d = C / heads.
+//   Ks  = softmax over pixels s of K[:, c]            (per n, c)   attention.py:63
+//   Qs  = softmax over the head's d channels of Q[s]  (per n, s, h) attention.py:64
+//   ctx = Ks_h^T V_h   (d x d per n, h)                             attention.py:66
+//   att = Qs_h ctx_h   -> written [m][C]                            attention.py:68-71
+// The 1x1 reprojection + residual is a conv epilogue (conv.hip).
+// Backward recomputes Ks/Qs from qkv and the saved (kmax, ksum).
+#include "common.h"
+
+namespace {
+
+constexpr int KS_CHUNK = 256;  // pixels per k-stat partial
+constexpr int PT = 64;         // pixels per apply tile
+
+// ---------------------------------------------------------------- k stats --
+template <typename T>
+__global__ void kstats_kernel(const T* __restrict__ qkv, int ld, int S, int C,
+                              float* __restrict__ parts, int nchunks) {
+  const int n = blockIdx.y, chunk = blockIdx.x;
+  const int s0 = chunk * KS_CHUNK, s1 = min(S, s0 + KS_CHUNK);
+  __shared__ float sm[4][64], ss[4][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int c = c0 + cl;
+    float mx = -INFINITY, sum = 0.f;
+    if (c < C) {
+      for (int s = s0 + pl; s < s1; s += 4) {
+        const float v = to_f32(qkv[((long)n * S + s) * ld + c]);
+        if (v > mx) {
+          sum = sum * __expf(mx - v) + 1.f;
+          mx = v;
+        } else {
+          sum += __expf(v - mx);
+        }
+      }
+    }
+    sm[pl][cl] = mx;
+    ss[pl][cl] = sum;
+    __syncthreads();
+    if (pl == 0 && c < C) {
+      float M = sm[0][cl];
+      for (int r = 1; r < 4; ++r) M = fmaxf(M, sm[r][cl]);
+      float t = 0.f;
+      for (int r = 0; r < 4; ++r)
+        if (sm[r][cl] > -INFINITY) t += ss[r][cl] * __expf(sm[r][cl] - M);
+      float* o = parts + (((long)n * nchunks + chunk) * C + c) * 2;
+      o[0] = M;
+      o[1] = t;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void kstats_combine_kernel(const float* __restrict__ parts, int N, int nchunks, int C,
+                                      float* __restrict__ kmax, float* __restrict__ ksum) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i % C;
+  float M = -INFINITY;
+  for (int k = 0; k < nchunks; ++k) M = fmaxf(M, parts[(((long)n * nchunks + k) * C + c) * 2]);
+  float t = 0.f;
+  for (int k = 0; k < nchunks; ++k) {
+    const float* p = parts + (((long)n * nchunks + k) * C + c) * 2;
+    if (p[0] > -INFINITY) t += p[1] * __expf(p[0] - M);
+  }
+  kmax[i] = M;
+  ksum[i] = t;
+}
+
+// ------------------------------------------------------------------- ctx --
+// partial ctx over a pixel chunk: parts[n][chunk][h][d][d]
+template <typename T>
+__global__ void ctx_kernel(const T* __restrict__ qkv, int ld, int S, int C, int heads,
+                           const float* __restrict__ kmax, const float* __restrict__ ksum,
+                           int chunk_px, int nchunks, float* __restrict__ parts) {
+  extern __shared__ float sh[];
+  const int d = C / heads;
+  const int chunk = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int s0 = chunk * chunk_px, s1 = min(S, s0 + chunk_px);
+  const int np = s1 - s0;
+  float* sK = sh;                  // [chunk_px][d]
+  float* sV = sh + chunk_px * d;   // [chunk_px][d]
+  for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
+    const int s = i / d, c = i % d;
+    const long row = ((long)n * S + s0 + s) * ld;
+    const int ch = h * d + c;
+    sK[i] = __expf(to_f32(qkv[row + ch]) - kmax[n * C + ch]) / ksum[n * C + ch];
+    sV[i] = to_f32(qkv[row + 2 * C + ch]);
+  }
+  __syncthreads();
+  const int dd = d * d;
+  const int lanes = dd >= 256 ? 1 : 256 / dd;
+  float* red = sh + 2 * chunk_px * d;  // [256]
+  for (int o0 = 0; o0 < dd; o0 += 256 / lanes) {
+    const int o = o0 + threadIdx.x % (256 / lanes);
+    const int pl = threadIdx.x / (256 / lanes);
+    float acc = 0.f;
+    if (o < dd && pl < lanes) {
+      const int c = o / d, cp = o % d;
+      for (int s = pl; s < np; s += lanes) acc += sK[s * d + c] * sV[s * d + cp];
+    }
+    if (lanes > 1) {
+      red[threadIdx.x] = acc;
+      __syncthreads();
+      if (pl == 0 && o < dd) {
+        float t = 0.f;
+        for (int r = 0; r < lanes; ++r) t += red[r * (256 / lanes) + threadIdx.x];
+        acc = t;
+      }
+      __syncthreads();
+    }
+    if (pl == 0 && o < dd)
+      parts[(((long)n * nchunks + chunk) * heads + h) * dd + o] = acc;
+  }
+}
+
+// out[n][j] = sum_b parts[n][b][j]
+__global__ void sum_parts_kernel(const float* __restrict__ parts, int N, int B, int L,
+                                 float* __restrict__ out) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)N * L) return;
+  const int n = i / L, j = i % L;
+  float t = 0.f;
+  for (int b = 0; b < B; ++b) t += parts[((long)n * B + b) * L + j];
+  out[i] = t;
+}
+
+// ----------------------------------------------------------------- apply --
+template <typename T>
+__global__ void apply_kernel(const T* __restrict__ qkv, int ld, int S, int C, int heads,
+                             const float* __restrict__ ctx, T* __restrict__ att, int ldo) {
+  extern __shared__ float sh[];
+  const int d = C / heads;
+  const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int s0 = tile * PT, np = min(PT, S - s0);
+  float* sC = sh;            // [d][d]
+  float* sQ = sh + d * d;    // [PT][d]
+  const float* cg = ctx + ((long)n * heads + h) * d * d;
+  for (int i = threadIdx.x; i < d * d; i += blockDim.x) sC[i] = cg[i];
+  for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
+    const int s = i / d, c = i % d;
+    sQ[i] = to_f32(qkv[((long)n * S + s0 + s) * ld + C + h * d + c]);
+  }
+  __syncthreads();
+  if (threadIdx.x < np) {
+    float* q = sQ + threadIdx.x * d;
+    float mx = -INFINITY;
+    for (int c = 0; c < d; ++c) mx = fmaxf(mx, q[c]);
+    float sum = 0.f;
+    for (int c = 0; c < d; ++c) {
+      q[c] = __expf(q[c] - mx);
+      sum += q[c];
+    }
+    const float inv = 1.f / sum;
+    for (int c = 0; c < d; ++c) q[c] *= inv;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
+    const int s = i / d, cp = i % d;
+    float acc = 0.f;
+    for (int c = 0; c < d; ++c) acc += sC[c * d + cp] * sQ[s * d + c];
+    att[((long)n * S + s0 + s) * ldo + h * d + cp] = from_f32<T>(acc);
+  }
+}
+
+// ------------------------------------------------------------ apply bwd --
+// dQ (into dqkv Q slot) and partial dctx per tile: parts[n][tile][h][d][d]
+template <typename T>
+__global__ void apply_bwd_kernel(const T* __restrict__ qkv, int ld, int S, int C, int heads,
+                                 const float* __restrict__ ctx, const T* __restrict__ datt,
+                                 int ldd, T* __restrict__ dqkv, int ldq, int ntiles,
+                                 float* __restrict__ parts) {
+  extern __shared__ float sh[];
+  const int d = C / heads;
+  const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int s0 = tile * PT, np = min(PT, S - s0);
+  float* sC = sh;                 // [d][d]
+  float* sQ = sC + d * d;         // [PT][d]  softmaxed q
+  float* sG = sQ + PT * d;        // [PT][d]  datt
+  float* sD = sG + PT * d;        // [PT][d]  dQs
+  const float* cg = ctx + ((long)n * heads + h) * d * d;
+  for (int i = threadIdx.x; i < d * d; i += blockDim.x) sC[i] = cg[i];
+  for (int i = threadIdx.x; i < PT * d; i += blockDim.x) {
+    const int s = i / d, c = i % d;
+    if (s < np) {
+      const long row = (long)n * S + s0 + s;
+      sQ[i] = to_f32(qkv[row * ld + C + h * d + c]);
+      sG[i] = to_f32(datt[row * ldd + h * d + c]);
+    } else {
+      sQ[i] = 0.f;
+      sG[i] = 0.f;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < np) {
+    float* q = sQ + threadIdx.x * d;
+    float mx = -INFINITY;
+    for (int c = 0; c < d; ++c) mx = fmaxf(mx, q[c]);
+    float sum = 0.f;
+    for (int c = 0; c < d; ++c) {
+      q[c] = __expf(q[c] - mx);
+      sum += q[c];
+    }
+    const float inv = 1.f / sum;
+    for (int c = 0; c < d; ++c) q[c] *= inv;
+  }
+  __syncthreads();
+  // dQs[s][c] = sum_c' ctx[c][c'] * datt[s][c']
+  for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
+    const int s = i / d, c = i % d;
+    float acc = 0.f;
+    for (int cp = 0; cp < d; ++cp) acc += sC[c * d + cp] * sG[s * d + cp];
+    sD[i] = acc;
+  }
+  // dctx partial[c][c'] = sum_s qs[s][c] * datt[s][c']
+  float* out = parts + (((long)n * ntiles + tile) * heads + h) * d * d;
+  for (int o = threadIdx.x; o < d * d; o += blockDim.x) {
+    const int c = o / d, cp = o % d;
+    float acc = 0.f;
+    for (int s = 0; s < np; ++s) acc += sQ[s * d + c] * sG[s * d + cp];
+    out[o] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < np) {
+    const int s = threadIdx.x;
+    float dot = 0.f;
+    for (int c = 0; c < d; ++c) dot += sQ[s * d + c] * sD[s * d + c];
+    const long row = (long)n * S + s0 + s;
+    for (int c = 0; c < d; ++c)
+      dqkv[row * ldq + C + h * d + c] = from_f32<T>(sQ[s * d + c] * (sD[s * d + c] - dot));
+  }
+}
+
+// ---------------------------------------------------------------- kv bwd --
+// dV (into dqkv V slot), dKs (f32 scratch [m][C]) and partial r[c] = sum_s Ks*dKs
+template <typename T>
+__global__ void kv_bwd_kernel(const T* __restrict__ qkv, int ld, int S, int C, int heads,
+                              const float* __restrict__ kmax, const float* __restrict__ ksum,
+                              const float* __restrict__ dctx, T* __restrict__ dqkv, int ldq,
+                              float* __restrict__ dks, int ntiles, float* __restrict__ parts) {
+  extern __shared__ float sh[];
+  const int d = C / heads;
+  const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int s0 = tile * PT, np = min(PT, S - s0);
+  float* sC = sh;             // dctx [d][d]
+  float* sK = sC + d * d;     // Ks [PT][d]
+  float* sV = sK + PT * d;    // V  [PT][d]
+  float* sP = sV + PT * d;    // Ks * dKs [PT][d]
+  const float* cg = dctx + ((long)n * heads + h) * d * d;
+  for (int i = threadIdx.x; i < d * d; i += blockDim.x) sC[i] = cg[i];
+  for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
+    const int s = i / d, c = i % d;
+    const long row = ((long)n * S + s0 + s) * ld;
+    const int ch = h * d + c;
+    sK[i] = __expf(to_f32(qkv[row + ch]) - kmax[n * C + ch]) / ksum[n * C + ch];
+    sV[i] = to_f32(qkv[row + 2 * C + ch]);
+  }
+  __syncthreads();
+  // each thread handles elements (s, c); accumulate r for its channel
+  for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
+    const int s = i / d, c = i % d;
+    float g = 0.f, dv = 0.f;
+    for (int cp = 0; cp < d; ++cp) {
+      g += sC[c * d + cp] * sV[s * d + cp];    // dKs[s][c]
+      dv += sK[s * d + cp] * sC[cp * d + c];   // dV[s][c]
+    }
+    const long row = (long)n * S + s0 + s;
+    dks[row * C + h * d + c] = g;
+    dqkv[row * ldq + 2 * C + h * d + c] = from_f32<T>(dv);
+    sP[i] = sK[i] * g;
+  }
+  __syncthreads();
+  float* out = parts + (((long)n * ntiles + tile) * C) + h * d;
+  for (int c = threadIdx.x; c < d; c += blockDim.x) {
+    float t = 0.f;
+    for (int s = 0; s < np; ++s) t += sP[s * d + c];
+    out[c] = t;
+  }
+}
+
+template <typename T>
+__global__ void k_bwd_kernel(const T* __restrict__ qkv, int ld, long M, int S, int C,
+                             const float* __restrict__ kmax, const float* __restrict__ ksum,
+                             const float* __restrict__ dks, const float* __restrict__ r,
+                             T* __restrict__ dqkv, int ldq) {
+  const long total = M * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long m = i / C;
+    const int c = i % C;
+    const int n = m / S;
+    const float ks = __expf(to_f32(qkv[m * ld + c]) - kmax[n * C + c]) / ksum[n * C + c];
+    dqkv[m * ldq + c] = from_f32<T>(ks * (dks[i] - r[n * C + c]));
+  }
+}
+
+inline int grid_for(long n) {
+  long b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+inline int ctx_chunk(int d) {  // keeps the ctx kernel's LDS <= 33 KB
+  int c = 4096 / d;
+  if (c > 1024) c = 1024;
+  return c;
+}
+
+}  // namespace
+
+extern "C" {
+
+// workspace sizes (floats)
+long um_attn_ws_kstats(int N, int S, int C) {
+  return (long)N * ceil_div(S, KS_CHUNK) * C * 2;
+}
+long um_attn_ws_ctx(int N, int S, int C, int heads) {
+  const int d = C / heads;
+  return (long)N * ceil_div(S, ctx_chunk(d)) * heads * d * d;
+}
+long um_attn_ws_tiles(int N, int S, int C, int heads) {
+  const int d = C / heads;
+  const long a = (long)N * ceil_div(S, PT) * heads * d * d;
+  const long b = (long)N * ceil_div(S, PT) * C;
+  return a > b ? a : b;
+}
+
+int um_attn_fwd(int dtype, int N, int S, int C, int heads, const void* qkv, int ld,
+                float* kmax, float* ksum, float* ctx, float* ws, void* att, int ldo,
+                hipStream_t st) {
+  UM_CHECK_ARG(C % heads == 0, "um_attn_fwd: C %% heads");
+  const int d = C / heads;
+  UM_CHECK_ARG(d <= 64, "um_attn_fwd: head dim %d > 64", d);
+  const int nks = ceil_div(S, KS_CHUNK);
+  const int cch = ctx_chunk(d);
+  const int nctx = ceil_div(S, cch);
+  if (dtype == UM_BF16) {
+    hipLaunchKernelGGL(kstats_kernel<bf16_t>, dim3(nks, N), dim3(256), 0, st,
+                       (const bf16_t*)qkv, ld, S, C, ws, nks);
+  } else {
+    hipLaunchKernelGGL(kstats_kernel<float>, dim3(nks, N), dim3(256), 0, st, (const float*)qkv,
+                       ld, S, C, ws, nks);
+  }
+  hipLaunchKernelGGL(kstats_combine_kernel, dim3(ceil_div(N * C, 256)), dim3(256), 0, st, ws, N,
+                     nks, C, kmax, ksum);
+  const size_t shm_ctx = (2 * (size_t)cch * d + 256) * sizeof(float);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(ctx_kernel<bf16_t>, dim3(nctx, heads, N), dim3(256), shm_ctx, st,
+                       (const bf16_t*)qkv, ld, S, C, heads, kmax, ksum, cch, nctx, ws);
+  else
+    hipLaunchKernelGGL(ctx_kernel<float>, dim3(nctx, heads, N), dim3(256), shm_ctx, st,
+                       (const float*)qkv, ld, S, C, heads, kmax, ksum, cch, nctx, ws);
+  const int L = heads * d * d;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div((long)N * L, 256)), dim3(256), 0, st, ws, N,
+                     nctx, L, ctx);
+  const size_t shm_ap = ((size_t)d * d + PT * d) * sizeof(float);
+  const dim3 g(ceil_div(S, PT), heads, N);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(apply_kernel<bf16_t>, g, dim3(256), shm_ap, st, (const bf16_t*)qkv, ld, S,
+                       C, heads, ctx, (bf16_t*)att, ldo);
+  else
+    hipLaunchKernelGGL(apply_kernel<float>, g, dim3(256), shm_ap, st, (const float*)qkv, ld, S, C,
+                       heads, ctx, (float*)att, ldo);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+// dqkv [M][3C] is fully written.  dks_ws: f32 [M][C]; ws: um_attn_ws_tiles floats;
+// dctx: f32 [N][heads][d][d]; r: f32 [N][C]
+int um_attn_bwd(int dtype, int N, int S, int C, int heads, const void* qkv, int ld,
+                const float* kmax, const float* ksum, const float* ctx, const void* datt,
+                int ldd, void* dqkv, int ldq, float* dks_ws, float* ws, float* dctx, float* r,
+                hipStream_t st) {
+  const int d = C / heads;
+  UM_CHECK_ARG(d <= 64 && C % heads == 0, "um_attn_bwd: head dim");
+  const int nt = ceil_div(S, PT);
+  const dim3 g(nt, heads, N);
+  const size_t shm_a = ((size_t)d * d + 3 * PT * d) * sizeof(float);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(apply_bwd_kernel<bf16_t>, g, dim3(256), shm_a, st, (const bf16_t*)qkv, ld,
+                       S, C, heads, ctx, (const bf16_t*)datt, ldd, (bf16_t*)dqkv, ldq, nt, ws);
+  else
+    hipLaunchKernelGGL(apply_bwd_kernel<float>, g, dim3(256), shm_a, st, (const float*)qkv, ld, S,
+                       C, heads, ctx, (const float*)datt, ldd, (float*)dqkv, ldq, nt, ws);
+  const int L = heads * d * d;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div((long)N * L, 256)), dim3(256), 0, st, ws, N,
+                     nt, L, dctx);
+  const size_t shm_k = ((size_t)d * d + 3 * PT * d) * sizeof(float);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(kv_bwd_kernel<bf16_t>, g, dim3(256), shm_k, st, (const bf16_t*)qkv, ld, S,
+                       C, heads, kmax, ksum, dctx, (bf16_t*)dqkv, ldq, dks_ws, nt, ws);
+  else
+    hipLaunchKernelGGL(kv_bwd_kernel<float>, g, dim3(256), shm_k, st, (const float*)qkv, ld, S, C,
+                       heads, kmax, ksum, dctx, (float*)dqkv, ldq, dks_ws, nt, ws);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div((long)N * C, 256)), dim3(256), 0, st, ws, N,
+                     nt, C, r);
+  const long M = (long)N * S;
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(k_bwd_kernel<bf16_t>, dim3(grid_for(M * C)), dim3(256), 0, st,
+                       (const bf16_t*)qkv, ld, M, S, C, kmax, ksum, dks_ws, r, (bf16_t*)dqkv, ldq);
+  else
+    hipLaunchKernelGGL(k_bwd_kernel<float>, dim3(grid_for(M * C)), dim3(256), 0, st,
+                       (const float*)qkv, ld, M, S, C, kmax, ksum, dks_ws, r, (float*)dqkv, ldq);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+}  // extern "C"

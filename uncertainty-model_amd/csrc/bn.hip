@@ -1,0 +1,304 @@
+// Training-mode BatchNorm2d + ELU for NHWC activations, split in the phases a
+// data-parallel (SyncBN) step needs:
+//   forward : conv epilogue partial sums -> um_bn_stats_reduce (f64 per channel)
+//             -> [optional all-reduce by the host over RCCL]
+//             -> um_bn_coeffs (mean/invstd/scale/shift + running-stat update)
+//             -> um_bn_elu_fwd (a = ELU(y*scale + shift)), or fused consumers
+//   backward: um_bn_elu_bwd_reduce (sum dz, sum dz*xhat) -> um_bn_stats_reduce
+//             -> [all-reduce] -> um_bn_bwd_coeffs (dgamma/dbeta + dx coeffs)
+//             -> um_bn_elu_bwd_apply (dy)
+// Semantics follow torch.nn.BatchNorm2d (reference model/layers/encoder.py:43,
+// model/layers/decoder.py:82): biased variance for normalisation, unbiased
+// for running_var, eps 1e-5, momentum 0.1.  ELU alpha = 1 (nn.ELU, reference
+// model/layers/encoder.py:44, decoder.py:84).
+#include "common.h"
+
+namespace {
+
+__global__ void stats_reduce_kernel(const float* __restrict__ parts, int nparts, int C,
+                                    double* __restrict__ out) {
+  // out[c][0..1] = sum_p parts[p][c][0..1]; one wave per channel
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int p = lane; p < nparts; p += 64) {
+    s += parts[((long)p * C + c) * 2];
+    q += parts[((long)p * C + c) * 2 + 1];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    q += __shfl_xor(q, o, 64);
+  }
+  if (lane == 0) {
+    out[c * 2] = s;
+    out[c * 2 + 1] = q;
+  }
+}
+
+__global__ void coeffs_kernel(const double* __restrict__ st, double count, int C,
+                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                              float eps, float momentum, float* running_mean, float* running_var,
+                              long long* nbt, float* __restrict__ mean_out,
+                              float* __restrict__ invstd_out, float* __restrict__ scale_out,
+                              float* __restrict__ shift_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt != nullptr) *nbt += 1;
+  if (c >= C) return;
+  const double mean = st[2 * c] / count;
+  double var = st[2 * c + 1] / count - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  scale_out[c] = g * invstd;
+  shift_out[c] = b - (float)mean * g * invstd;
+  if (running_mean != nullptr) {
+    const double unb = count > 1 ? var * count / (count - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
+template <typename T>
+__global__ void bn_elu_fwd_kernel(const T* __restrict__ y, int ldy, long M, int C,
+                                  const float* __restrict__ scale, const float* __restrict__ shift,
+                                  T* __restrict__ a, int lda, int apply_elu) {
+  // 8 channels per thread (C % 8 == 0)
+  const int cg = C / 8;
+  const long total = M * cg;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long m = i / cg;
+    const int c = (int)(i - m * cg) * 8;
+    float v[8];
+    load8(y + m * ldy + c, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float z = v[e] * scale[c + e] + shift[c + e];
+      v[e] = apply_elu ? eluf_(z) : z;
+    }
+    store8(a + m * lda + c, v);
+  }
+}
+
+// Backward reduce: dz = (da + add[n][c]) * ELU'(z), z = y*scale + shift,
+// xhat = (y - mean) * invstd; partial sums per block [blk][C][2].
+template <typename T>
+__global__ void bn_elu_bwd_reduce_kernel(const T* __restrict__ da, int ldda, const T* __restrict__ y,
+                                         int ldy, long M, int C, long HW,
+                                         const float* __restrict__ mean,
+                                         const float* __restrict__ invstd,
+                                         const float* __restrict__ scale,
+                                         const float* __restrict__ shift,
+                                         const float* __restrict__ add_nc, int apply_elu,
+                                         float* __restrict__ parts, int rows_per_block) {
+  // block: 256 threads = (256/CG) row lanes x CG channel-groups of 8, looped
+  extern __shared__ float red[];  // [256][2*8]
+  const int cg = C / 8;
+  const long m0 = (long)blockIdx.x * rows_per_block;
+  const long m1 = min(M, m0 + rows_per_block);
+  for (int g0 = 0; g0 < cg; g0 += 32) {
+    const int g = g0 + (threadIdx.x & 31);
+    const int rl = threadIdx.x >> 5;  // 8 row lanes
+    float s[8], q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
+    if (g < cg) {
+      const int c = g * 8;
+      float mu[8], is[8], sc[8], sh[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        mu[e] = mean[c + e]; is[e] = invstd[c + e]; sc[e] = scale[c + e]; sh[e] = shift[c + e];
+      }
+      for (long m = m0 + rl; m < m1; m += 8) {
+        float dv[8], yv[8];
+        load8(da + m * ldda + c, dv);
+        load8(y + m * ldy + c, yv);
+        const float* ad = add_nc ? add_nc + (m / HW) * C + c : nullptr;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float d = dv[e] + (ad ? ad[e] : 0.f);
+          if (apply_elu) {
+            const float z = yv[e] * sc[e] + sh[e];
+            d = z > 0.f ? d : d * __expf(z);
+          }
+          s[e] += d;
+          q[e] += d * (yv[e] - mu[e]) * is[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[threadIdx.x * 16 + e] = s[e];
+      red[threadIdx.x * 16 + 8 + e] = q[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < 32 && g < cg) {
+      for (int e = 0; e < 8; ++e) {
+        float ts = 0.f, tq = 0.f;
+        for (int r = 0; r < 8; ++r) {
+          ts += red[(r * 32 + threadIdx.x) * 16 + e];
+          tq += red[(r * 32 + threadIdx.x) * 16 + 8 + e];
+        }
+        float* o = parts + ((long)blockIdx.x * C + g * 8 + e) * 2;
+        o[0] = ts;
+        o[1] = tq;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void bwd_coeffs_kernel(const double* __restrict__ st, double count, int C,
+                                  const float* __restrict__ gamma,
+                                  const float* __restrict__ invstd,
+                                  const double* __restrict__ st_local, float* dgamma,
+                                  float* dbeta, int accumulate, float* __restrict__ k1,
+                                  float* __restrict__ k2, float* __restrict__ k3) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double sdz = st[2 * c], sdzx = st[2 * c + 1];
+  const float g = gamma ? gamma[c] : 1.f;
+  // dx = g*invstd*(dz - sdz/n - xhat*sdzx/n)
+  k1[c] = g * invstd[c];
+  k2[c] = (float)(sdz / count);
+  k3[c] = (float)(sdzx / count);
+  // parameter grads use the local (per-rank) sums, like torch SyncBatchNorm
+  const double* sl = st_local ? st_local : st;
+  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)sl[2 * c + 1];
+  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)sl[2 * c];
+}
+
+template <typename T>
+__global__ void bn_elu_bwd_apply_kernel(const T* __restrict__ da, int ldda,
+                                        const T* __restrict__ y, int ldy, long M, int C, long HW,
+                                        const float* __restrict__ mean,
+                                        const float* __restrict__ invstd,
+                                        const float* __restrict__ scale,
+                                        const float* __restrict__ shift,
+                                        const float* __restrict__ add_nc, int apply_elu,
+                                        const float* __restrict__ k1, const float* __restrict__ k2,
+                                        const float* __restrict__ k3, T* __restrict__ dy,
+                                        int lddy) {
+  const int cg = C / 8;
+  const long total = M * cg;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long m = i / cg;
+    const int c = (int)(i - m * cg) * 8;
+    float dv[8], yv[8], o[8];
+    load8(da + m * ldda + c, dv);
+    load8(y + m * ldy + c, yv);
+    const float* ad = add_nc ? add_nc + (m / HW) * C + c : nullptr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float d = dv[e] + (ad ? ad[e] : 0.f);
+      if (apply_elu) {
+        const float z = yv[e] * scale[c + e] + shift[c + e];
+        d = z > 0.f ? d : d * __expf(z);
+      }
+      const float xh = (yv[e] - mean[c + e]) * invstd[c + e];
+      o[e] = k1[c + e] * (d - k2[c + e] - xh * k3[c + e]);
+    }
+    store8(dy + m * lddy + c, o);
+  }
+}
+
+constexpr int BWD_ROWS = 512;
+
+inline int grid_for(long n) {
+  long b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int um_bn_stats_reduce(const float* parts, int nparts, int C, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(ceil_div(C, 4)), dim3(256), 0, st, parts, nparts,
+                     C, out);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_bn_coeffs(const double* stats, double count, int C, const float* gamma, const float* beta,
+                 float eps, float momentum, float* running_mean, float* running_var,
+                 long long* num_batches_tracked, float* mean, float* invstd, float* scale,
+                 float* shift, hipStream_t st) {
+  hipLaunchKernelGGL(coeffs_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, stats, count, C,
+                     gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked,
+                     mean, invstd, scale, shift);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
+                  const float* shift, void* a, int lda, int apply_elu, hipStream_t st) {
+  UM_CHECK_ARG(C % 8 == 0 && ldy % 8 == 0 && lda % 8 == 0, "um_bn_elu_fwd: C/ld not multiple of 8");
+  const int g = grid_for(M * C / 8);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)y,
+                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu);
+  else
+    hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)y, ldy,
+                       M, C, scale, shift, (float*)a, lda, apply_elu);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_bn_bwd_parts(long M) { return (int)((M + BWD_ROWS - 1) / BWD_ROWS); }
+
+int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int ldda,
+                         const void* y, int ldy, const float* mean, const float* invstd,
+                         const float* scale, const float* shift, const float* add_nc,
+                         int apply_elu, float* parts, hipStream_t st) {
+  UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_reduce: C %% 8");
+  const int blocks = um_bn_bwd_parts(M);
+  const size_t shm = 256 * 16 * sizeof(float);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
+                       (const bf16_t*)da, ldda, (const bf16_t*)y, ldy, M, C, HW, mean, invstd,
+                       scale, shift, add_nc, apply_elu, parts, BWD_ROWS);
+  else
+    hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), shm, st,
+                       (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
+                       scale, shift, add_nc, apply_elu, parts, BWD_ROWS);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamma,
+                     const float* invstd, const double* stats_local, float* dgamma, float* dbeta,
+                     int accumulate, float* k1, float* k2, float* k3, hipStream_t st) {
+  hipLaunchKernelGGL(bwd_coeffs_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, stats, count, C,
+                     gamma, invstd, stats_local, dgamma, dbeta, accumulate, k1, k2, k3);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_bn_elu_bwd_apply(int dtype, long M, int C, long HW, const void* da, int ldda,
+                        const void* y, int ldy, const float* mean, const float* invstd,
+                        const float* scale, const float* shift, const float* add_nc,
+                        int apply_elu, const float* k1, const float* k2, const float* k3,
+                        void* dy, int lddy, hipStream_t st) {
+  UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_apply: C %% 8");
+  const int g = grid_for(M * C / 8);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, st,
+                       (const bf16_t*)da, ldda, (const bf16_t*)y, ldy, M, C, HW, mean, invstd,
+                       scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy);
+  else
+    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, st,
+                       (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
+                       scale, shift, add_nc, apply_elu, k1, k2, k3, (float*)dy, lddy);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+}  // extern "C"

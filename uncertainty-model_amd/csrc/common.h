@@ -1,0 +1,132 @@
+// Common device/host helpers for the umamd HIP library (gfx950 / CDNA4 only).
+//
+// Activations are NHWC ("channels-last") with an explicit pixel stride `ld`
+// (elements between consecutive pixels) so producers can write straight into
+// a channel slice of a wider buffer.  Element storage type is either f32 or
+// bf16 (UM_F32 / UM_BF16); all arithmetic is f32.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../include/umamd.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __hip_bfloat16 bf16_t;
+
+// ------------------------------------------------------------ error state --
+namespace umamd {
+void set_error(const char* fmt, ...);
+}  // namespace umamd
+
+#define UM_CHECK_ARG(cond, ...)                    \
+  do {                                             \
+    if (!(cond)) {                                 \
+      umamd::set_error(__VA_ARGS__);               \
+      return UM_ERR_ARG;                           \
+    }                                              \
+  } while (0)
+
+#define UM_LAUNCH_CHECK()                                               \
+  do {                                                                  \
+    hipError_t _e = hipGetLastError();                                  \
+    if (_e != hipSuccess) {                                             \
+      umamd::set_error("%s: %s", __func__, hipGetErrorString(_e));      \
+      return UM_ERR_HIP;                                                \
+    }                                                                   \
+  } while (0)
+
+// ------------------------------------------------------------ conversions --
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16_t x) { return __bfloat162float(x); }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float x) {
+  return __float2bfloat16(x);
+}
+
+// 8-element vector load/store (16 B for bf16, 32 B for f32) -> f32[8]
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void load8(const bf16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void store8(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  // round-to-nearest-even via the compiler's cvt (keeps NaN a NaN)
+  bf16_t x = __float2bfloat16(a), y = __float2bfloat16(b);
+  return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) |
+         ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float* v) {
+  uint4 u;
+  u.x = pack_bf16x2(v[0], v[1]);
+  u.y = pack_bf16x2(v[2], v[3]);
+  u.z = pack_bf16x2(v[4], v[5]);
+  u.w = pack_bf16x2(v[6], v[7]);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
+// raw 8-element copies (no conversion) used for LDS staging
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16_t> { uint4 v; };
+template <> struct Raw8<float> { uint4 a, b; };
+__device__ __forceinline__ void raw_load8(const bf16_t* p, Raw8<bf16_t>& r) {
+  r.v = *reinterpret_cast<const uint4*>(p);
+}
+__device__ __forceinline__ void raw_load8(const float* p, Raw8<float>& r) {
+  r.a = *reinterpret_cast<const uint4*>(p);
+  r.b = *reinterpret_cast<const uint4*>(p + 4);
+}
+__device__ __forceinline__ void raw_zero(Raw8<bf16_t>& r) { r.v = make_uint4(0, 0, 0, 0); }
+__device__ __forceinline__ void raw_zero(Raw8<float>& r) {
+  r.a = make_uint4(0, 0, 0, 0);
+  r.b = r.a;
+}
+__device__ __forceinline__ void raw_store8(bf16_t* p, const Raw8<bf16_t>& r) {
+  *reinterpret_cast<uint4*>(p) = r.v;
+}
+__device__ __forceinline__ void raw_store8(float* p, const Raw8<float>& r) {
+  *reinterpret_cast<uint4*>(p) = r.a;
+  *reinterpret_cast<uint4*>(p + 4) = r.b;
+}
+
+// ---------------------------------------------------------- wave helpers --
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float eluf_(float x) { return x > 0.f ? x : expm1f(x); }
+
+// reflect index for padding (|pad| < n), torch 'reflect' semantics
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  if (i < 0) i = -i;
+  if (i >= n) i = 2 * (n - 1) - i;
+  return i;
+}
+
+static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,694 @@
+// Implicit-GEMM convolutions on MFMA for gfx950 (CDNA4).
+//
+// One kernel template serves the forward conv and the data gradient:
+//   forward  : Y[m=(n,p,q)][k]  = sum_{(r,s,c)} X[n, p*st-pad+r, q*st-pad+s, c] * Wf[k][r][s][c]
+//   dgrad    : DX[m=(n,h,w)][c] = sum_{(r,s,k)} DY[src(n,h,w,r,s)][k] * WT[c][r][s][k]
+// where src() inverts the forward gather: the stride-2 parity filter and the
+// reflect-pad fold (a border pixel of X feeds two padded taps).
+// The weight gradient is a separate template whose operands are both
+// pixel-major, transposed into LDS.
+//
+// Tiles: BM x BN output, BK = 32 reduction step, 256 threads = 4 waves, each
+// wave a (BM/WM) x (BN/WN) sub-tile of 16x16 MFMA fragments.  LDS rows are
+// padded by 8 elements.  One LDS buffer + register prefetch of the next tile.
+//
+// bf16: v_mfma_f32_16x16x32_bf16 (lane l: A[l&15][8(l>>4)+j], j<8).
+// f32 : 8 x v_mfma_f32_16x16x4_f32 per BK step with the k-permutation
+//       "lane group g, element e -> k = 8g+e" on both operands (exact f32).
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 32;
+constexpr int LDK = BK + 8;  // padded LDS row (elements)
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+
+struct ConvArgs {
+  // "input" geometry of the GEMM A gather
+  int N, H, W, C, ldx;   // forward: X geometry.  dgrad: DX geometry (output)
+  int P, Q, K, ldy;      // forward: Y geometry.  dgrad: DY geometry (input)
+  int R, stride, pad, pad_mode;
+  const void* a_src;     // forward: X; dgrad: DY
+  const void* b_src;     // forward: Wf [K][RRC]; dgrad: WT [C][RRK]
+  const float* bias;
+  void* out;             // forward: Y; dgrad: DX
+  int ld_out;
+  int M, NC, KK;         // GEMM sizes: rows, cols, reduction
+  int epilogue, accumulate, out_f32;
+  float epi_scale;
+  const void* residual;
+  int ldr;
+  float* stats;
+};
+
+template <typename T> struct Frag;
+template <> struct Frag<bf16_t> { bf16x8_t v; };
+template <> struct Frag<float> { float v[8]; };
+
+__device__ __forceinline__ void lds_frag(const bf16_t* p, Frag<bf16_t>& f) {
+  f.v = *reinterpret_cast<const bf16x8_t*>(p);
+}
+__device__ __forceinline__ void lds_frag(const float* p, Frag<float>& f) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+  f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+}
+__device__ __forceinline__ void mfma(f32x4_t& acc, const Frag<bf16_t>& a, const Frag<bf16_t>& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mfma(f32x4_t& acc, const Frag<float>& a, const Frag<float>& b) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[e], b.v[e], acc, 0, 0, 0);
+}
+
+// add 8 raw elements into an f32 accumulator (used by the reflect fold)
+__device__ __forceinline__ void accum8(const bf16_t* p, float* v) {
+  float t[8];
+  load8(p, t);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] += t[i];
+}
+__device__ __forceinline__ void accum8(const float* p, float* v) {
+  float t[8];
+  load8(p, t);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] += t[i];
+}
+__device__ __forceinline__ void f32_to_raw(const float* v, Raw8<bf16_t>& r) {
+  r.v.x = pack_bf16x2(v[0], v[1]);
+  r.v.y = pack_bf16x2(v[2], v[3]);
+  r.v.z = pack_bf16x2(v[4], v[5]);
+  r.v.w = pack_bf16x2(v[6], v[7]);
+}
+__device__ __forceinline__ void f32_to_raw(const float* v, Raw8<float>& r) {
+  r.a = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                   __float_as_uint(v[3]));
+  r.b = make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]),
+                   __float_as_uint(v[7]));
+}
+
+// sources in [0, n) of a dgrad tap: forward used index r(o*st + tap - pad) = i
+__device__ __forceinline__ int dgrad_sources(int i, int tap, int n_in, int n_out, int st,
+                                             int pad, int reflect, int* srcs) {
+  int cnt = 0;
+  int cand[3];
+  int nc = 1;
+  cand[0] = i;
+  if (reflect) {
+    if (i >= 1 && i <= pad) cand[nc++] = -i;
+    if (i >= n_in - 1 - pad && i <= n_in - 2) cand[nc++] = 2 * (n_in - 1) - i;
+  }
+  for (int c = 0; c < nc; ++c) {
+    const int t = cand[c] + pad - tap;  // = o * st
+    if (t < 0) continue;
+    if (st == 2) {
+      if (t & 1) continue;
+      const int o = t >> 1;
+      if (o < n_out) srcs[cnt++] = o;
+    } else {
+      if (t < n_out) srcs[cnt++] = t;
+    }
+  }
+  return cnt;
+}
+
+template <typename T, int MODE, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  constexpr int A_CHUNKS = BM * (BK / 8);
+  constexpr int B_CHUNKS = BN * (BK / 8);
+  constexpr int A_PER = (A_CHUNKS + 255) / 256;
+  constexpr int B_PER = (B_CHUNKS + 255) / 256;
+  static_assert(WM * WN == 4, "4 waves");
+
+  __shared__ __attribute__((aligned(16))) T sA[BM * LDK];
+  __shared__ __attribute__((aligned(16))) T sB[BN * LDK];
+  __shared__ float sStat[WM][BN][2];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bm = blockIdx.x * BM;
+  const int bn = blockIdx.y * BN;
+
+  const T* __restrict__ asrc = reinterpret_cast<const T*>(a.a_src);
+  const T* __restrict__ bsrc = reinterpret_cast<const T*>(a.b_src);
+
+  // Per-thread A rows: decode pixel coordinates once.
+  int a_row[A_PER], a_kc[A_PER], a_n[A_PER], a_y[A_PER], a_x[A_PER];
+  bool a_ok[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int c = tid + i * 256;
+    a_row[i] = c / (BK / 8);
+    a_kc[i] = c % (BK / 8);
+    const int m = bm + a_row[i];
+    a_ok[i] = (c < A_CHUNKS) && (m < a.M);
+    const int mm = a_ok[i] ? m : 0;
+    if (MODE == MODE_FWD) {
+      const int pq = a.P * a.Q;
+      a_n[i] = mm / pq;
+      const int r = mm - a_n[i] * pq;
+      const int p = r / a.Q, q = r - (r / a.Q) * a.Q;
+      a_y[i] = p * a.stride - a.pad;
+      a_x[i] = q * a.stride - a.pad;
+    } else {
+      const int hw = a.H * a.W;
+      a_n[i] = mm / hw;
+      const int r = mm - a_n[i] * hw;
+      a_y[i] = r / a.W;
+      a_x[i] = r - a_y[i] * a.W;
+    }
+  }
+  int b_row[B_PER], b_kc[B_PER];
+  bool b_ok[B_PER];
+#pragma unroll
+  for (int i = 0; i < B_PER; ++i) {
+    const int c = tid + i * 256;
+    b_row[i] = c / (BK / 8);
+    b_kc[i] = c % (BK / 8);
+    b_ok[i] = (c < B_CHUNKS) && (bn + b_row[i] < a.NC);
+  }
+
+  // channel count of the gathered operand (per tap)
+  const int CH = (MODE == MODE_FWD) ? a.C : a.K;
+
+  Raw8<T> ra[A_PER], rb[B_PER];
+
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int kidx = k0 + a_kc[i] * 8;
+      raw_zero(ra[i]);
+      if (!a_ok[i] || kidx >= a.KK) continue;
+      const int tap = kidx / CH;
+      const int ch = kidx - tap * CH;
+      const int r = tap / a.R, s = tap - (tap / a.R) * a.R;
+      if (MODE == MODE_FWD) {
+        int yy = a_y[i] + r, xx = a_x[i] + s;
+        if (a.pad_mode == UM_PAD_REFLECT) {
+          yy = reflect_idx(yy, a.H);
+          xx = reflect_idx(xx, a.W);
+        } else if (yy < 0 || yy >= a.H || xx < 0 || xx >= a.W) {
+          continue;
+        }
+        raw_load8(asrc + ((long)(a_n[i] * a.H + yy) * a.W + xx) * a.ldx + ch, ra[i]);
+      } else {
+        int sy[3], sx[3];
+        const bool refl = a.pad_mode == UM_PAD_REFLECT;
+        const int ny = dgrad_sources(a_y[i], r, a.H, a.P, a.stride, a.pad, refl, sy);
+        const int nx = dgrad_sources(a_x[i], s, a.W, a.Q, a.stride, a.pad, refl, sx);
+        if (ny == 0 || nx == 0) continue;
+        if (ny == 1 && nx == 1) {
+          raw_load8(asrc + ((long)(a_n[i] * a.P + sy[0]) * a.Q + sx[0]) * a.ldy + ch, ra[i]);
+        } else {
+          float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          for (int u = 0; u < ny; ++u)
+            for (int w = 0; w < nx; ++w)
+              accum8(asrc + ((long)(a_n[i] * a.P + sy[u]) * a.Q + sx[w]) * a.ldy + ch, v);
+          f32_to_raw(v, ra[i]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int kidx = k0 + b_kc[i] * 8;
+      raw_zero(rb[i]);
+      if (!b_ok[i] || kidx >= a.KK) continue;
+      raw_load8(bsrc + (long)(bn + b_row[i]) * a.KK + kidx, rb[i]);
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (a.KK + BK - 1) / BK;
+  load_tiles(0);
+  const int frow = lane & 15;
+  const int fk = (lane >> 4) * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i)
+      if (tid + i * 256 < A_CHUNKS) raw_store8(&sA[a_row[i] * LDK + a_kc[i] * 8], ra[i]);
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i)
+      if (tid + i * 256 < B_CHUNKS) raw_store8(&sB[b_row[i] * LDK + b_kc[i] * 8], rb[i]);
+    __syncthreads();
+    if (kt + 1 < nk) load_tiles((kt + 1) * BK);
+    Frag<T> fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      lds_frag(&sA[(wm * (BM / WM) + i * 16 + frow) * LDK + fk], fa[i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      lds_frag(&sB[(wn * (BN / WN) + j * 16 + frow) * LDK + fk], fb[j]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) mfma(acc[i][j], fa[i], fb[j]);
+  }
+
+  // ------------------------------------------------------------- epilogue --
+  const int col_l = lane & 15;
+  const int row_g = (lane >> 4) * 4;
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = bn + wn * (BN / WN) + j * 16 + col_l;
+    const bool nok = n < a.NC;
+    const float bv = (a.bias != nullptr && nok) ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm + wm * (BM / WM) + i * 16 + row_g + r;
+        if (!nok || m >= a.M) continue;
+        float v = acc[i][j][r] + bv;
+        const long off = (long)m * a.ld_out + n;
+        if (a.epilogue == UM_EPI_RESIDUAL)
+          v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
+        if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
+        if (a.out_f32) {
+          float* o = reinterpret_cast<float*>(a.out) + off;
+          if (a.accumulate) v += *o;
+          *o = v;
+        } else {
+          T* o = reinterpret_cast<T*>(a.out) + off;
+          if (a.accumulate) v += to_f32(*o);
+          *o = from_f32<T>(v);
+        }
+        csum[j] += v;
+        csq[j] += v * v;
+      }
+    }
+  }
+  if (a.epilogue == UM_EPI_STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s = csum[j], q = csq[j];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        sStat[wm][wn * (BN / WN) + j * 16 + lane][0] = s;
+        sStat[wm][wn * (BN / WN) + j * 16 + lane][1] = q;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      const int n = bn + c;
+      if (n >= a.NC) continue;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) { s += sStat[w][c][0]; q += sStat[w][c][1]; }
+      float* out = a.stats + ((long)blockIdx.x * a.NC + n) * 2;
+      out[0] = s;
+      out[1] = q;
+    }
+  }
+}
+
+template <typename T, int MODE, int BM, int BN, int WM, int WN>
+int launch_conv(const ConvArgs& a, hipStream_t st) {
+  dim3 grid(ceil_div(a.M, BM), ceil_div(a.NC, BN));
+  hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, WM, WN>), grid, dim3(256), 0, st, a);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+constexpr int STATS_BM = 128;  // fixed M tile whenever stats are requested
+
+template <typename T, int MODE>
+int dispatch_conv(const ConvArgs& a, hipStream_t st) {
+  if (a.epilogue == UM_EPI_STATS) {
+    // BM fixed to STATS_BM so the partial-row count is shape-independent
+    if (a.NC <= 32) return launch_conv<T, MODE, 128, 32, 4, 1>(a, st);
+    if (a.NC <= 64) return launch_conv<T, MODE, 128, 64, 2, 2>(a, st);
+    return launch_conv<T, MODE, 128, 128, 2, 2>(a, st);
+  }
+  if (a.NC <= 16) return launch_conv<T, MODE, 256, 16, 4, 1>(a, st);
+  if (a.NC <= 32) return launch_conv<T, MODE, 256, 32, 4, 1>(a, st);
+  const long big = (long)ceil_div(a.M, 128) * ceil_div(a.NC, 128);
+  if (a.NC <= 64 || big < 512) {
+    const long mid = (long)ceil_div(a.M, 128) * ceil_div(a.NC, 64);
+    if (mid >= 512) return launch_conv<T, MODE, 128, 64, 2, 2>(a, st);
+    return launch_conv<T, MODE, 64, 64, 2, 2>(a, st);
+  }
+  return launch_conv<T, MODE, 128, 128, 2, 2>(a, st);
+}
+
+// ------------------------------------------------------------ weight grad --
+// C[k][j] = sum_m DY[m][k] * X[m][j], j = (r, s, c); both operands are
+// staged transposed into LDS ([row][m]) so MFMA fragments read 8 consecutive m.
+struct WgradArgs {
+  int N, H, W, C, ldx, K, R, stride, pad, pad_mode, P, Q, ldy;
+  const void* x;
+  const void* dy;
+  float* slabs;
+  int M, RRC, m_per_split;
+};
+
+template <typename T, int BM, int BN>
+__global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int A_CH = BK * BM / 8;  // dy chunks: 32 m x BM/8 k-chunks
+  constexpr int B_CH = BK * BN / 8;
+  constexpr int A_PER = (A_CH + 255) / 256, B_PER = (B_CH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) T sA[BM * LDK];
+  __shared__ __attribute__((aligned(16))) T sB[BN * LDK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bk = blockIdx.x * BM;  // output-channel tile
+  const int bj = blockIdx.y * BN;  // (r,s,c) tile
+  const int m_begin = blockIdx.z * a.m_per_split;
+  const int m_end = min(a.M, m_begin + a.m_per_split);
+  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ DY = reinterpret_cast<const T*>(a.dy);
+
+  // fixed column chunks per thread
+  int a_m[A_PER], a_c[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int c = tid + i * 256;
+    a_m[i] = c / (BM / 8);
+    a_c[i] = (c % (BM / 8)) * 8;
+  }
+  int b_m[B_PER], b_j[B_PER], b_r[B_PER], b_s[B_PER], b_ch[B_PER];
+  bool b_ok[B_PER];
+#pragma unroll
+  for (int i = 0; i < B_PER; ++i) {
+    const int c = tid + i * 256;
+    b_m[i] = c / (BN / 8);
+    b_j[i] = (c % (BN / 8)) * 8;
+    const int j = bj + b_j[i];
+    b_ok[i] = (c < B_CH) && (j < a.RRC);
+    const int jj = b_ok[i] ? j : 0;
+    const int tap = jj / a.C;
+    b_ch[i] = jj - tap * a.C;
+    b_r[i] = tap / a.R;
+    b_s[i] = tap - b_r[i] * a.R;
+  }
+
+  float va[A_PER][8], vb[B_PER][8];
+  const int pq = a.P * a.Q;
+  auto load_tiles = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int m = m0 + a_m[i];
+      const int k = bk + a_c[i];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) va[i][e] = 0.f;
+      if (tid + i * 256 < A_CH && m < m_end && k < a.K) load8(DY + (long)m * a.ldy + k, va[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int m = m0 + b_m[i];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vb[i][e] = 0.f;
+      if (!b_ok[i] || m >= m_end) continue;
+      const int n = m / pq;
+      const int rr = m - n * pq;
+      const int p = rr / a.Q, q = rr - (rr / a.Q) * a.Q;
+      int yy = p * a.stride - a.pad + b_r[i], xx = q * a.stride - a.pad + b_s[i];
+      if (a.pad_mode == UM_PAD_REFLECT) {
+        yy = reflect_idx(yy, a.H);
+        xx = reflect_idx(xx, a.W);
+      } else if (yy < 0 || yy >= a.H || xx < 0 || xx >= a.W) {
+        continue;
+      }
+      load8(X + ((long)(n * a.H + yy) * a.W + xx) * a.ldx + b_ch[i], vb[i]);
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fk = (lane >> 4) * 8;
+  if (m_begin < m_end) load_tiles(m_begin);
+  for (int m0 = m_begin; m0 < m_end; m0 += BK) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i)
+      if (tid + i * 256 < A_CH)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sA[(a_c[i] + e) * LDK + a_m[i]] = from_f32<T>(va[i][e]);
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i)
+      if (tid + i * 256 < B_CH)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sB[(b_j[i] + e) * LDK + b_m[i]] = from_f32<T>(vb[i][e]);
+    __syncthreads();
+    if (m0 + BK < m_end) load_tiles(m0 + BK);
+    Frag<T> fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) lds_frag(&sA[(wm * (BM / WM) + i * 16 + frow) * LDK + fk], fa[i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) lds_frag(&sB[(wn * (BN / WN) + j * 16 + frow) * LDK + fk], fb[j]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) mfma(acc[i][j], fa[i], fb[j]);
+  }
+
+  float* out = a.slabs + (long)blockIdx.z * a.K * a.RRC;
+  const int col_l = lane & 15, row_g = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = bk + wm * (BM / WM) + i * 16 + row_g + r;
+        const int jj = bj + wn * (BN / WN) + j * 16 + col_l;
+        if (k < a.K && jj < a.RRC) out[(long)k * a.RRC + jj] = acc[i][j][r];
+      }
+}
+
+template <typename T, int BM, int BN>
+int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
+  dim3 grid(ceil_div(a.K, BM), ceil_div(a.RRC, BN), splits);
+  hipLaunchKernelGGL((wgrad_kernel<T, BM, BN>), grid, dim3(256), 0, st, a);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int splits, int K, int Kreal,
+                                    int R, int C, int Creal, float* __restrict__ dw,
+                                    int accumulate) {
+  // dw[k][c][r][s]  <-  sum_z slabs[z][k][(r*R+s)*C + c]   (slabs hold K >= Kreal rows)
+  const long total = (long)Kreal * Creal * R * R;
+  const long RRC = (long)R * R * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int s = i % R;
+    const int r = (i / R) % R;
+    const int c = (i / (R * R)) % Creal;
+    const int k = i / ((long)R * R * Creal);
+    const long src = (long)k * RRC + (r * R + s) * C + c;
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += slabs[z * (long)K * RRC + src];
+    dw[i] = accumulate ? dw[i] + v : v;
+  }
+}
+
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ w, int K, int Creal, int R, int C,
+                                   T* __restrict__ wf, T* __restrict__ wT, int ldT) {
+  const long total = (long)K * R * R * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    // i indexes wf [K][R][R][C]
+    const int c = i % C;
+    const int s = (i / C) % R;
+    const int r = (i / ((long)C * R)) % R;
+    const int k = i / ((long)C * R * R);
+    const float v = c < Creal ? w[(((long)k * Creal + c) * R + r) * R + s] : 0.f;
+    if (wf) wf[i] = from_f32<T>(v);
+    if (wT) wT[((long)c * R * R + r * R + s) * ldT + k] = from_f32<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ y, int M, int C, int ld,
+                              float* __restrict__ parts, int rows_per_block) {
+  // block: 256 threads = 8 row lanes x 32 channel lanes per channel tile
+  const int m0 = blockIdx.x * rows_per_block;
+  const int m1 = min(M, m0 + rows_per_block);
+  for (int c0 = 0; c0 < C; c0 += 32) {
+    const int c = c0 + (threadIdx.x & 31);
+    float s = 0.f;
+    if (c < C)
+      for (int m = m0 + (threadIdx.x >> 5); m < m1; m += 8) s += to_f32(y[(long)m * ld + c]);
+    __shared__ float red[8][33];
+    red[threadIdx.x >> 5][threadIdx.x & 31] = s;
+    __syncthreads();
+    if (threadIdx.x < 32 && c < C) {
+      float t = 0.f;
+      for (int r = 0; r < 8; ++r) t += red[r][threadIdx.x];
+      parts[(long)blockIdx.x * C + c] = t;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void reduce_rows_kernel(const float* __restrict__ p, int parts, int C, int stride,
+                                   float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int r = 0; r < parts; ++r) s += p[(long)r * stride + c];
+  out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+constexpr int COLSUM_ROWS = 1024;
+
+}  // namespace
+
+extern "C" {
+
+int um_conv_stats_parts(int M, int K) {
+  (void)K;
+  return ceil_div(M, STATS_BM);
+}
+
+int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x, const void* wf,
+                  const float* bias, int K, int R, int stride, int pad, int pad_mode, int P,
+                  int Q, int ydtype, void* y, int ldy, int epilogue, float epi_scale,
+                  const void* residual, int ldr, float* stats, hipStream_t st) {
+  UM_CHECK_ARG(C % 8 == 0 && ldx % 8 == 0, "um_conv2d_fwd: C (%d) and ldx (%d) must be multiples of 8", C, ldx);
+  UM_CHECK_ARG(stride == 1 || stride == 2, "um_conv2d_fwd: stride %d", stride);
+  UM_CHECK_ARG(P == (H + 2 * pad - R) / stride + 1 && Q == (W + 2 * pad - R) / stride + 1,
+               "um_conv2d_fwd: output size mismatch");
+  UM_CHECK_ARG(pad_mode == UM_PAD_ZERO || pad < H, "um_conv2d_fwd: reflect pad too large");
+  UM_CHECK_ARG(epilogue != UM_EPI_STATS || stats != nullptr, "um_conv2d_fwd: stats buffer missing");
+  UM_CHECK_ARG(epilogue != UM_EPI_RESIDUAL || residual != nullptr, "um_conv2d_fwd: residual missing");
+  ConvArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx;
+  a.P = P; a.Q = Q; a.K = K; a.ldy = ldy;
+  a.R = R; a.stride = stride; a.pad = pad; a.pad_mode = pad_mode;
+  a.a_src = x; a.b_src = wf; a.bias = bias; a.out = y; a.ld_out = ldy;
+  a.M = N * P * Q; a.NC = K; a.KK = R * R * C;
+  a.epilogue = epilogue; a.accumulate = 0;
+  a.out_f32 = (ydtype == UM_F32);
+  a.epi_scale = epi_scale; a.residual = residual; a.ldr = ldr; a.stats = stats;
+  UM_CHECK_ARG(ydtype == dtype || epilogue == UM_EPI_SIGMOID_SCALE || dtype == UM_F32,
+               "um_conv2d_fwd: ydtype must match dtype");
+  if (a.M == 0) return UM_OK;
+  return dtype == UM_BF16 ? dispatch_conv<bf16_t, MODE_FWD>(a, st)
+                          : dispatch_conv<float, MODE_FWD>(a, st);
+}
+
+int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, int accumulate,
+                    const void* wT, int K, int R, int stride, int pad, int pad_mode, int P,
+                    int Q, const void* dy, int ldy, hipStream_t st) {
+  UM_CHECK_ARG(K % 8 == 0 && ldy % 8 == 0, "um_conv2d_dgrad: K (%d) and ldy (%d) must be multiples of 8", K, ldy);
+  UM_CHECK_ARG(stride == 1 || stride == 2, "um_conv2d_dgrad: stride %d", stride);
+  UM_CHECK_ARG(pad_mode == UM_PAD_ZERO || stride == 1, "um_conv2d_dgrad: reflect needs stride 1");
+  ConvArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx;
+  a.P = P; a.Q = Q; a.K = K; a.ldy = ldy;
+  a.R = R; a.stride = stride; a.pad = pad; a.pad_mode = pad_mode;
+  a.a_src = dy; a.b_src = wT; a.bias = nullptr; a.out = dx; a.ld_out = ldx;
+  a.M = N * H * W; a.NC = C; a.KK = R * R * K;
+  a.epilogue = UM_EPI_NONE; a.accumulate = accumulate; a.out_f32 = (dtype == UM_F32);
+  if (a.M == 0) return UM_OK;
+  return dtype == UM_BF16 ? dispatch_conv<bf16_t, MODE_DGRAD>(a, st)
+                          : dispatch_conv<float, MODE_DGRAD>(a, st);
+}
+
+int um_conv_wgrad_splits(int M, int K, int RRC) {
+  const long tiles = (long)ceil_div(K, 64) * ceil_div(RRC, 64);
+  long splits = (1024 + tiles - 1) / tiles;
+  const long max_by_m = (M + 511) / 512;  // >= 512 pixels per split
+  if (splits > max_by_m) splits = max_by_m;
+  const long max_by_bytes = (64l << 20) / ((long)K * RRC * 4);  // <= 64 MB of slabs
+  if (splits > max_by_bytes) splits = max_by_bytes;
+  if (splits < 1) splits = 1;
+  return (int)splits;
+}
+
+int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* x, int K, int R,
+                    int stride, int pad, int pad_mode, int P, int Q, const void* dy, int ldy,
+                    float* slabs, int splits, hipStream_t st) {
+  UM_CHECK_ARG(C % 8 == 0 && K % 8 == 0, "um_conv2d_wgrad: C (%d), K (%d) must be multiples of 8", C, K);
+  UM_CHECK_ARG(splits >= 1, "um_conv2d_wgrad: splits");
+  WgradArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx; a.K = K; a.R = R; a.stride = stride;
+  a.pad = pad; a.pad_mode = pad_mode; a.P = P; a.Q = Q; a.ldy = ldy;
+  a.x = x; a.dy = dy; a.slabs = slabs;
+  a.M = N * P * Q; a.RRC = R * R * C;
+  a.m_per_split = ceil_div(ceil_div(a.M, splits), BK) * BK;
+  if (dtype == UM_BF16) return launch_wgrad<bf16_t, 64, 64>(a, splits, st);
+  return launch_wgrad<float, 64, 64>(a, splits, st);
+}
+
+int um_conv_wgrad_reduce(const float* slabs, int splits, int K, int Kreal, int R, int C,
+                         int Creal, float* dw, int accumulate, hipStream_t st) {
+  UM_CHECK_ARG(Kreal <= K && Creal <= C, "um_conv_wgrad_reduce: sizes");
+  const long total = (long)Kreal * Creal * R * R;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slabs, splits, K, Kreal,
+                     R, C, Creal, dw, accumulate);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C, void* wf, void* wT,
+                   int ldT, hipStream_t st) {
+  UM_CHECK_ARG(C >= Creal, "um_pack_weight: C < Creal");
+  const long total = (long)K * R * R * C;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, w, K, Creal,
+                       R, C, (bf16_t*)wf, (bf16_t*)wT, ldT);
+  else
+    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, st, w, K, Creal, R,
+                       C, (float*)wf, (float*)wT, ldT);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_colsum_parts(int M) { return ceil_div(M, COLSUM_ROWS); }
+
+int um_colsum(int dtype, int M, int C, int ld, const void* y, float* parts, hipStream_t st) {
+  const int blocks = ceil_div(M, COLSUM_ROWS);
+  if (blocks == 0) return UM_OK;
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)y, M,
+                       C, ld, parts, COLSUM_ROWS);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)y, M,
+                       C, ld, parts, COLSUM_ROWS);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_reduce_rows(const float* partials, int parts, int C, int stride, float* out, int accumulate,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, partials, parts,
+                     C, stride, out, accumulate);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,256 @@
+// Element-wise pieces of the encoder graph and layout plumbing.
+//
+//   um_merge_fwd / um_merge_bwd / um_merge_wgrad
+//       NodeBlock's sigmoid-weighted predecessor sum, reference
+//       model/layers/encoder.py:115-124.  Input i is weighted by
+//       sigmoid(w[widx[i]]) where the host passes the reference's index map
+//       (F3: widx = [0, 0, 1, 2, ...]).
+//   um_image_to_nhwc   NCHW f32 image -> NHWC (padded channels, zero fill)
+//   um_axpy            y += alpha * x over n elements (gradient accumulation)
+//   um_sigmoid_scale_bwd  d/dlogit of scale*sigmoid(logit) (disp head,
+//       reference model/layers/decoder.py:246 with ConvLayer sigmoid)
+#include "common.h"
+
+namespace {
+
+constexpr int MAX_SRC = 16;
+struct MergeArgs {
+  const void* src[MAX_SRC];
+  void* dsrc[MAX_SRC];
+  int widx[MAX_SRC];
+  int acc[MAX_SRC];
+  float coef[MAX_SRC];  // used when w == null (constant coefficients)
+};
+
+inline int grid_for(long n) {
+  long b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+template <typename T>
+__global__ void merge_fwd_kernel(MergeArgs a, int nsrc, const float* __restrict__ w, long n8,
+                                 T* __restrict__ dst) {
+  float coef[MAX_SRC];
+  for (int i = 0; i < nsrc; ++i) coef[i] = w ? sigmoidf_(w[a.widx[i]]) : a.coef[i];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8;
+       i += (long)gridDim.x * blockDim.x) {
+    float acc[8], v[8];
+    load8(reinterpret_cast<const T*>(a.src[0]) + i * 8, acc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= coef[0];
+    for (int s = 1; s < nsrc; ++s) {
+      load8(reinterpret_cast<const T*>(a.src[s]) + i * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += coef[s] * v[e];
+    }
+    store8(dst + i * 8, acc);
+  }
+}
+
+// dsrc_i (+)= coef_i * dm ; partial dot products sum(dm * src_i) per block
+template <typename T>
+__global__ void merge_bwd_kernel(MergeArgs a, int nsrc, const float* __restrict__ w, long n8,
+                                 const T* __restrict__ dm, float* __restrict__ parts) {
+  float coef[MAX_SRC], dot[MAX_SRC];
+  for (int i = 0; i < nsrc; ++i) {
+    coef[i] = w ? sigmoidf_(w[a.widx[i]]) : a.coef[i];
+    dot[i] = 0.f;
+  }
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8;
+       i += (long)gridDim.x * blockDim.x) {
+    float g[8], v[8], o[8];
+    load8(dm + i * 8, g);
+    for (int s = 0; s < nsrc; ++s) {
+      if (parts) {
+        load8(reinterpret_cast<const T*>(a.src[s]) + i * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dot[s] += g[e] * v[e];
+      }
+      if (a.dsrc[s]) {
+        T* d = reinterpret_cast<T*>(a.dsrc[s]) + i * 8;
+        if (a.acc[s]) load8(d, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (a.acc[s] ? o[e] : 0.f) + coef[s] * g[e];
+        store8(d, o);
+      }
+    }
+  }
+  if (parts) {
+    __shared__ float red[4];
+    for (int s = 0; s < nsrc; ++s) {
+      float t = wave_sum(dot[s]);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+      __syncthreads();
+      if (threadIdx.x == 0) parts[(long)blockIdx.x * nsrc + s] = red[0] + red[1] + red[2] + red[3];
+      __syncthreads();
+    }
+  }
+}
+
+__global__ void merge_wgrad_kernel(const float* __restrict__ parts, int nparts, int nsrc,
+                                   MergeArgs a, const float* __restrict__ w, float* dw,
+                                   int nw, int accumulate) {
+  // single block; dw[widx[i]] += sigmoid'(w) * sum_p parts[p][i]
+  __shared__ double tot[MAX_SRC];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int s = wave; s < nsrc; s += 4) {
+    double t = 0.0;
+    for (int p = lane; p < nparts; p += 64) t += parts[(long)p * nsrc + s];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) tot[s] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (!accumulate)
+      for (int j = 0; j < nw; ++j) dw[j] = 0.f;
+    for (int s = 0; s < nsrc; ++s) {
+      const float sg = sigmoidf_(w[a.widx[s]]);
+      dw[a.widx[s]] += (float)(tot[s] * sg * (1.0 - sg));
+    }
+  }
+}
+
+template <typename T>
+__global__ void image_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int H, int W,
+                                     int Cp, T* __restrict__ out) {
+  const long total = (long)N * H * W * Cp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = i % Cp;
+    const long pix = i / Cp;
+    const int xw = pix % W;
+    const int yh = (pix / W) % H;
+    const int n = pix / ((long)W * H);
+    const float v = c < C ? x[(((long)n * C + c) * H + yh) * W + xw] : 0.f;
+    out[i] = from_f32<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void axpy_kernel(long n, float alpha, const T* __restrict__ x, T* __restrict__ y) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    y[i] = from_f32<T>(to_f32(y[i]) + alpha * to_f32(x[i]));
+}
+
+// dlogit[m][c] = dd[m][c] * d * (1 - d/scale) for c < C; channels [C, ldo) zeroed
+template <typename T>
+__global__ void sigmoid_scale_bwd_kernel(long M, int C, const float* __restrict__ d, int ldd,
+                                         const float* __restrict__ dd, int lddd, float scale,
+                                         T* __restrict__ dlogit, int ldo) {
+  const long total = M * ldo;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long m = i / ldo;
+    const int c = i - m * ldo;
+    float v = 0.f;
+    if (c < C) {
+      const float dv = d[m * ldd + c];
+      v = dd[m * lddd + c] * dv * (1.f - dv / scale);
+    }
+    dlogit[i] = from_f32<T>(v);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int um_merge_fwd(int dtype, int nsrc, const void* const* srcs, const int* widx,
+                 const float* w, const float* coefs, long count, void* dst, hipStream_t st) {
+  UM_CHECK_ARG(nsrc >= 1 && nsrc <= MAX_SRC, "um_merge_fwd: nsrc %d", nsrc);
+  UM_CHECK_ARG(count % 8 == 0, "um_merge_fwd: count %% 8");
+  MergeArgs a{};
+  for (int i = 0; i < nsrc; ++i) {
+    a.src[i] = srcs[i];
+    a.widx[i] = widx ? widx[i] : 0;
+    a.coef[i] = coefs ? coefs[i] : 1.f;
+  }
+  const long n8 = count / 8;
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(merge_fwd_kernel<bf16_t>, dim3(grid_for(n8)), dim3(256), 0, st, a, nsrc, w,
+                       n8, (bf16_t*)dst);
+  else
+    hipLaunchKernelGGL(merge_fwd_kernel<float>, dim3(grid_for(n8)), dim3(256), 0, st, a, nsrc, w,
+                       n8, (float*)dst);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_merge_parts(long count) { return grid_for(count / 8); }
+
+int um_merge_bwd(int dtype, int nsrc, const void* const* srcs, void* const* dsrcs,
+                 const int* accumulate, const int* widx, const float* w, const float* coefs,
+                 long count, const void* dm, float* parts, hipStream_t st) {
+  UM_CHECK_ARG(nsrc >= 1 && nsrc <= MAX_SRC, "um_merge_bwd: nsrc %d", nsrc);
+  UM_CHECK_ARG(count % 8 == 0, "um_merge_bwd: count %% 8");
+  MergeArgs a{};
+  for (int i = 0; i < nsrc; ++i) {
+    a.src[i] = srcs ? srcs[i] : nullptr;
+    a.dsrc[i] = dsrcs[i];
+    a.acc[i] = accumulate[i];
+    a.widx[i] = widx ? widx[i] : 0;
+    a.coef[i] = coefs ? coefs[i] : 1.f;
+  }
+  const long n8 = count / 8;
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(merge_bwd_kernel<bf16_t>, dim3(grid_for(n8)), dim3(256), 0, st, a, nsrc, w,
+                       n8, (const bf16_t*)dm, parts);
+  else
+    hipLaunchKernelGGL(merge_bwd_kernel<float>, dim3(grid_for(n8)), dim3(256), 0, st, a, nsrc, w,
+                       n8, (const float*)dm, parts);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_merge_wgrad(const float* parts, int nparts, int nsrc, const int* widx, const float* w,
+                   float* dw, int nw, int accumulate, hipStream_t st) {
+  MergeArgs a{};
+  for (int i = 0; i < nsrc; ++i) a.widx[i] = widx[i];
+  hipLaunchKernelGGL(merge_wgrad_kernel, dim3(1), dim3(256), 0, st, parts, nparts, nsrc, a, w, dw,
+                     nw, accumulate);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_image_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp, void* out,
+                     hipStream_t st) {
+  const long total = (long)N * H * W * Cp;
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(image_to_nhwc_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, x, N,
+                       C, H, W, Cp, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(image_to_nhwc_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x, N,
+                       C, H, W, Cp, (float*)out);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_axpy(int dtype, long n, float alpha, const void* x, void* y, hipStream_t st) {
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(axpy_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, n, alpha,
+                       (const bf16_t*)x, (bf16_t*)y);
+  else
+    hipLaunchKernelGGL(axpy_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, n, alpha,
+                       (const float*)x, (float*)y);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_sigmoid_scale_bwd(int dtype, long M, int C, const float* d, int ldd, const float* dd,
+                         int lddd, float scale, void* dlogit, int ldo, hipStream_t st) {
+  const long total = M * ldo;
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(sigmoid_scale_bwd_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st,
+                       M, C, d, ldd, dd, lddd, scale, (bf16_t*)dlogit, ldo);
+  else
+    hipLaunchKernelGGL(sigmoid_scale_bwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, M,
+                       C, d, ldd, dd, lddd, scale, (float*)dlogit, ldo);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+}  // extern "C"

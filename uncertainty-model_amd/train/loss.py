@@ -1,0 +1,143 @@
+"""Loss functions (reference train/loss.py), HIP-backed.
+
+``TukraUncertaintyLoss.forward`` (reference :512-568) runs the fused umamd
+loss stack: per scale a DSSIM-map kernel and a per-pixel terms kernel in the
+forward, and one backward kernel producing d(total)/d(prediction) for all
+four channels, including the WSSIM term's path through the warp, both L-R
+consistency terms (with the scatter into the warped disparity), the
+edge-aware smoothness and the reprojection-error NLL.
+
+The sub-loss modules keep the reference's names and constructor kwargs so
+configs and attribute access (``loss.wssim.previous_image_error``,
+``loss.predictive_error.loss_type``...) work; the sub-losses are evaluated
+inside the fused kernels, not through their own ``forward``.
+"""
+from typing import Optional
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+from torch.nn import Module
+
+from umamd import lossfn as LF
+
+from .utils import ImagePyramid
+
+
+class _FusedOnly(nn.Module):
+    def forward(self, *args, **kwargs):
+        raise NotImplementedError(
+            f'umamd: {type(self).__name__} is evaluated inside TukraUncertaintyLoss\'s fused '
+            f'HIP kernels; a standalone forward is not implemented')
+
+
+class WeightedSSIMLoss(_FusedOnly):
+    """SSIM/L1 photometric error (reference :15-151)."""
+
+    def __init__(self, alpha: float = 0.85, k1: float = 0.01, k2: float = 0.03) -> None:
+        super().__init__()
+        if k1 != 0.01 or k2 != 0.03:
+            raise NotImplementedError('umamd WeightedSSIMLoss: k1/k2 are compiled in (0.01, 0.03)')
+        self.alpha = alpha
+        self.k1 = k1 ** 2
+        self.k2 = k2 ** 2
+        self.pool = nn.AvgPool2d(kernel_size=3, stride=1)
+        self._previous_image_error = None
+
+    @property
+    def previous_image_error(self) -> Tensor:
+        """Error map [B,2,h,w] of the last scale evaluated (reference :38-41)."""
+        return self._previous_image_error
+
+
+class ConsistencyLoss(_FusedOnly):
+    """L-R consistency (reference :154-188)."""
+
+
+class SmoothnessLoss(_FusedOnly):
+    """Edge-aware smoothness (reference :191-264)."""
+
+
+class PerceptualLoss(_FusedOnly):
+    """Discriminator feature L1 (reference :267-305); adversarial path, not implemented."""
+
+
+class GeneratorLoss(_FusedOnly):
+    """GAN generator loss (reference :308-337); adversarial path, not implemented."""
+
+    def __init__(self, loss: str = 'mse') -> None:
+        super().__init__()
+        self.adversarial = nn.MSELoss() if loss == 'mse' else nn.BCELoss()
+
+
+class ReprojectionErrorLoss(_FusedOnly):
+    """Uncertainty loss (reference :340-434)."""
+
+    def __init__(self, loss_type: str = 'l1', smoothness_weight: float = 1.0,
+                 consistency_weight: float = 1.0, pooling: bool = False) -> None:
+        super().__init__()
+        if loss_type not in ('l1', 'bayesian', 'log_bayesian'):
+            raise ValueError('Loss must be either "l1", "bayesian" or "log_bayesian".')
+        if pooling:
+            raise NotImplementedError('umamd ReprojectionErrorLoss: pooling=True is not '
+                                      'implemented (every reference config uses False)')
+        self.loss_type = loss_type
+        self.smoothness_weight = smoothness_weight
+        self.consistency_weight = consistency_weight
+        self.smoothness = SmoothnessLoss() if smoothness_weight > 0 else None
+        self.consistency = ConsistencyLoss() if consistency_weight > 0 else None
+        self.pool = nn.Identity()
+
+
+class TukraUncertaintyLoss(nn.Module):
+    """Total loss of the uncertainty model (reference :437-568)."""
+
+    def __init__(self, wssim_weight: float = 1.0, consistency_weight: float = 1.0,
+                 smoothness_weight: float = 1.0, adversarial_weight: float = 0.85,
+                 predictive_error_weight: float = 1.0, perceptual_weight: float = 0.05,
+                 wssim_alpha: float = 0.85, perceptual_start: int = 5,
+                 adversarial_loss_type: str = 'mse',
+                 error_loss_config: Optional[dict] = None) -> None:
+        super().__init__()
+        self.wssim = WeightedSSIMLoss(wssim_alpha)
+        self.consistency = ConsistencyLoss()
+        self.smoothness = SmoothnessLoss()
+        self.adversarial = GeneratorLoss(adversarial_loss_type)
+        self.perceptual = PerceptualLoss()
+        self.predictive_error = ReprojectionErrorLoss(**(error_loss_config or {}))
+        self.perceptual_start = perceptual_start
+        self.wssim_weight = wssim_weight
+        self.consistency_weight = consistency_weight
+        self.smoothness_weight = smoothness_weight
+        self.adversarial_weight = adversarial_weight
+        self.perceptual_weight = perceptual_weight
+        self.predictive_error_weight = predictive_error_weight
+        self.last_terms: Optional[Tensor] = None
+
+    def _cfg(self):
+        pe = self.predictive_error
+        return {'alpha': float(self.wssim.alpha), 'loss_type': LF.LOSS_TYPES[pe.loss_type],
+                'esw': float(pe.smoothness_weight), 'ecw': float(pe.consistency_weight),
+                'w_wssim': float(self.wssim_weight), 'w_cons': float(self.consistency_weight),
+                'w_smooth': float(self.smoothness_weight),
+                'w_err': float(self.predictive_error_weight)}
+
+    def forward(self, image_pyramid: ImagePyramid, predictions: ImagePyramid,
+                recon_pyramid: ImagePyramid, epoch: Optional[int] = None,
+                discriminator: Optional[Module] = None):
+        if discriminator is not None:
+            raise NotImplementedError('umamd: adversarial loss terms are not implemented yet')
+        n = len(predictions)
+        for p, im, r in zip(predictions, image_pyramid, recon_pyramid):
+            tag = getattr(r, '_umamd_recon', None)
+            if tag is None or tag != (id(p), id(im)):
+                raise ValueError('TukraUncertaintyLoss (umamd): recon_pyramid must be '
+                                 'train.utils.reconstruct_pyramid(predictions, image_pyramid) '
+                                 '(the fused backward differentiates through that warp)')
+        outs = LF.tukra_loss(self._cfg(), list(predictions), list(image_pyramid),
+                             list(recon_pyramid))
+        disp_loss, error_loss, terms = outs[0], outs[1], outs[2]
+        self.wssim._previous_image_error = outs[3 + n - 1]
+        self.last_error_maps = list(outs[3:3 + n])
+        self.last_terms = terms  # [disp, error, wssim, consistency, smoothness, error-term]
+        return disp_loss, error_loss

@@ -1,0 +1,136 @@
+"""Training loop (reference train/train.py:18-267), host-side Python.
+
+Same functions, signatures, logging and checkpoint format.  The step body is
+the reference's (train.py:112-129): pyramid -> model -> reconstruct -> loss
+-> backward -> optimiser step; the compute runs on the umamd HIP kernels and
+the optimiser is the fused umamd Adam (identical update rule to
+torch.optim.Adam with default betas/eps).
+"""
+import os
+import os.path
+from copy import deepcopy
+from typing import Optional, Tuple
+
+import torch
+from torch.nn import Module
+from torch.optim import Optimizer
+from torch.utils.data import DataLoader
+
+from umamd.optim import Adam
+
+from . import utils as u
+from .utils import Device, Loss, LRAdjuster, ScaleAdjuster
+
+try:
+    import tqdm
+except ImportError:  # pragma: no cover
+    tqdm = None
+
+
+def save_model(model: Module, save_model_to: str, disc: Optional[Module] = None,
+               epoch_number: Optional[int] = None, is_final: bool = False) -> None:
+    """state_dict checkpoint as ``final.pt`` / ``epoch_NNN.pt`` (reference :18-48)."""
+    os.makedirs(save_model_to, exist_ok=True)
+    filename = 'final.pt' if is_final else f'epoch_{epoch_number:03}.pt'
+    filepath = os.path.join(save_model_to, filename)
+    state_dict = {'model': model.state_dict(), 'disc': disc.state_dict()} \
+        if disc is not None else model.state_dict()
+    print(f'Saving model to:\n\t{filepath}')
+    torch.save(state_dict, filepath)
+
+
+def train_step(model: Module, left, right, loss_function: Module, optimiser: Optimizer,
+               scale: float, scales: int = 4, batch_index: int = 0):
+    """One step of the reference loop body (train.py:116-129) without logging;
+    returns the (disp_loss, error_loss) device tensors."""
+    images = torch.cat([left, right], dim=1)
+    image_pyramid = u.scale_pyramid(images, scales)
+    optimiser.zero_grad()
+    disparities = model(left, scale)
+    recon_pyramid = u.reconstruct_pyramid(disparities, image_pyramid)
+    disp_loss, error_loss = loss_function(image_pyramid, disparities, recon_pyramid,
+                                          batch_index, None)
+    (disp_loss + error_loss).backward()
+    optimiser.step()
+    return disp_loss, error_loss
+
+
+def train_one_epoch(model: Module, loader: DataLoader, loss_function: Module,
+                    model_optimiser: Optimizer, scale: float,
+                    disc: Optional[Module] = None,
+                    disc_optimiser: Optional[Optimizer] = None,
+                    disc_loss_function: Optional[Module] = None,
+                    epoch_number: Optional[int] = None, scales: int = 4,
+                    perceptual_update_freq: int = 10, device: Device = 'cpu',
+                    no_pbar: bool = False, rank: int = 0) -> Tuple[float, float]:
+    if disc is not None:
+        raise NotImplementedError('umamd: adversarial training is not implemented yet')
+    model.train()
+    running_disp_loss = running_error_loss = 0.0
+    disp_loss_per_image = unc_loss_per_image = None
+    batch_size = loader.batch_size if loader.batch_size is not None else len(loader)
+    description = f'Epoch #{epoch_number}' if epoch_number is not None else 'Epoch'
+    it = tqdm.tqdm(loader, description, unit='batch', disable=(no_pbar or rank > 0)) \
+        if tqdm is not None else loader
+    for i, image_pair in enumerate(it):
+        left = image_pair['left'].to(device)
+        right = image_pair['right'].to(device)
+        disp_loss, error_loss = train_step(model, left, right, loss_function,
+                                           model_optimiser, scale, scales, i)
+        if rank == 0:
+            running_disp_loss += disp_loss.item()
+            running_error_loss += error_loss.item()
+            disp_loss_per_image = running_disp_loss / ((i + 1) * batch_size)
+            unc_loss_per_image = running_error_loss / ((i + 1) * batch_size)
+            if tqdm is not None and hasattr(it, 'set_postfix'):
+                it.set_postfix(disp=disp_loss_per_image, unc=unc_loss_per_image,
+                               disc=None, scale=scale)
+    if no_pbar and rank == 0:
+        print(f'{description}:'
+              f'\n\tdisparity loss: {disp_loss_per_image:.2e}'
+              f'\n\tuncertainty loss: {unc_loss_per_image:.2e}'
+              f'\n\tdiscriminator loss: None'
+              f'\n\tdisparity scale: {scale:.2f}')
+    return disp_loss_per_image, unc_loss_per_image, None
+
+
+def train_model(model: Module, loader: DataLoader, loss_function: Module,
+                epochs: int, learning_rate: float,
+                disc: Optional[Module] = None,
+                disc_loss_function: Optional[Module] = None,
+                adjust_learning_rate: LRAdjuster = u.adjust_learning_rate,
+                adjust_disparity: ScaleAdjuster = u.adjust_disparity,
+                perceptual_update_freq: int = 10,
+                val_loader: Optional[DataLoader] = None,
+                evaluate_every: Optional[int] = None,
+                save_evaluation_to: Optional[str] = None,
+                save_every: Optional[int] = None,
+                save_model_to: Optional[str] = None,
+                finetune: bool = False, device: Device = 'cpu',
+                no_pbar: bool = False, rank: int = 0) -> Tuple[Loss, Loss]:
+    """Epoch loop with the reference's LR / disparity-scale schedules (:173-267)."""
+    from .evaluate import evaluate_model
+    model_optimiser = Adam(model.parameters(), learning_rate)
+    training_losses, validation_metrics = [], []
+    for i in range(epochs):
+        adjust_learning_rate(model_optimiser, i, learning_rate)
+        scale = 1 if finetune else adjust_disparity(i)
+        loss = train_one_epoch(model, loader, loss_function, model_optimiser, scale, disc,
+                               None, disc_loss_function, epoch_number=(i + 1),
+                               perceptual_update_freq=perceptual_update_freq, device=device,
+                               no_pbar=no_pbar, rank=rank)
+        if rank == 0:
+            training_losses.append(loss)
+        if evaluate_every is not None and (i + 1) % evaluate_every == 0:
+            metrics = evaluate_model(model, val_loader, save_evaluation_to,
+                                     epoch_number=(i + 1), is_final=False, scale=scale,
+                                     no_pbar=no_pbar, device=device, rank=rank)
+            if rank == 0:
+                validation_metrics.append(metrics)
+        if save_every is not None and (i + 1) % save_every == 0 and rank == 0:
+            save_model(model, save_model_to, disc, epoch_number=(i + 1))
+    if rank == 0:
+        print('Training completed.')
+    if save_model_to is not None and rank == 0:
+        save_model(model, save_model_to, is_final=True)
+    return training_losses, validation_metrics

@@ -1,0 +1,152 @@
+"""ctypes binding of libumamd.so (the C ABI declared in include/umamd.h).
+
+The product path has no fallback: if the library is missing or no HIP device
+is present, ``lib()`` raises.  Every wrapper passes torch's *current* stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libumamd.so')
+
+UM_F32, UM_BF16 = 0, 1
+PAD_ZERO, PAD_REFLECT = 0, 1
+EPI_NONE, EPI_STATS, EPI_SIGMOID_SCALE, EPI_RESIDUAL = 0, 1, 2, 3
+CAT_COPY, CAT_UP2, CAT_PSHUF = 0, 1, 2
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+_D = ctypes.c_double
+
+
+class CatSrc(ctypes.Structure):
+    _fields_ = [('ptr', _P), ('scale', _P), ('C', _I), ('ld', _I), ('op', _I),
+                ('coff', _I), ('dtype', _I), ('h', _I), ('w', _I)]
+
+
+# name -> (restype, argtypes); 's' = stream
+_SIG = {
+    'um_last_error': (ctypes.c_char_p, []),
+    'um_version': (_I, []),
+    'um_conv_stats_parts': (_I, [_I, _I]),
+    'um_conv2d_fwd': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I,
+                           _I, _P, _I, _I, _F, _P, _I, _P, 's']),
+    'um_conv2d_dgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
+                             _P, _I, 's']),
+    'um_conv_wgrad_splits': (_I, [_I, _I, _I]),
+    'um_conv2d_wgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I,
+                             _P, _I, 's']),
+    'um_conv_wgrad_reduce': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, 's']),
+    'um_pack_weight': (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _I, 's']),
+    'um_colsum_parts': (_I, [_I]),
+    'um_colsum': (_I, [_I, _I, _I, _I, _P, _P, 's']),
+    'um_reduce_rows': (_I, [_P, _I, _I, _I, _P, _I, 's']),
+    'um_bn_stats_reduce': (_I, [_P, _I, _I, _P, 's']),
+    'um_bn_coeffs': (_I, [_P, _D, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, 's']),
+    'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, 's']),
+    'um_bn_bwd_parts': (_I, [_L]),
+    'um_bn_elu_bwd_reduce': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P,
+                                  's']),
+    'um_bn_bwd_coeffs': (_I, [_P, _D, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, 's']),
+    'um_bn_elu_bwd_apply': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P,
+                                 _P, _P, _P, _I, 's']),
+    'um_merge_fwd': (_I, [_I, _I, _P, _P, _P, _P, _L, _P, 's']),
+    'um_merge_parts': (_I, [_L]),
+    'um_merge_bwd': (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _L, _P, _P, 's']),
+    'um_merge_wgrad': (_I, [_P, _I, _I, _P, _P, _P, _I, _I, 's']),
+    'um_image_to_nhwc': (_I, [_I, _P, _I, _I, _I, _I, _I, _P, 's']),
+    'um_axpy': (_I, [_I, _L, _F, _P, _P, 's']),
+    'um_sigmoid_scale_bwd': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
+    'um_attn_ws_kstats': (_L, [_I, _I, _I]),
+    'um_attn_ws_ctx': (_L, [_I, _I, _I, _I]),
+    'um_attn_ws_tiles': (_L, [_I, _I, _I, _I]),
+    'um_attn_fwd': (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, 's']),
+    'um_attn_bwd': (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _I, _P, _P, _P,
+                         _P, 's']),
+    'um_concat_build': (_I, [_I, _I, _I, _I, _P, _I, _I, _I, _P, 's']),
+    'um_concat_bwd_src': (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _I, _P, 's']),
+    'um_channel_mean': (_I, [_I, _I, _L, _I, _P, _I, _P, 's']),
+    'um_se_mlp_fwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, 's']),
+    'um_se_mlp_bwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, 's']),
+    'um_pyramid_level': (_I, [_P, _I, _I, _I, _P, _I, _I, 's']),
+    'um_warp': (_I, [_P, _I, _I, _I, _I, _P, _L, _L, _F, _P, 's']),
+    'um_loss_parts': (_I, [_I, _I, _I]),
+    'um_loss_fwd_scale': (_I, [_P, _P, _P, _I, _I, _I, _I, _F, _I, _F, _F, _P, _P, _P, 's']),
+    'um_loss_finalize': (_I, [_I, _P, _P, _P, _F, _F, _F, _F, _F, _F, _I, _P, 's']),
+    'um_loss_bwd_scale': (_I, [_P, _P, _P, _I, _I, _I, _I, _F, _I, _F, _F, _P, _P, _F, _F, _F,
+                               _F, _F, _P, 's']),
+    'um_adam_chunk': (_I, []),
+    'um_adam_step': (_I, [_P, _P, _I, _F, _F, _F, _F, _F, _I, 's']),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class UmamdError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load the HIP library (raises if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise UmamdError(f'{LIB_PATH} not found: build it with '
+                         f'`python uncertainty-model_amd/umamd/_build.py` (hipcc, gfx950)')
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIG.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = [_P if a == 's' else a for a in args]
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    return sorted(_SIG)
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def call(name: str, *args):
+    """Call a C-ABI entry; the trailing stream argument is appended."""
+    fn = getattr(lib(), name)
+    rc = fn(*args, stream())
+    if rc != 0:
+        msg = lib().um_last_error().decode(errors='replace')
+        raise UmamdError(f'{name} failed ({rc}): {msg}')
+
+
+def query(name: str, *args):
+    """Call a pure host-side query entry (no stream)."""
+    return getattr(lib(), name)(*args)
+
+
+def require_device(t: torch.Tensor):
+    if not t.is_cuda:
+        raise UmamdError('umamd kernels need tensors on a HIP device (got CPU tensor); '
+                         'the HIP path has no CPU fallback')
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return UM_F32
+    if dt == torch.bfloat16:
+        return UM_BF16
+    raise UmamdError(f'unsupported activation dtype {dt}')

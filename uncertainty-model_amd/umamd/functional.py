@@ -1,0 +1,541 @@
+"""Autograd functions over the umamd C ABI (HIP kernels on gfx950).
+
+Activations inside the model are NHWC tensors ``[N, H, W, C]`` (C a multiple
+of 8), element type float32 or bfloat16; parameters stay in the reference's
+NCHW float32 layout and are repacked per call by ``um_pack_weight``.  No
+function here has a CPU path: every op calls the HIP library.
+
+Granularity (one autograd node each):
+  * ``conv_bn_elu``     Conv2d (+zero/reflect pad) -> BatchNorm2d(train) -> ELU,
+                        optionally followed by the SE squeeze/excite gate
+                        (reference model/layers/encoder.py:21-52,
+                        model/layers/decoder.py:55-87,90-136)
+  * ``merge``           NodeBlock weighted predecessor sum (encoder.py:115-124)
+  * ``attention_block`` EfficientAttention incl. 1x1 convs and residual
+                        (model/layers/attention.py:42-76)
+  * ``concat``          decoder concat of copy / x2-bilinear / pixel-shuffle
+                        sources with optional per-(n,c) gates
+                        (model/layers/decoder.py:228-242)
+  * ``disp_head``       ConvLayer(sigmoid) * scale (decoder.py:244-247)
+  * ``tukra_loss``      the 4-scale loss stack (train/loss.py:512-568)
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from ._lib import call, ptr, query
+
+
+def ceil8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def _dt(t: torch.Tensor) -> int:
+    return L.dtype_code(t.dtype)
+
+
+# --------------------------------------------------------------- helpers ----
+def _pack(weight: torch.Tensor, Cp: int, dtype: torch.dtype, wf=True, wT=True, ldT=None):
+    """Repack an NCHW f32 conv weight to [K][R][R][Cp] and [Cp][R][R][ldT]."""
+    K, Creal, R, _ = weight.shape
+    ldT = ldT or K
+    w = weight.detach()
+    if w.dtype != torch.float32 or not w.is_contiguous():
+        w = w.float().contiguous()
+    f = torch.empty((K, R, R, Cp), dtype=dtype, device=w.device) if wf else None
+    t = None
+    if wT:
+        t = (torch.zeros if ldT != K else torch.empty)((Cp, R, R, ldT), dtype=dtype,
+                                                        device=w.device)
+    call('um_pack_weight', L.dtype_code(dtype), ptr(w), K, Creal, R, Cp, ptr(f), ptr(t), ldT)
+    return f, t
+
+
+def _conv_fwd(x, wf, bias, K, R, stride, pad, pad_mode, out_dtype=None, epi=L.EPI_NONE,
+              epi_scale=1.0, residual=None, stats=None, out=None, ldo=None):
+    N, H, W, C = x.shape
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - R) // stride + 1
+    od = out_dtype or x.dtype
+    if out is None:
+        ldo = ldo or K
+        out = torch.empty((N, P, Q, ldo), dtype=od, device=x.device)
+    call('um_conv2d_fwd', _dt(x), N, H, W, C, C, ptr(x), ptr(wf), ptr(bias), K, R, stride, pad,
+         pad_mode, P, Q, L.dtype_code(od), ptr(out), out.shape[-1], epi, float(epi_scale),
+         ptr(residual), residual.shape[-1] if residual is not None else 0, ptr(stats))
+    return out
+
+
+def _conv_dgrad(dy, wT, x_shape, K, R, stride, pad, pad_mode, dx=None, accumulate=False):
+    N, H, W, C = x_shape
+    _, P, Q, ldy = dy.shape
+    if dx is None:
+        dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    call('um_conv2d_dgrad', _dt(dy), N, H, W, C, C, ptr(dx), int(accumulate), ptr(wT), K, R,
+         stride, pad, pad_mode, P, Q, ptr(dy), ldy)
+    return dx
+
+
+def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None):
+    """dW in the reference NCHW layout [Kreal][Creal][R][R] (f32)."""
+    N, H, W, C = x.shape
+    _, P, Q, ldy = dy.shape
+    M = N * P * Q
+    RRC = R * R * C
+    splits = query('um_conv_wgrad_splits', M, K, RRC)
+    slabs = torch.empty((splits, K, RRC), dtype=torch.float32, device=x.device)
+    call('um_conv2d_wgrad', _dt(x), N, H, W, C, C, ptr(x), K, R, stride, pad, pad_mode, P, Q,
+         ptr(dy), ldy, ptr(slabs), splits)
+    if dw is None:
+        dw = torch.empty((Kreal, Creal, R, R), dtype=torch.float32, device=x.device)
+    call('um_conv_wgrad_reduce', ptr(slabs), splits, K, Kreal, R, C, Creal, ptr(dw), 0)
+    return dw
+
+
+def _colsum(y, C):
+    """sum over pixels of y[..., :C] -> f32 [C]"""
+    M = y.numel() // y.shape[-1]
+    parts_n = query('um_colsum_parts', M)
+    parts = torch.empty((parts_n, C), dtype=torch.float32, device=y.device)
+    call('um_colsum', _dt(y), M, C, y.shape[-1], ptr(y), ptr(parts))
+    out = torch.empty((C,), dtype=torch.float32, device=y.device)
+    call('um_reduce_rows', ptr(parts), parts_n, C, C, ptr(out), 0)
+    return out
+
+
+class BNSync:
+    """How a BN layer exchanges statistics (SyncBatchNorm semantics)."""
+
+    def __init__(self, bn: torch.nn.Module):
+        self.bn = bn
+        self.group = None
+        self.world = 1
+        if isinstance(bn, torch.nn.SyncBatchNorm) and dist.is_available() and \
+                dist.is_initialized():
+            self.group = bn.process_group or dist.group.WORLD
+            self.world = dist.get_world_size(self.group)
+
+    def all_reduce(self, t: torch.Tensor):
+        if self.world > 1:
+            dist.all_reduce(t, group=self.group)
+
+
+def _bn_forward_coeffs(parts, nparts, K, count, bn, sync: BNSync, training: bool, device):
+    mean = torch.empty(K, dtype=torch.float32, device=device)
+    invstd = torch.empty_like(mean)
+    scale = torch.empty_like(mean)
+    shift = torch.empty_like(mean)
+    gamma = bn.weight if bn.affine else None
+    beta = bn.bias if bn.affine else None
+    if training or not bn.track_running_stats:
+        st = torch.empty((K, 2), dtype=torch.float64, device=device)
+        call('um_bn_stats_reduce', ptr(parts), nparts, K, ptr(st))
+        sync.all_reduce(st)
+        upd = training and bn.track_running_stats and bn.running_mean is not None
+        if upd and bn.momentum is None:
+            raise NotImplementedError('BatchNorm momentum=None (cumulative average) is not supported')
+        call('um_bn_coeffs', ptr(st), float(count * sync.world), K, ptr(gamma), ptr(beta),
+             float(bn.eps), float(bn.momentum or 0.0),
+             ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
+             ptr(bn.num_batches_tracked) if upd and bn.num_batches_tracked is not None else None,
+             ptr(mean), ptr(invstd), ptr(scale), ptr(shift))
+    else:
+        # eval mode: normalise with the running statistics
+        st = torch.stack([bn.running_mean.double(), (bn.running_var.double() + bn.running_mean.double() ** 2)], 1).contiguous()
+        call('um_bn_coeffs', ptr(st), 1.0, K, ptr(gamma), ptr(beta), float(bn.eps), 0.0, None,
+             None, None, ptr(mean), ptr(invstd), ptr(scale), ptr(shift))
+    return mean, invstd, scale, shift
+
+
+# ---------------------------------------------------------- conv+BN+ELU ----
+class ConvSpec:
+    """Static description of a conv block (non-tensor autograd argument)."""
+
+    def __init__(self, conv: torch.nn.Conv2d, bn: Optional[torch.nn.Module], pad: int,
+                 pad_mode: int, elu: bool = True):
+        self.conv = conv
+        self.bn = bn
+        self.stride = conv.stride[0]
+        self.pad = pad
+        self.pad_mode = pad_mode
+        self.elu = elu
+
+
+class ConvBNELUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec):
+        L.require_device(x)
+        N, H, W, Cp = x.shape
+        K, Creal, R, _ = weight.shape
+        bn = spec.bn
+        dev = x.device
+        wf, wT = _pack(weight, Cp, x.dtype)
+        P = (H + 2 * spec.pad - R) // spec.stride + 1
+        Q = (W + 2 * spec.pad - R) // spec.stride + 1
+        M = N * P * Q
+        bias_f = bias.detach().float().contiguous() if bias is not None else None
+        if bn is not None:
+            training = bn.training
+            sync = BNSync(bn)
+            nparts = query('um_conv_stats_parts', M, K)
+            parts = torch.empty((nparts, K, 2), dtype=torch.float32, device=dev)
+            y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
+                          epi=L.EPI_STATS if training else L.EPI_NONE, stats=parts)
+            mean, invstd, scale, shift = _bn_forward_coeffs(parts, nparts, K, M, bn, sync,
+                                                            training, dev)
+        else:  # ConvELUBlock(batch_norm=False): identity normalisation
+            sync = None
+            training = False
+            y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode)
+            mean = torch.zeros(K, dtype=torch.float32, device=dev)
+            shift = mean
+            invstd = torch.ones(K, dtype=torch.float32, device=dev)
+            scale = invstd
+        a = torch.empty_like(y)
+        call('um_bn_elu_fwd', _dt(y), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
+             int(spec.elu))
+        outs = [a]
+        se = None
+        if w1 is not None:
+            R1 = w1.shape[0]
+            pooled = torch.zeros((N, K), dtype=torch.float32, device=dev)
+            call('um_channel_mean', _dt(a), N, P * Q, K, ptr(a), K, ptr(pooled))
+            z1 = torch.empty((N, R1), dtype=torch.float32, device=dev)
+            s = torch.empty((N, K), dtype=torch.float32, device=dev)
+            call('um_se_mlp_fwd', N, K, R1, ptr(pooled), ptr(w1.detach().float().contiguous()),
+                 ptr(w2.detach().float().contiguous()), ptr(z1), ptr(s))
+            se = (pooled, z1, s)
+            outs.append(s)
+        ctx.spec = spec
+        ctx.sync = sync
+        ctx.has_bn = bn is not None and training
+        ctx.geom = (N, H, W, Cp, K, Creal, R, P, Q)
+        ctx.se = se
+        ctx.save_for_backward(x, wT, y, mean, invstd, scale, shift, gamma, w1, w2)
+        return tuple(outs) if len(outs) > 1 else outs[0]
+
+    @staticmethod
+    def backward(ctx, da, ds=None):
+        x, wT, y, mean, invstd, scale, shift, gamma, w1, w2 = ctx.saved_tensors
+        N, H, W, Cp, K, Creal, R, P, Q = ctx.geom
+        spec = ctx.spec
+        M = N * P * Q
+        dev = y.device
+        da = da.contiguous() if da is not None else torch.zeros_like(y)
+        add_nc = None
+        dw1 = dw2 = None
+        if ctx.se is not None and ds is not None:
+            pooled, z1, s = ctx.se
+            R1 = w1.shape[0]
+            dw1 = torch.zeros(w1.shape, dtype=torch.float32, device=dev)
+            dw2 = torch.zeros(w2.shape, dtype=torch.float32, device=dev)
+            add_nc = torch.empty((N, K), dtype=torch.float32, device=dev)
+            call('um_se_mlp_bwd', N, K, R1, ptr(ds.float().contiguous()), ptr(s), ptr(z1),
+                 ptr(pooled), ptr(w1.detach().float().contiguous()),
+                 ptr(w2.detach().float().contiguous()), ptr(dw1), ptr(dw2), ptr(add_nc),
+                 1.0 / (P * Q))
+        dgamma = dbeta = None
+        k1 = torch.empty(K, dtype=torch.float32, device=dev)
+        k2 = torch.empty_like(k1)
+        k3 = torch.empty_like(k1)
+        if ctx.has_bn:
+            nb = query('um_bn_bwd_parts', M)
+            parts = torch.empty((nb, K, 2), dtype=torch.float32, device=dev)
+            call('um_bn_elu_bwd_reduce', _dt(y), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
+                 ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(parts))
+            st = torch.empty((K, 2), dtype=torch.float64, device=dev)
+            call('um_bn_stats_reduce', ptr(parts), nb, K, ptr(st))
+            st_local = None
+            if ctx.sync is not None and ctx.sync.world > 1:
+                st_local = st.clone()
+                ctx.sync.all_reduce(st)
+            world = ctx.sync.world if ctx.sync is not None else 1
+            if gamma is not None:
+                dgamma = torch.empty(K, dtype=torch.float32, device=dev)
+                dbeta = torch.empty(K, dtype=torch.float32, device=dev)
+            call('um_bn_bwd_coeffs', ptr(st), float(M * world), K, ptr(gamma), ptr(invstd),
+                 ptr(st_local), ptr(dgamma), ptr(dbeta), 0, ptr(k1), ptr(k2), ptr(k3))
+        else:
+            # no batch statistics (no BN, or BN in eval mode): dy = dz * scale
+            k1.copy_(scale)
+            k2.zero_()
+            k3.zero_()
+            if gamma is not None and spec.bn is not None:
+                raise NotImplementedError('backward through an eval-mode BatchNorm')
+        dy = torch.empty_like(y)
+        call('um_bn_elu_bwd_apply', _dt(y), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
+             ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1), ptr(k2),
+             ptr(k3), ptr(dy), K)
+        dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode)
+        dbias = _colsum(dy, K) if ctx.needs_input_grad[2] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _conv_dgrad(dy, wT, (N, H, W, Cp), K, R, spec.stride, spec.pad, spec.pad_mode)
+        return dx, dW, dbias, dgamma, dbeta, dw1, dw2, None
+
+
+def conv_bn_elu(x, conv, bn, pad, pad_mode, se=None, elu=True):
+    """Conv2d -> BatchNorm2d (train: batch stats; eval: running stats; None:
+    identity) -> ELU [-> SE gate].  Returns a, or (a, gate) with ``se``."""
+    spec = ConvSpec(conv, bn, pad, pad_mode, elu)
+    w1 = se.excite[0].weight if se is not None else None
+    w2 = se.excite[2].weight if se is not None else None
+    affine = bn is not None and bn.affine
+    return ConvBNELUFn.apply(x, conv.weight, conv.bias,
+                             bn.weight if affine else None, bn.bias if affine else None,
+                             w1, w2, spec)
+
+
+# -------------------------------------------------------------------- merge --
+class MergeFn(torch.autograd.Function):
+    """out = sum_i c_i * src_i with c_i = sigmoid(w[widx[i]]) (w given) or the
+    constant coefs[i] (w None: GraphBlock output-node average)."""
+
+    @staticmethod
+    def forward(ctx, w, widx: List[int], coefs, *srcs):
+        out = torch.empty_like(srcs[0])
+        n = len(srcs)
+        arr = (ctypes_p * n)(*[s.data_ptr() for s in srcs])
+        idx = (ctypes_i * n)(*widx)
+        cf = (ctypes_f * n)(*coefs) if coefs is not None else None
+        call('um_merge_fwd', _dt(out), n, arr, idx, ptr(w), cf, out.numel(), ptr(out))
+        ctx.widx = list(widx)
+        ctx.coefs = coefs
+        ctx.has_w = w is not None
+        ctx.save_for_backward(w, *srcs)
+        return out
+
+    @staticmethod
+    def backward(ctx, dm):
+        w, *srcs = ctx.saved_tensors
+        n = len(srcs)
+        dm = dm.contiguous()
+        dsrcs = [torch.empty_like(s) if ctx.needs_input_grad[3 + i] else None
+                 for i, s in enumerate(srcs)]
+        need_w = ctx.has_w and ctx.needs_input_grad[0]
+        nparts = query('um_merge_parts', dm.numel())
+        parts = torch.empty((nparts, n), dtype=torch.float32, device=dm.device) if need_w else None
+        arr = (ctypes_p * n)(*[s.data_ptr() for s in srcs])
+        darr = (ctypes_p * n)(*[d.data_ptr() if d is not None else None for d in dsrcs])
+        acc = (ctypes_i * n)(*([0] * n))
+        idx = (ctypes_i * n)(*ctx.widx)
+        cf = (ctypes_f * n)(*ctx.coefs) if ctx.coefs is not None else None
+        call('um_merge_bwd', _dt(dm), n, arr, darr, acc, idx, ptr(w), cf, dm.numel(), ptr(dm),
+             ptr(parts))
+        dw = None
+        if need_w:
+            dw = torch.empty_like(w, dtype=torch.float32)
+            call('um_merge_wgrad', ptr(parts), nparts, n, idx, ptr(w), ptr(dw), w.numel(), 0)
+        return (dw, None, None, *dsrcs)
+
+
+import ctypes as _ct  # noqa: E402
+
+ctypes_p = _ct.c_void_p
+ctypes_i = _ct.c_int
+ctypes_f = _ct.c_float
+
+
+def merge(inputs: Sequence[torch.Tensor], w: Optional[torch.Tensor], widx: Sequence[int],
+          coefs: Optional[Sequence[float]] = None):
+    if len(inputs) == 1 and w is None and coefs is None:
+        return inputs[0]
+    return MergeFn.apply(w, list(widx), list(coefs) if coefs is not None else None, *inputs)
+
+
+# ---------------------------------------------------------------- attention --
+class AttentionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wk, bk, wq, bq, wv, bv, wr, br, heads: int):
+        L.require_device(x)
+        N, H, W, C = x.shape
+        S = H * W
+        dt = x.dtype
+        dev = x.device
+        wf = torch.empty((3 * C, 1, 1, C), dtype=dt, device=dev)
+        wT = torch.empty((C, 1, 1, 3 * C), dtype=dt, device=dev)
+        for i, wgt in enumerate((wk, wq, wv)):
+            # rows [iC, (i+1)C) of wf; columns [iC, (i+1)C) of wT (row stride 3C)
+            call('um_pack_weight', L.dtype_code(dt), ptr(wgt.detach().float().contiguous()), C,
+                 C, 1, C, wf[i * C].data_ptr(), wT.data_ptr() + i * C * wT.element_size(),
+                 3 * C)
+        bqkv = torch.cat([bk.detach(), bq.detach(), bv.detach()]).float().contiguous()
+        qkv = _conv_fwd(x, wf, bqkv, 3 * C, 1, 1, 0, L.PAD_ZERO)
+        kmax = torch.empty((N, C), dtype=torch.float32, device=dev)
+        ksum = torch.empty_like(kmax)
+        ctxm = torch.empty((N, heads, (C // heads) ** 2), dtype=torch.float32, device=dev)
+        wsn = max(query('um_attn_ws_kstats', N, S, C), query('um_attn_ws_ctx', N, S, C, heads))
+        ws = torch.empty(wsn, dtype=torch.float32, device=dev)
+        att = torch.empty((N, H, W, C), dtype=dt, device=dev)
+        call('um_attn_fwd', L.dtype_code(dt), N, S, C, heads, ptr(qkv), 3 * C, ptr(kmax),
+             ptr(ksum), ptr(ctxm), ptr(ws), ptr(att), C)
+        wrf, wrT = _pack(wr, C, dt)
+        out = _conv_fwd(att, wrf, br.detach().float().contiguous(), C, 1, 1, 0, L.PAD_ZERO,
+                        epi=L.EPI_RESIDUAL, residual=x)
+        ctx.heads = heads
+        ctx.save_for_backward(x, qkv, kmax, ksum, ctxm, att, wT, wrT)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, qkv, kmax, ksum, ctxm, att, wT, wrT = ctx.saved_tensors
+        heads = ctx.heads
+        N, H, W, C = x.shape
+        S = H * W
+        dev = x.device
+        dt = x.dtype
+        dout = dout.contiguous()
+        datt = _conv_dgrad(dout, wrT, (N, H, W, C), C, 1, 1, 0, L.PAD_ZERO)
+        dwr = _conv_wgrad(att, dout, C, C, C, 1, 1, 0, L.PAD_ZERO)
+        dbr = _colsum(dout, C)
+        dqkv = torch.empty((N, H, W, 3 * C), dtype=dt, device=dev)
+        dks = torch.empty((N * S, C), dtype=torch.float32, device=dev)
+        ws = torch.empty(query('um_attn_ws_tiles', N, S, C, heads), dtype=torch.float32,
+                         device=dev)
+        dctx = torch.empty_like(ctxm)
+        r = torch.empty((N, C), dtype=torch.float32, device=dev)
+        call('um_attn_bwd', L.dtype_code(dt), N, S, C, heads, ptr(qkv), 3 * C, ptr(kmax),
+             ptr(ksum), ptr(ctxm), ptr(datt), C, ptr(dqkv), 3 * C, ptr(dks), ptr(ws), ptr(dctx),
+             ptr(r))
+        dwqkv = _conv_wgrad(x, dqkv, 3 * C, 3 * C, C, 1, 1, 0, L.PAD_ZERO)
+        dbqkv = _colsum(dqkv, 3 * C)
+        dx = dout.clone() if dout.dtype == dt else dout.to(dt)
+        _conv_dgrad(dqkv, wT, (N, H, W, C), 3 * C, 1, 1, 0, L.PAD_ZERO, dx=dx, accumulate=True)
+        return (dx, dwqkv[:C], dbqkv[:C], dwqkv[C:2 * C], dbqkv[C:2 * C], dwqkv[2 * C:],
+                dbqkv[2 * C:], dwr, dbr, None)
+
+
+def attention_block(x, att_module):
+    m = att_module
+    return AttentionFn.apply(x, m.keys.weight, m.keys.bias, m.queries.weight, m.queries.bias,
+                             m.values.weight, m.values.bias, m.reprojection.weight,
+                             m.reprojection.bias, m.head_size)
+
+
+# ------------------------------------------------------------------- concat --
+class CatSource:
+    """A concat input: tensor (NHWC), op, optional gate [N][C] f32."""
+
+    def __init__(self, t: torch.Tensor, op: int, C: int, gate: Optional[torch.Tensor] = None):
+        self.t, self.op, self.C, self.gate = t, op, C, gate
+
+
+class ConcatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, meta, *tensors):
+        # meta: list of (op, C, has_gate); tensors: src0, [gate0], src1, ...
+        N, H, W, Ctot, dtype = meta['out']
+        srcs, it = [], iter(tensors)
+        structs = (L.CatSrc * len(meta['srcs']))()
+        coff = 0
+        saved = []
+        for i, (op, C) in enumerate(meta['srcs']):
+            t = next(it)
+            g = next(it) if meta['gates'][i] else None
+            srcs.append((t, g))
+            h, w = (H, W) if op == L.CAT_COPY else (H // 2, W // 2)
+            structs[i] = L.CatSrc(t.data_ptr(), g.data_ptr() if g is not None else None, C,
+                                  t.shape[-1], op, coff, _dt(t), h, w)
+            coff += C
+            saved += [t] + ([g] if g is not None else [])
+        out = torch.empty((N, H, W, Ctot), dtype=dtype, device=tensors[0].device)
+        call('um_concat_build', L.dtype_code(dtype), N, H, W, ptr(out), Ctot, Ctot,
+             len(srcs), structs)
+        ctx.meta = meta
+        ctx.save_for_backward(*saved)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        meta = ctx.meta
+        N, H, W, Ctot, dtype = meta['out']
+        g = g.contiguous()
+        saved = list(ctx.saved_tensors)
+        grads = []
+        coff = 0
+        k = 1  # index into needs_input_grad (0 = meta)
+        for i, (op, C) in enumerate(meta['srcs']):
+            t = saved.pop(0)
+            gate = saved.pop(0) if meta['gates'][i] else None
+            need_t = ctx.needs_input_grad[k]
+            need_g = gate is not None and ctx.needs_input_grad[k + 1]
+            h, w = (H, W) if op == L.CAT_COPY else (H // 2, W // 2)
+            s = L.CatSrc(t.data_ptr(), gate.data_ptr() if gate is not None else None, C,
+                         t.shape[-1], op, coff, _dt(t), h, w)
+            dt_ = torch.empty_like(t) if need_t else None
+            dg = torch.zeros_like(gate) if need_g else None
+            if need_t or need_g:
+                call('um_concat_bwd_src', L.dtype_code(dtype), N, H, W, ptr(g), Ctot,
+                     _ct.byref(s), ptr(dt_), t.shape[-1], _dt(t), 0, ptr(dg))
+            grads.append(dt_)
+            if gate is not None:
+                grads.append(dg)
+            k += 2 if gate is not None else 1
+            coff += C
+        return (None, *grads)
+
+
+def concat(sources: Sequence[CatSource], N, H, W, dtype):
+    Ctot = ceil8(sum(s.C for s in sources))
+    meta = {'out': (N, H, W, Ctot, dtype), 'srcs': [(s.op, s.C) for s in sources],
+            'gates': [s.gate is not None for s in sources]}
+    tensors = []
+    for s in sources:
+        tensors.append(s.t)
+        if s.gate is not None:
+            tensors.append(s.gate)
+    return ConcatFn.apply(meta, *tensors)
+
+
+# ---------------------------------------------------------------- disp head --
+class DispHeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, scale: float):
+        N, H, W, Cp = x.shape
+        K, Creal, R, _ = weight.shape
+        Kp = ceil8(K)
+        wf, wT = _pack(weight, Cp, x.dtype, ldT=Kp)
+        d = _conv_fwd(x, wf, bias.detach().float().contiguous(), K, R, 1, 1, L.PAD_REFLECT,
+                      out_dtype=torch.float32, epi=L.EPI_SIGMOID_SCALE, epi_scale=scale)
+        ctx.scale = float(scale)
+        ctx.save_for_backward(x, wT, d)
+        ctx.geom = (K, Kp, Creal, R)
+        return d
+
+    @staticmethod
+    def backward(ctx, dd):
+        x, wT, d = ctx.saved_tensors
+        K, Kp, Creal, R = ctx.geom
+        N, H, W, Cp = x.shape
+        dd = dd.contiguous().float()
+        M = N * H * W
+        dl = torch.empty((N, H, W, Kp), dtype=x.dtype, device=x.device)
+        call('um_sigmoid_scale_bwd', _dt(dl), M, K, ptr(d), K, ptr(dd), dd.shape[-1], ctx.scale,
+             ptr(dl), Kp)
+        dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)
+        db = _colsum(dl, K)
+        dx = _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT) \
+            if ctx.needs_input_grad[0] else None
+        return dx, dW, db, None
+
+
+def disp_head(x, conv, scale):
+    return DispHeadFn.apply(x, conv.weight, conv.bias, float(scale))
+
+
+# ------------------------------------------------------------------- inputs --
+def image_to_nhwc(img: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """[N,C,H,W] f32 (any strides) -> NHWC [N,H,W,ceil8(C)] in ``dtype``."""
+    L.require_device(img)
+    x = img.detach()
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        x = x.float().contiguous()
+    N, C, H, W = x.shape
+    Cp = ceil8(C)
+    out = torch.empty((N, H, W, Cp), dtype=dtype, device=x.device)
+    call('um_image_to_nhwc', L.dtype_code(dtype), ptr(x), N, C, H, W, Cp, ptr(out))
+    return out
