@@ -96,7 +96,8 @@ def test_conv_first_layer_padded_channels():
     assert _rel(_nchw(yd), yr) < 1e-4
 
 
-def test_merge():
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_merge(dtype):
     from umamd import functional as U
     w = torch.tensor([0.3, -0.7, 1.1, 0.2])
     xs = [torch.randn(2, 4, 6, 16) for _ in range(4)]
@@ -108,18 +109,20 @@ def test_merge():
     g = torch.randn_like(ref)
     (ref * g).sum().backward()
     wd = w.to(DEV).requires_grad_(True)
-    xd = [x.to(DEV).requires_grad_(True) for x in xs]
+    xd = [x.to(DEV).to(dtype).requires_grad_(True) for x in xs]
     out = U.merge(xd, wd, [0, 0, 1, 2])
-    (out * g.to(DEV)).sum().backward()
-    assert _rel(out, ref) < 1e-6
-    assert _rel(wd.grad, wr.grad) < 1e-5
+    (out.float() * g.to(DEV)).sum().backward()
+    tol = 1e-6 if dtype == torch.float32 else 2e-2
+    assert _rel(out, ref) < tol
+    assert _rel(wd.grad, wr.grad) < tol * 10
     assert wd.grad[3].item() == 0.0  # F3: last weight never used
     for a, b in zip(xd, xr):
-        assert _rel(a.grad, b.grad) < 1e-6
+        assert _rel(a.grad, b.grad) < tol
 
 
 @pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 8), (512, 2, 4), (256, 4, 8)])
-def test_attention_block(C, H, W):
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_attention_block(C, H, W, dtype):
     from oracle.model import efficient_attention
     from umamd import functional as U
     import importlib
@@ -131,20 +134,21 @@ def test_attention_block(C, H, W):
     g = torch.randn_like(yr)
     (yr * g).sum().backward()
     ad = att.to(DEV)
-    xd = _nhwc(x).requires_grad_(True)
+    xd = _nhwc(x).to(dtype).requires_grad_(True)
     yd = U.attention_block(xd, ad)
-    (yd * _nhwc(g)).sum().backward()
-    assert _rel(_nchw(yd), yr) < 1e-5
-    assert _rel(_nchw(xd.grad), xr.grad) < 1e-4
+    (yd.float() * _nhwc(g)).sum().backward()
+    tol = 1e-4 if dtype == torch.float32 else 5e-2
+    assert _rel(_nchw(yd), yr) < tol / 10
+    assert _rel(_nchw(xd.grad), xr.grad) < tol
     for name in ('keys', 'queries', 'values', 'reprojection'):
         for t in ('weight', 'bias'):
             ref = P[f'{name}.{t}'].grad
             got = getattr(getattr(ad, name), t).grad
             if name == 'keys' and t == 'bias':
                 # softmax over pixels is shift invariant: true gradient 0
-                assert got.abs().max() < 1e-4 * (1 + ref.abs().max())
+                assert got.abs().max() < tol * (1 + ref.abs().max())
                 continue
-            assert _rel(got, ref) < 1e-4, (name, t)
+            assert _rel(got, ref) < tol, (name, t)
 
 
 def _decoder_stage_case(cfg, N, h, w, with_gate, with_disp):
@@ -167,7 +171,8 @@ def _decoder_stage_case(cfg, N, h, w, with_gate, with_disp):
 
 @pytest.mark.parametrize('with_gate,with_disp,fC', [(False, False, 256), (True, True, 64),
                                                       (True, True, 3)])
-def test_decoder_stage(with_gate, with_disp, fC):
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_decoder_stage(with_gate, with_disp, fC, dtype):
     from oracle.model import decoder_stage
     cfg = dict(in_channels=64, feature_in_channels=fC, skip_in_channels=64,
                upsample_channels=16, out_channels=32, skip_out_channels=32,
@@ -188,28 +193,29 @@ def test_decoder_stage(with_gate, with_disp, fC):
 
     from umamd.functional import image_to_nhwc
     sd = st.to(DEV)
-    xd = _nhwc(x).requires_grad_(True)
-    fd = image_to_nhwc(f.to(DEV), torch.float32) if fC % 8 else _nhwc(f)
+    xd = _nhwc(x).to(dtype).requires_grad_(True)
+    fd = image_to_nhwc(f.to(DEV), dtype) if fC % 8 else _nhwc(f).to(dtype)
     fd.requires_grad_(fC % 8 == 0)
-    skd = _nhwc(sk).requires_grad_(True)
+    skd = _nhwc(sk).to(dtype).requires_grad_(True)
     gated = gate.to(DEV).requires_grad_(True) if gate is not None else None
     dd = _nhwc(d).requires_grad_(True) if d is not None else None
     out_d, (u1, s), disp_d = sd._fwd(xd, fd, (skd, gated) if gated is not None else skd, dd,
                                      0.3)
-    skip_d = u1 * s[:, None, None, :]
-    ((out_d * _nhwc(go)).sum() + (skip_d * _nhwc(gs)).sum() +
+    skip_d = u1.float() * s[:, None, None, :]
+    ((out_d.float() * _nhwc(go)).sum() + (skip_d * _nhwc(gs)).sum() +
      (disp_d * _nhwc(gd)).sum()).backward()
-    assert _rel(_nchw(out_d), out_r) < 1e-4
-    assert _rel(_nchw(skip_d), skip_r) < 1e-4
-    assert _rel(_nchw(disp_d), disp_r) < 1e-4
-    assert _rel(_nchw(xd.grad), xr.grad) < 1e-3
-    assert _rel(_nchw(skd.grad), skr.grad) < 1e-3
+    t = 1e-3 if dtype == torch.float32 else 1e-1
+    assert _rel(_nchw(out_d), out_r) < t / 10
+    assert _rel(_nchw(skip_d), skip_r) < t / 10
+    assert _rel(_nchw(disp_d), disp_r) < t / 10
+    assert _rel(_nchw(xd.grad), xr.grad) < t
+    assert _rel(_nchw(skd.grad), skr.grad) < t
     if fC % 8 == 0:
-        assert _rel(_nchw(fd.grad), fr.grad) < 1e-3
+        assert _rel(_nchw(fd.grad), fr.grad) < t
     if dd is not None:
-        assert _rel(_nchw(dd.grad), dr.grad) < 1e-3
+        assert _rel(_nchw(dd.grad), dr.grad) < t
     if gated is not None:
-        assert _rel(gated.grad, gr.grad) < 1e-3
+        assert _rel(gated.grad, gr.grad) < t
     sdict = dict(sd.named_parameters())
     for k, v in P.items():
         if not (v.is_floating_point() and 'running' not in k) or v.grad is None:
@@ -218,7 +224,7 @@ def test_decoder_stage(with_gate, with_disp, fC):
         if k.endswith('layers.0.layers.0.bias') and 'disp' not in k:
             continue  # pre-BN bias: true gradient 0
         assert got is not None, k
-        assert _rel(got, v.grad) < 2e-3, k
+        assert _rel(got, v.grad) < 2 * t, k
 
 
 def test_pyramid_and_warp_goldens():
@@ -256,3 +262,20 @@ def test_adam_matches_torch():
         o2.step()
     for a, b in zip(pd, pr):
         assert _rel(a, b) < 1e-6
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [(8, 32, 7, 2, 64, 128), (32, 32, 7, 1, 32, 64),
+                                  (64, 64, 3, 1, 32, 64)])
+def test_conv_large(dtype, case):
+    from umamd import functional as U
+    from umamd._lib import PAD_ZERO
+    Cin, Cout, k, stride, H, W = case
+    conv = nn.Conv2d(Cin, Cout, k, stride)
+    bn = nn.BatchNorm2d(Cout)
+    x = torch.rand(2, Cin, H, W)
+    yr = F.elu(bn(conv(F.pad(x, ((k - 1) // 2,) * 4))))
+    yd = U.conv_bn_elu(_nhwc(x).to(dtype), conv.to(DEV), bn.to(DEV), (k - 1) // 2, PAD_ZERO)
+    err = _rel(_nchw(yd), yr)
+    print(f'conv_large {case} {dtype}: {err:.3e}')
+    assert err < (1e-4 if dtype == torch.float32 else 5e-2)

@@ -7,6 +7,10 @@
 //   backward: um_bn_elu_bwd_reduce (sum dz, sum dz*xhat) -> um_bn_stats_reduce
 //             -> [all-reduce] -> um_bn_bwd_coeffs (dgamma/dbeta + dx coeffs)
 //             -> um_bn_elu_bwd_apply (dy)
+// The pre-BN conv output y is always f32 (also in bf16 mode): BN subtracts a
+// batch mean that can be much larger than the batch std, so a bf16 y would
+// amplify its rounding error by mean/std (measured 4e-2 after one node,
+// 40 % after a stage).  a / da / dy use the activation dtype.
 // Semantics follow torch.nn.BatchNorm2d (reference model/layers/encoder.py:43,
 // model/layers/decoder.py:82): biased variance for normalisation, unbiased
 // for running_var, eps 1e-5, momentum 0.1.  ELU alpha = 1 (nn.ELU, reference
@@ -63,7 +67,7 @@ __global__ void coeffs_kernel(const double* __restrict__ st, double count, int C
 }
 
 template <typename T>
-__global__ void bn_elu_fwd_kernel(const T* __restrict__ y, int ldy, long M, int C,
+__global__ void bn_elu_fwd_kernel(const float* __restrict__ y, int ldy, long M, int C,
                                   const float* __restrict__ scale, const float* __restrict__ shift,
                                   T* __restrict__ a, int lda, int apply_elu) {
   // 8 channels per thread (C % 8 == 0)
@@ -87,7 +91,7 @@ __global__ void bn_elu_fwd_kernel(const T* __restrict__ y, int ldy, long M, int 
 // Backward reduce: dz = (da + add[n][c]) * ELU'(z), z = y*scale + shift,
 // xhat = (y - mean) * invstd; partial sums per block [blk][C][2].
 template <typename T>
-__global__ void bn_elu_bwd_reduce_kernel(const T* __restrict__ da, int ldda, const T* __restrict__ y,
+__global__ void bn_elu_bwd_reduce_kernel(const T* __restrict__ da, int ldda, const float* __restrict__ y,
                                          int ldy, long M, int C, long HW,
                                          const float* __restrict__ mean,
                                          const float* __restrict__ invstd,
@@ -174,7 +178,7 @@ __global__ void bwd_coeffs_kernel(const double* __restrict__ st, double count, i
 
 template <typename T>
 __global__ void bn_elu_bwd_apply_kernel(const T* __restrict__ da, int ldda,
-                                        const T* __restrict__ y, int ldy, long M, int C, long HW,
+                                        const float* __restrict__ y, int ldy, long M, int C, long HW,
                                         const float* __restrict__ mean,
                                         const float* __restrict__ invstd,
                                         const float* __restrict__ scale,
@@ -243,7 +247,7 @@ int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float*
   UM_CHECK_ARG(C % 8 == 0 && ldy % 8 == 0 && lda % 8 == 0, "um_bn_elu_fwd: C/ld not multiple of 8");
   const int g = grid_for(M * C / 8);
   if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)y,
+    hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const float*)y,
                        ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu);
   else
     hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)y, ldy,
@@ -263,7 +267,7 @@ int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int 
   const size_t shm = 256 * 16 * sizeof(float);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
-                       (const bf16_t*)da, ldda, (const bf16_t*)y, ldy, M, C, HW, mean, invstd,
+                       (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
                        scale, shift, add_nc, apply_elu, parts, BWD_ROWS);
   else
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), shm, st,
@@ -291,7 +295,7 @@ int um_bn_elu_bwd_apply(int dtype, long M, int C, long HW, const void* da, int l
   const int g = grid_for(M * C / 8);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, st,
-                       (const bf16_t*)da, ldda, (const bf16_t*)y, ldy, M, C, HW, mean, invstd,
+                       (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
                        scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy);
   else
     hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, st,

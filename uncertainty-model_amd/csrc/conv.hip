@@ -591,8 +591,7 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
   a.epilogue = epilogue; a.accumulate = 0;
   a.out_f32 = (ydtype == UM_F32);
   a.epi_scale = epi_scale; a.residual = residual; a.ldr = ldr; a.stats = stats;
-  UM_CHECK_ARG(ydtype == dtype || epilogue == UM_EPI_SIGMOID_SCALE || dtype == UM_F32,
-               "um_conv2d_fwd: ydtype must match dtype");
+  UM_CHECK_ARG(ydtype == dtype || ydtype == UM_F32, "um_conv2d_fwd: ydtype must be dtype or f32");
   if (a.M == 0) return UM_OK;
   return dtype == UM_BF16 ? dispatch_conv<bf16_t, MODE_FWD>(a, st)
                           : dispatch_conv<float, MODE_FWD>(a, st);

@@ -184,19 +184,21 @@ class ConvBNELUFn(torch.autograd.Function):
             nparts = query('um_conv_stats_parts', M, K)
             parts = torch.empty((nparts, K, 2), dtype=torch.float32, device=dev)
             y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
+                          out_dtype=torch.float32,
                           epi=L.EPI_STATS if training else L.EPI_NONE, stats=parts)
             mean, invstd, scale, shift = _bn_forward_coeffs(parts, nparts, K, M, bn, sync,
                                                             training, dev)
         else:  # ConvELUBlock(batch_norm=False): identity normalisation
             sync = None
             training = False
-            y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode)
+            y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
+                          out_dtype=torch.float32)
             mean = torch.zeros(K, dtype=torch.float32, device=dev)
             shift = mean
             invstd = torch.ones(K, dtype=torch.float32, device=dev)
             scale = invstd
-        a = torch.empty_like(y)
-        call('um_bn_elu_fwd', _dt(y), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
+        a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y is f32 (pre-BN)
+        call('um_bn_elu_fwd', _dt(a), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
              int(spec.elu))
         outs = [a]
         se = None
@@ -225,7 +227,10 @@ class ConvBNELUFn(torch.autograd.Function):
         spec = ctx.spec
         M = N * P * Q
         dev = y.device
-        da = da.contiguous() if da is not None else torch.zeros_like(y)
+        adt = x.dtype
+        da = da.contiguous() if da is not None else torch.zeros(y.shape, dtype=adt, device=dev)
+        if da.dtype != adt:
+            da = da.to(adt)
         add_nc = None
         dw1 = dw2 = None
         if ctx.se is not None and ds is not None:
@@ -245,7 +250,7 @@ class ConvBNELUFn(torch.autograd.Function):
         if ctx.has_bn:
             nb = query('um_bn_bwd_parts', M)
             parts = torch.empty((nb, K, 2), dtype=torch.float32, device=dev)
-            call('um_bn_elu_bwd_reduce', _dt(y), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
+            call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
                  ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(parts))
             st = torch.empty((K, 2), dtype=torch.float64, device=dev)
             call('um_bn_stats_reduce', ptr(parts), nb, K, ptr(st))
@@ -266,8 +271,8 @@ class ConvBNELUFn(torch.autograd.Function):
             k3.zero_()
             if gamma is not None and spec.bn is not None:
                 raise NotImplementedError('backward through an eval-mode BatchNorm')
-        dy = torch.empty_like(y)
-        call('um_bn_elu_bwd_apply', _dt(y), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
+        dy = torch.empty(y.shape, dtype=adt, device=dev)
+        call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
              ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1), ptr(k2),
              ptr(k3), ptr(dy), K)
         dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode)

@@ -59,6 +59,7 @@ class _WarpFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, disp, img, sign: float):
         L.require_device(img)
+        ctx.set_materialize_grads(False)
         imgc = _f32c(img)
         N, C, H, W = imgc.shape
         d = disp.detach()
@@ -76,6 +77,8 @@ class _WarpFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if g is None:
+            return None, None, None
         raise NotImplementedError(
             'gradient through reconstruct() is provided by TukraUncertaintyLoss directly '
             '(fused); a standalone warp backward (adversarial path) is not implemented yet')
@@ -156,5 +159,8 @@ class TukraLossFn(torch.autograd.Function):
 
 
 def tukra_loss(cfg: dict, preds, pyramid, recon):
+    """The fused backward differentiates through the warp itself, so the
+    recon tensors enter as plain (detached) data."""
     n = len(preds)
-    return TukraLossFn.apply(cfg, n, *preds, *pyramid, *recon)
+    return TukraLossFn.apply(cfg, n, *preds, *[p.detach() for p in pyramid],
+                             *[r.detach() for r in recon])
