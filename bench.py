@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Benchmark: stereo-pairs/sec of the self-supervised depth+uncertainty
+training step (BASELINE.json metric) at 256x512, batch 8 per GPU, bayesian
+error loss, bf16 compute (BASELINE config 2 / config 4 per-GPU shape).
+
+A step = reference train/train.py:116-129 on synthetic device-resident U[0,1)
+pairs: image pyramid -> model forward -> reconstruct -> 4-scale loss ->
+backward -> Adam.  N>1: one process per GPU (torchrun), DDP over RCCL with
+SyncBatchNorm semantics (reference parallel_main.py:156-158), weak scaling.
+
+Prints ONE JSON line (rank 0) with a ``roofline`` object for the dominant
+kernel (measured with HIP events around its launches on the launch stream)
+and a ``cpu_baseline`` (the oracle's CPU train step on a bounded sample,
+rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(REPO, 'uncertainty-model_amd'), REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import yaml  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA
+F32_PEAK_TFLOPS = 157.3     # f32 MFMA
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=8, help='pairs per GPU')
+    ap.add_argument('--height', type=int, default=256)
+    ap.add_argument('--width', type=int, default=512)
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--loss-type', default='bayesian', choices=['l1', 'bayesian', 'log_bayesian'])
+    ap.add_argument('--config', default='config.yml')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--cpu-sample-batch', type=int, default=2)
+    ap.add_argument('--cpu-sample-steps', type=int, default=2)
+    return ap.parse_args()
+
+
+def load_cfg(path, loss_type):
+    with open(os.path.join(REPO, path)) as f:
+        cfg = yaml.safe_load(f)
+    lg = cfg['model']['encoder'].get('load_graph')
+    if lg and not os.path.isabs(lg):
+        cfg['model']['encoder']['load_graph'] = os.path.join(REPO, lg)
+    cfg['loss']['error_loss_config']['loss_type'] = loss_type
+    return cfg
+
+
+def build(cfg, dtype, device, world):
+    import model as M
+    from train.loss import TukraUncertaintyLoss
+    from umamd.optim import Adam
+    torch.manual_seed(0)
+    m = M.RandomlyConnectedModel(**cfg['model'], dtype=dtype).to(device).train()
+    if world > 1:
+        m = torch.nn.SyncBatchNorm.convert_sync_batchnorm(m)
+        m = torch.nn.parallel.DistributedDataParallel(m, device_ids=[device.index])
+    lf = TukraUncertaintyLoss(**cfg['loss'])
+    opt = Adam(m.parameters(), 1e-4)
+    return m, lf, opt
+
+
+def step(m, lf, opt, left, right, scale):
+    import train.utils as u
+    images = torch.cat([left, right], 1)
+    pyr = u.scale_pyramid(images, 4)
+    opt.zero_grad(set_to_none=True)
+    d = m(left, scale)
+    dl, el = lf(pyr, d, u.reconstruct_pyramid(d, pyr), 0, None)
+    (dl + el).backward()
+    opt.step()
+    return dl, el
+
+
+# ------------------------------------------------------------- roofline ----
+def loss_bwd_bytes(N, H, W):
+    """Algorithmic HBM bytes of one fused loss-backward launch at an h x w
+    scale: per pixel 6 f32 image reads + 6 f32 recon reads (the SSIM stencil)
+    + 4 f32 prediction reads + 2 f32 error-map reads + 4 f32 gradient writes.
+    (SURVEY 8d prices the fused stack at 56 B/px all-f32 without the recon;
+    this kernel also reads the saved recon and error map.)"""
+    return N * H * W * 4 * (6 + 6 + 4 + 2 + 4)
+
+
+def conv_flops(args):
+    # um_conv2d_fwd(dtype, N, H, W, C, ldx, x, wf, bias, K, R, stride, pad, mode, P, Q, ...)
+    N, C, K, R, P, Q = args[1], args[4], args[9], args[10], args[14], args[15]
+    return 2.0 * N * P * Q * K * R * R * C
+
+
+def measure_roofline(m, lf, opt, left, right, scale, dtype):
+    """Time every launch of the candidate kernels with HIP events on the
+    launch stream; report the one with the largest total time."""
+    from umamd import _lib
+    rec = _lib.Recorder({'um_conv2d_fwd', 'um_loss_bwd_scale'})
+    with rec:
+        step(m, lf, opt, left, right, scale)
+    torch.cuda.synchronize()
+    groups = {}
+    for name, args, ms in rec.results():
+        groups.setdefault(name, []).append((args, ms))
+    tot = {k: sum(ms for _, ms in v) for k, v in groups.items()}
+    dom = max(tot, key=tot.get)
+    items = groups[dom]
+    avg_ms = tot[dom] / len(items)
+    if dom == 'um_loss_bwd_scale':
+        # args: img, rec, pred, pld, N, H, W, ...
+        byts = sum(loss_bwd_bytes(a[4], a[5], a[6]) for a, _ in items) / len(items)
+        ach = byts / (avg_ms * 1e-3) / 1e9
+        return {'kernel': 'loss_bwd_kernel (um_loss_bwd_scale)', 'bound': 'hbm',
+                'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': round(ach / HBM_PEAK_GBS, 4), 'traffic': None,
+                'launches_per_step': len(items), 'avg_launch_ms': round(avg_ms, 4),
+                'all_kernels_ms': {k: round(v, 3) for k, v in tot.items()}}
+    flops = sum(conv_flops(a) for a, _ in items) / len(items)
+    ach = flops / (avg_ms * 1e-3) / 1e12
+    peak = BF16_PEAK_TFLOPS if dtype == 'bf16' else F32_PEAK_TFLOPS
+    return {'kernel': 'conv_gemm_kernel fwd (um_conv2d_fwd)', 'bound': 'mfma',
+            'achieved': round(ach, 2), 'peak': peak, 'unit': 'TFLOP/s',
+            'frac': round(ach / peak, 4), 'traffic': None,
+            'launches_per_step': len(items), 'avg_launch_ms': round(avg_ms, 4),
+            'all_kernels_ms': {k: round(v, 3) for k, v in tot.items()}}
+
+
+# --------------------------------------------------------- CPU baseline ----
+def cpu_baseline(cfg, H, W, batch, steps):
+    """Oracle (plain-PyTorch CPU restatement, pinned to reference goldens)
+    train step on the host cores; bounded sample."""
+    from oracle import model as OM, step as OS
+    threads = os.cpu_count() or 1
+    threads = min(threads, 64)
+    torch.set_num_threads(threads)
+    graphs = OM.load_stage_graphs(cfg['model']['encoder'])
+    P = OS.formula_state_dict(OS.param_specs(cfg['model'], graphs))
+    g = torch.Generator().manual_seed(1234)
+    left = torch.rand(batch, 3, H, W, generator=g)
+    right = torch.rand(batch, 3, H, W, generator=g)
+    st = {}
+    OS.train_step(P, left, right, 0.3, cfg['model'], cfg['loss'], graphs, st)  # warm-up
+    best = float('inf')
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        OS.train_step(P, left, right, 0.3, cfg['model'], cfg['loss'], graphs, st)
+        best = min(best, time.perf_counter() - t0)
+    cpu = ''
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    cpu = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {'value': round(batch / best, 3), 'unit': 'stereo-pairs/sec', 'cores': threads,
+            'kind': 'port',
+            'sample': f'oracle train step (fp32, {cfg["loss"]["error_loss_config"]["loss_type"]}) '
+                      f'B={batch} {H}x{W}, 1 warm-up + best of {steps}; {cpu}'}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl', init_method='env://')
+    torch.cuda.set_device(local)
+    device = torch.device('cuda', local)
+    cfg = load_cfg(a.config, a.loss_type)
+    m, lf, opt = build(cfg, a.dtype, device, world)
+    g = torch.Generator(device='cpu').manual_seed(1234 + rank)
+    left = torch.rand(a.batch, 3, a.height, a.width, generator=g).to(device)
+    right = torch.rand(a.batch, 3, a.height, a.width, generator=g).to(device)
+    scale = 0.3  # adjust_disparity(0)
+
+    for _ in range(a.warmup):
+        step(m, lf, opt, left, right, scale)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        dl, el = step(m, lf, opt, left, right, scale)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    losses = (float(dl), float(el))
+
+    roof = None
+    if not a.no_roofline:
+        roof = measure_roofline(m, lf, opt, left, right, scale, a.dtype)
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, a.height, a.width, a.cpu_sample_batch, a.cpu_sample_steps)
+
+    if rank == 0:
+        total = a.batch * world * a.steps
+        out = {
+            'metric': 'stereo-pairs/sec (train step) at 256x512, 1/2/4/8 MI355X; loss delta vs ref',
+            'value': round(total / elapsed, 2),
+            'unit': 'stereo-pairs/sec',
+            'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+            'ms_per_step': round(elapsed / a.steps * 1e3, 3),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': a.dtype, 'data': 'synthetic U[0,1) stereo pairs (device-resident), '
+                                      'formula-free random init (torch.manual_seed(0))',
+            'config': {'workload': f'depth+uncertainty train step (BASELINE config '
+                                   f'{"2" if world == 1 else "4"}): fwd+4-scale loss+bwd+Adam',
+                       'global_batch': a.batch * world, 'per_gpu_batch': a.batch,
+                       'height': a.height, 'width': a.width, 'loss': a.loss_type,
+                       'parallelism': f'dp{world}' + ('+syncbn' if world > 1 else ''),
+                       'graph': 'config.yml (nodes=5, K5 stage graphs)'},
+            'final_losses': {'disp': round(losses[0], 5), 'error': round(losses[1], 5)},
+            'roofline': roof,
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

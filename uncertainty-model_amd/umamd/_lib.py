@@ -124,10 +124,45 @@ def ptr(t) -> Optional[int]:
     return t.data_ptr()
 
 
+class Recorder:
+    """Context manager timing the launches of selected C-ABI entries with
+    HIP events recorded on the launch stream (torch's current stream)."""
+
+    _active = None
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.items = []
+
+    def __enter__(self):
+        Recorder._active = self
+        return self
+
+    def __exit__(self, *exc):
+        Recorder._active = None
+
+    def results(self):
+        """[(name, args, ms)] -- synchronises on the events."""
+        out = []
+        for name, args, e0, e1 in self.items:
+            e1.synchronize()
+            out.append((name, args, e0.elapsed_time(e1)))
+        return out
+
+
 def call(name: str, *args):
     """Call a C-ABI entry; the trailing stream argument is appended."""
     fn = getattr(lib(), name)
-    rc = fn(*args, stream())
+    rec = Recorder._active
+    if rec is not None and name in rec.names:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = fn(*args, stream())
+        e1.record()
+        rec.items.append((name, args, e0, e1))
+    else:
+        rc = fn(*args, stream())
     if rc != 0:
         msg = lib().um_last_error().decode(errors='replace')
         raise UmamdError(f'{name} failed ({rc}): {msg}')
