@@ -48,6 +48,8 @@ def parse():
     ap.add_argument('--config', default='config.yml')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--no-graph', action='store_true',
+                    help='eager launches instead of the captured HIP graph (N=1)')
     ap.add_argument('--cpu-sample-batch', type=int, default=2)
     ap.add_argument('--cpu-sample-steps', type=int, default=2)
     return ap.parse_args()
@@ -190,15 +192,25 @@ def main():
     right = torch.rand(a.batch, 3, a.height, a.width, generator=g).to(device)
     scale = 0.3  # adjust_disparity(0)
 
-    for _ in range(a.warmup):
-        step(m, lf, opt, left, right, scale)
+    use_graph = world == 1 and not a.no_graph
+    if use_graph:
+        from train.graph import CapturedTrainStep
+        # the capture's own eager warm-up steps count toward W; one replay warms the graph
+        cap = CapturedTrainStep(m, lf, opt, left, right, scale, warmup=max(1, a.warmup - 1))
+        run = cap
+        run()
+    else:
+        def run():
+            return step(m, lf, opt, left, right, scale)
+        for _ in range(a.warmup):
+            run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        dl, el = step(m, lf, opt, left, right, scale)
+        dl, el = run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -233,6 +245,7 @@ def main():
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch,
                        'height': a.height, 'width': a.width, 'loss': a.loss_type,
                        'parallelism': f'dp{world}' + ('+syncbn' if world > 1 else ''),
+                       'launch': 'hip-graph' if use_graph else 'eager',
                        'graph': 'config.yml (nodes=5, K5 stage graphs)'},
             'final_losses': {'disp': round(losses[0], 5), 'error': round(losses[1], 5)},
             'roofline': roof,

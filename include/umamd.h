@@ -78,6 +78,16 @@ int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* 
 int um_conv_wgrad_reduce(const float* slabs, int splits, int K, int Kreal, int R, int C,
                          int Creal, float* dw, int accumulate, hipStream_t stream);
 
+/* segment variants: reference input channels [src0[i], src0[i]+len[i]) are
+ * placed at packed channels [dst0[i], ...) (host arrays, nseg <= 4); the rest
+ * of the packed channels are zero.  Keeps concat sources 8-channel aligned. */
+int um_conv_wgrad_reduce_seg(const float* slabs, int splits, int K, int Kreal, int R, int C,
+                             int Creal, float* dw, int accumulate, int nseg, const int* src0,
+                             const int* dst0, const int* len, hipStream_t stream);
+int um_pack_weight_seg(int dtype, const float* w, int K, int Creal, int R, int C, void* wf,
+                       void* wT, int ldT, int nseg, const int* src0, const int* dst0,
+                       const int* len, hipStream_t stream);
+
 /* repack f32 NCHW weight [K][Creal][R][R] -> wf [K][R][R][C] (row stride ldf
  * elements) and wT [C][R][R][ldT] (column offset applied by the caller); C >= Creal, zero fill */
 int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C,
@@ -113,11 +123,13 @@ int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamm
                      const float* invstd, const double* stats_local, float* dgamma,
                      float* dbeta, int accumulate, float* k1, float* k2, float* k3,
                      hipStream_t stream);
+/* sum_parts (optional): per-block partial sums of dy, [um_bn_bwd_parts(M)][C]
+ * (the conv-bias gradient, reduced by um_reduce_rows) */
 int um_bn_elu_bwd_apply(int dtype, long M, int C, long HW, const void* da, int ldda,
                         const void* y, int ldy, const float* mean, const float* invstd,
                         const float* scale, const float* shift, const float* add_nc,
                         int apply_elu, const float* k1, const float* k2, const float* k3,
-                        void* dy, int lddy, hipStream_t stream);
+                        void* dy, int lddy, float* sum_parts, hipStream_t stream);
 
 /* ------------------------------------------------------- encoder misc ---
  * NodeBlock merge, reference model/layers/encoder.py:115-124 (F3 index map
@@ -208,6 +220,10 @@ int um_loss_bwd_scale(const float* img, const float* rec, const float* pred, int
 int um_adam_chunk(void);
 int um_adam_step(const void* table, const void* chunks, int nchunks, float lr, float beta1,
                  float beta2, float eps, float weight_decay, int step, hipStream_t stream);
+/* graph-replayable: *dstep += 1 on the device, bias corrections from it; lr from *dlr if non-null */
+int um_adam_step_dev(const void* table, const void* chunks, int nchunks, float lr,
+                     const float* dlr, float beta1, float beta2, float eps, float weight_decay,
+                     int* dstep, hipStream_t stream);
 
 #ifdef __cplusplus
 }

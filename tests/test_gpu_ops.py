@@ -274,8 +274,19 @@ def test_conv_large(dtype, case):
     conv = nn.Conv2d(Cin, Cout, k, stride)
     bn = nn.BatchNorm2d(Cout)
     x = torch.rand(2, Cin, H, W)
-    yr = F.elu(bn(conv(F.pad(x, ((k - 1) // 2,) * 4))))
-    yd = U.conv_bn_elu(_nhwc(x).to(dtype), conv.to(DEV), bn.to(DEV), (k - 1) // 2, PAD_ZERO)
-    err = _rel(_nchw(yd), yr)
-    print(f'conv_large {case} {dtype}: {err:.3e}')
-    assert err < (1e-4 if dtype == torch.float32 else 5e-2)
+    xr = x.clone().requires_grad_(True)
+    cr, br = nn.Conv2d(Cin, Cout, k, stride), nn.BatchNorm2d(Cout)
+    cr.load_state_dict(conv.state_dict())
+    br.load_state_dict(bn.state_dict())
+    yr = F.elu(br(cr(F.pad(xr, ((k - 1) // 2,) * 4))))
+    g = torch.randn_like(yr)
+    (yr * g).sum().backward()
+    cd, bd = conv.to(DEV), bn.to(DEV)
+    xd = _nhwc(x).to(dtype).requires_grad_(True)
+    yd = U.conv_bn_elu(xd, cd, bd, (k - 1) // 2, PAD_ZERO)
+    (yd.float() * _nhwc(g)).sum().backward()
+    errs = [_rel(_nchw(yd), yr), _rel(_nchw(xd.grad), xr.grad), _rel(cd.weight.grad, cr.weight.grad),
+            _rel(cd.bias.grad, cr.bias.grad) if cr.bias.grad.abs().max() > 1e-3 else 0.0]
+    print(f'conv_large {case} {dtype}: y {errs[0]:.3e} dx {errs[1]:.3e} dw {errs[2]:.3e}')
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert errs[0] < tol and errs[1] < tol * 2 and errs[2] < tol * 2, errs

@@ -20,7 +20,14 @@ constexpr int CHUNK = 4096;
 
 __global__ void adam_kernel(const AdamEntry* __restrict__ tab, const int2* __restrict__ chunks,
                             int nchunks, float lr_bc1, float b1, float b2, float inv_sqrt_bc2,
-                            float eps, float wd) {
+                            float eps, float wd, const int* __restrict__ dstep,
+                            const float* __restrict__ dlr) {
+  if (dstep != nullptr) {  // graph-replayable: step count (and lr) live on the device
+    const int step = *dstep;
+    const float lr = dlr ? *dlr : lr_bc1;
+    lr_bc1 = (float)(lr / (1.0 - pow((double)b1, step)));
+    inv_sqrt_bc2 = (float)(1.0 / sqrt(1.0 - pow((double)b2, step)));
+  }
   for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
     const int2 ch = chunks[ci];  // (entry, chunk index within entry)
     const AdamEntry e = tab[ch.x];
@@ -40,6 +47,8 @@ __global__ void adam_kernel(const AdamEntry* __restrict__ tab, const int2* __res
   }
 }
 
+__global__ void inc_kernel(int* step) { *step += 1; }
+
 }  // namespace
 
 extern "C" {
@@ -57,7 +66,23 @@ int um_adam_step(const void* table, const void* chunks, int nchunks, float lr, f
   if (blocks == 0) return UM_OK;
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, st, (const AdamEntry*)table,
                      (const int2*)chunks, nchunks, (float)(lr / bc1), beta1, beta2,
-                     (float)(1.0 / sqrt(bc2)), eps, weight_decay);
+                     (float)(1.0 / sqrt(bc2)), eps, weight_decay, nullptr, nullptr);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+// Graph-replayable variant: increments the device step counter, then updates
+// with bias corrections computed from it; lr read from dlr (device) if given.
+int um_adam_step_dev(const void* table, const void* chunks, int nchunks, float lr,
+                     const float* dlr, float beta1, float beta2, float eps, float weight_decay,
+                     int* dstep, hipStream_t st) {
+  UM_CHECK_ARG(dstep != nullptr, "um_adam_step_dev: step counter");
+  hipLaunchKernelGGL(inc_kernel, dim3(1), dim3(1), 0, st, dstep);
+  const int blocks = nchunks < 8192 ? nchunks : 8192;
+  if (blocks == 0) return UM_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, st, (const AdamEntry*)table,
+                     (const int2*)chunks, nchunks, lr, beta1, beta2, 1.f, eps, weight_decay,
+                     dstep, dlr);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

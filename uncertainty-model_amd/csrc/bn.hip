@@ -26,9 +26,17 @@ __global__ void stats_reduce_kernel(const float* __restrict__ parts, int nparts,
   const int lane = threadIdx.x & 63;
   if (c >= C) return;
   double s = 0.0, q = 0.0;
-  for (int p = lane; p < nparts; p += 64) {
-    s += parts[((long)p * C + c) * 2];
-    q += parts[((long)p * C + c) * 2 + 1];
+  int p = lane;
+  for (; p + 64 < nparts; p += 128) {  // two rows in flight per lane
+    const float2 a = *reinterpret_cast<const float2*>(parts + ((long)p * C + c) * 2);
+    const float2 b = *reinterpret_cast<const float2*>(parts + ((long)(p + 64) * C + c) * 2);
+    s += (double)a.x + (double)b.x;
+    q += (double)a.y + (double)b.y;
+  }
+  for (; p < nparts; p += 64) {
+    const float2 a = *reinterpret_cast<const float2*>(parts + ((long)p * C + c) * 2);
+    s += a.x;
+    q += a.y;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -91,68 +99,55 @@ __global__ void bn_elu_fwd_kernel(const float* __restrict__ y, int ldy, long M, 
 // Backward reduce: dz = (da + add[n][c]) * ELU'(z), z = y*scale + shift,
 // xhat = (y - mean) * invstd; partial sums per block [blk][C][2].
 template <typename T>
-__global__ void bn_elu_bwd_reduce_kernel(const T* __restrict__ da, int ldda, const float* __restrict__ y,
-                                         int ldy, long M, int C, long HW,
-                                         const float* __restrict__ mean,
-                                         const float* __restrict__ invstd,
-                                         const float* __restrict__ scale,
-                                         const float* __restrict__ shift,
-                                         const float* __restrict__ add_nc, int apply_elu,
-                                         float* __restrict__ parts, int rows_per_block) {
-  // block: 256 threads = (256/CG) row lanes x CG channel-groups of 8, looped
-  extern __shared__ float red[];  // [256][2*8]
+__global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
+    const T* __restrict__ da, int ldda, const float* __restrict__ y, int ldy, long M, int C,
+    long HW, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ add_nc, int apply_elu, float* __restrict__ parts,
+    int rows_per_block) {
+  extern __shared__ float red[];  // [256][16]
   const int cg = C / 8;
+  const RowMap rm(cg);
   const long m0 = (long)blockIdx.x * rows_per_block;
   const long m1 = min(M, m0 + rows_per_block);
-  for (int g0 = 0; g0 < cg; g0 += 32) {
-    const int g = g0 + (threadIdx.x & 31);
-    const int rl = threadIdx.x >> 5;  // 8 row lanes
-    float s[8], q[8];
+  for (int g0 = 0; g0 < cg; g0 += rm.G) {
+    const int g = g0 + rm.g;
+    float acc[16];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
-    if (g < cg) {
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    if (rm.active() && g < cg) {
       const int c = g * 8;
       float mu[8], is[8], sc[8], sh[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        mu[e] = mean[c + e]; is[e] = invstd[c + e]; sc[e] = scale[c + e]; sh[e] = shift[c + e];
-      }
-      for (long m = m0 + rl; m < m1; m += 8) {
-        float dv[8], yv[8];
+      load8(mean + c, mu);
+      load8(invstd + c, is);
+      load8(scale + c, sc);
+      load8(shift + c, sh);
+      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+        float dv[8], yv[8], ad[8];
         load8(da + m * ldda + c, dv);
         load8(y + m * ldy + c, yv);
-        const float* ad = add_nc ? add_nc + (m / HW) * C + c : nullptr;
+        if (add_nc) load8(add_nc + (m / HW) * C + c, ad);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float d = dv[e] + (ad ? ad[e] : 0.f);
+          float d = dv[e] + (add_nc ? ad[e] : 0.f);
           if (apply_elu) {
             const float z = yv[e] * sc[e] + sh[e];
             d = z > 0.f ? d : d * __expf(z);
           }
-          s[e] += d;
-          q[e] += d * (yv[e] - mu[e]) * is[e];
+          acc[e] += d;
+          acc[8 + e] += d * (yv[e] - mu[e]) * is[e];
         }
       }
     }
+    lane_reduce<16>(red, rm, acc);
+    if (rm.lane == 0 && g < cg) {
+      float* o = parts + ((long)blockIdx.x * C + g * 8) * 2;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[threadIdx.x * 16 + e] = s[e];
-      red[threadIdx.x * 16 + 8 + e] = q[e];
-    }
-    __syncthreads();
-    if (threadIdx.x < 32 && g < cg) {
       for (int e = 0; e < 8; ++e) {
-        float ts = 0.f, tq = 0.f;
-        for (int r = 0; r < 8; ++r) {
-          ts += red[(r * 32 + threadIdx.x) * 16 + e];
-          tq += red[(r * 32 + threadIdx.x) * 16 + 8 + e];
-        }
-        float* o = parts + ((long)blockIdx.x * C + g * 8 + e) * 2;
-        o[0] = ts;
-        o[1] = tq;
+        o[2 * e] = acc[e];
+        o[2 * e + 1] = acc[8 + e];
       }
     }
-    __syncthreads();
   }
 }
 
@@ -176,42 +171,75 @@ __global__ void bwd_coeffs_kernel(const double* __restrict__ st, double count, i
   if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)sl[2 * c];
 }
 
+// dy = k1*(dz - k2 - xhat*k3); optional per-block partial sums of dy
+// ([blk][C], the conv-bias gradient) written to sum_parts.
 template <typename T>
-__global__ void bn_elu_bwd_apply_kernel(const T* __restrict__ da, int ldda,
-                                        const float* __restrict__ y, int ldy, long M, int C, long HW,
-                                        const float* __restrict__ mean,
-                                        const float* __restrict__ invstd,
-                                        const float* __restrict__ scale,
-                                        const float* __restrict__ shift,
-                                        const float* __restrict__ add_nc, int apply_elu,
-                                        const float* __restrict__ k1, const float* __restrict__ k2,
-                                        const float* __restrict__ k3, T* __restrict__ dy,
-                                        int lddy) {
+__global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
+    const T* __restrict__ da, int ldda, const float* __restrict__ y, int ldy, long M, int C,
+    long HW, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ add_nc, int apply_elu, const float* __restrict__ k1,
+    const float* __restrict__ k2, const float* __restrict__ k3, T* __restrict__ dy, int lddy,
+    float* __restrict__ sum_parts, int rows_per_block) {
+  extern __shared__ float red[];  // [256][8]
   const int cg = C / 8;
-  const long total = M * cg;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const long m = i / cg;
-    const int c = (int)(i - m * cg) * 8;
-    float dv[8], yv[8], o[8];
-    load8(da + m * ldda + c, dv);
-    load8(y + m * ldy + c, yv);
-    const float* ad = add_nc ? add_nc + (m / HW) * C + c : nullptr;
+  const RowMap rm(cg);
+  const long m0 = (long)blockIdx.x * rows_per_block;
+  const long m1 = min(M, m0 + rows_per_block);
+  for (int g0 = 0; g0 < cg; g0 += rm.G) {
+    const int g = g0 + rm.g;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (rm.active() && g < cg) {
+      const int c = g * 8;
+      // dy = A*dz + B*y + D  with A = k1, B = -k1*k3*invstd, D = -k1*k2 + k1*k3*mean*invstd
+      float sc[8], sh[8], A[8], B[8], D[8];
+      {
+        float mu[8], is[8], a1[8], a2[8], a3[8];
+        load8(mean + c, mu);
+        load8(invstd + c, is);
+        load8(k1 + c, a1);
+        load8(k2 + c, a2);
+        load8(k3 + c, a3);
+        load8(scale + c, sc);
+        load8(shift + c, sh);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float d = dv[e] + (ad ? ad[e] : 0.f);
-      if (apply_elu) {
-        const float z = yv[e] * scale[c + e] + shift[c + e];
-        d = z > 0.f ? d : d * __expf(z);
+        for (int e = 0; e < 8; ++e) {
+          A[e] = a1[e];
+          B[e] = -a1[e] * a3[e] * is[e];
+          D[e] = -a1[e] * a2[e] + a1[e] * a3[e] * mu[e] * is[e];
+        }
       }
-      const float xh = (yv[e] - mean[c + e]) * invstd[c + e];
-      o[e] = k1[c + e] * (d - k2[c + e] - xh * k3[c + e]);
+      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+        float dv[8], yv[8], ad[8], o[8];
+        load8(da + m * ldda + c, dv);
+        load8(y + m * ldy + c, yv);
+        if (add_nc) load8(add_nc + (m / HW) * C + c, ad);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float d = dv[e] + (add_nc ? ad[e] : 0.f);
+          if (apply_elu) {
+            const float z = yv[e] * sc[e] + sh[e];
+            d = z > 0.f ? d : d * __expf(z);
+          }
+          o[e] = A[e] * d + B[e] * yv[e] + D[e];
+        }
+        store8(dy + m * lddy + c, o);
+        if (sum_parts) {
+          float r[8];
+          load8_rounded(o, r, dy);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += r[e];
+        }
+      }
     }
-    store8(dy + m * lddy + c, o);
+    if (sum_parts) {
+      lane_reduce<8>(red, rm, acc);
+      if (rm.lane == 0 && g < cg) store8(sum_parts + (long)blockIdx.x * C + g * 8, acc);
+    }
   }
 }
 
-constexpr int BWD_ROWS = 512;
+constexpr int BWD_ROWS = 256;
 
 inline int grid_for(long n) {
   long b = (n + 255) / 256;
@@ -263,6 +291,7 @@ int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int 
                          const float* scale, const float* shift, const float* add_nc,
                          int apply_elu, float* parts, hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_reduce: C %% 8");
+  UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_reduce: C %% 8");
   const int blocks = um_bn_bwd_parts(M);
   const size_t shm = 256 * 16 * sizeof(float);
   if (dtype == UM_BF16)
@@ -290,17 +319,20 @@ int um_bn_elu_bwd_apply(int dtype, long M, int C, long HW, const void* da, int l
                         const void* y, int ldy, const float* mean, const float* invstd,
                         const float* scale, const float* shift, const float* add_nc,
                         int apply_elu, const float* k1, const float* k2, const float* k3,
-                        void* dy, int lddy, hipStream_t st) {
+                        void* dy, int lddy, float* sum_parts, hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_apply: C %% 8");
-  const int g = grid_for(M * C / 8);
+  const int blocks = um_bn_bwd_parts(M);
+  const size_t shm = 256 * 8 * sizeof(float);
   if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, st,
+    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
                        (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy);
+                       scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy, sum_parts,
+                       BWD_ROWS);
   else
-    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, st,
+    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, dim3(blocks), dim3(256), shm, st,
                        (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, k1, k2, k3, (float*)dy, lddy);
+                       scale, shift, add_nc, apply_elu, k1, k2, k3, (float*)dy, lddy, sum_parts,
+                       BWD_ROWS);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

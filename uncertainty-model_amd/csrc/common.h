@@ -83,6 +83,16 @@ __device__ __forceinline__ void store8(bf16_t* p, const float* v) {
   *reinterpret_cast<uint4*>(p) = u;
 }
 
+// the values of v as they are stored in a T tensor (bf16 rounding)
+__device__ __forceinline__ void load8_rounded(const float* v, float* r, const float*) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = v[i];
+}
+__device__ __forceinline__ void load8_rounded(const float* v, float* r, const bf16_t*) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = __bfloat162float(__float2bfloat16(v[i]));
+}
+
 // raw 8-element copies (no conversion) used for LDS staging
 template <typename T> struct Raw8;
 template <> struct Raw8<bf16_t> { uint4 v; };
@@ -117,6 +127,36 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
+}
+
+// Row-chunk x channel-group block mapping shared by the backward kernels:
+// thread t owns 8 channels g = t % G (G = min(C/8, 256)) and row lane
+// t / G; a block covers BWD_ROWS rows and all channel groups (looped when
+// C/8 > 256).  Per-channel results are reduced across row lanes in LDS.
+struct RowMap {
+  int G, lanes, g, lane;
+  __device__ RowMap(int cg) {
+    G = cg < 256 ? cg : 256;
+    lanes = 256 / G;
+    g = threadIdx.x % G;
+    lane = threadIdx.x / G;
+  }
+  __device__ bool active() const { return lane < lanes; }
+};
+
+// reduce red[lanes][G][NV] over lanes into thread (lane==0) registers
+template <int NV>
+__device__ __forceinline__ void lane_reduce(float* red, const RowMap& rm, float* v) {
+  if (rm.active())
+#pragma unroll
+    for (int e = 0; e < NV; ++e) red[(rm.lane * rm.G + rm.g) * NV + e] = v[e];
+  __syncthreads();
+  if (rm.lane == 0) {
+    for (int r = 1; r < rm.lanes; ++r)
+#pragma unroll
+      for (int e = 0; e < NV; ++e) v[e] += red[(r * rm.G + rm.g) * NV + e];
+  }
+  __syncthreads();
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }

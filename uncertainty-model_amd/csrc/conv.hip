@@ -22,6 +22,20 @@
 namespace {
 
 constexpr int BK = 32;
+
+// input-channel segments of a packed weight: reference channels
+// [src0, src0+len) live at packed channels [dst0, dst0+len); other packed
+// channels are zero (used to keep concat segments 8-channel aligned)
+constexpr int MAX_SEG = 4;
+struct Segs {
+  int n;
+  int src0[MAX_SEG], dst0[MAX_SEG], len[MAX_SEG];
+};
+__device__ __forceinline__ int seg_src(const Segs& g, int c) {  // packed -> reference, or -1
+  for (int i = 0; i < g.n; ++i)
+    if (c >= g.dst0[i] && c < g.dst0[i] + g.len[i]) return g.src0[i] + c - g.dst0[i];
+  return -1;
+}
 constexpr int LDK = BK + 8;  // padded LDS row (elements)
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1 };
@@ -492,28 +506,186 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
   return UM_OK;
 }
 
+// ---- bf16 weight gradient: both operands pixel-major in memory.  Each thread
+// loads an 8(m) x 8(col) bf16 block (8 x 16 B), transposes it in registers
+// (v_perm) and writes 8 x ds_write_b128 rows of 8 consecutive m, so the MFMA
+// fragments (8 consecutive reduction elements per lane) read with
+// ds_read_b128.  Tile BM (out channels) x 128 (r,s,c) x 64 pixels, 4 waves.
+constexpr int WBK = 64;
+constexpr int WLDK = WBK + 8;
+
+__device__ __forceinline__ void transpose8x8_bf16(const uint4* in, uint4* out) {
+  // in[r] = row r (8 bf16 of consecutive cols); out[e] = col e (8 bf16 of consecutive rows)
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(in);  // w[r*4 + d]
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);              // o[e*4 + q]
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t x = w[(2 * q) * 4 + (e >> 1)], y = w[(2 * q + 1) * 4 + (e >> 1)];
+      o[e * 4 + q] = (e & 1) ? __builtin_amdgcn_perm(y, x, 0x07060302u)
+                             : __builtin_amdgcn_perm(y, x, 0x05040100u);
+    }
+}
+
+template <int BM>
+__global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgradArgs a) {
+  constexpr int BN = 128;
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int A_BLK = BM;       // (BM/8) x (WBK/8)
+  constexpr int B_BLK = BN;       // (BN/8) x (WBK/8)
+  static_assert(A_BLK + B_BLK <= 256, "one 8x8 block per thread");
+  __shared__ __attribute__((aligned(16))) bf16_t sA[BM * WLDK];
+  __shared__ __attribute__((aligned(16))) bf16_t sB[BN * WLDK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bk = blockIdx.x * BM;
+  const int bj = blockIdx.y * BN;
+  const int m_begin = blockIdx.z * a.m_per_split;
+  const int m_end = min(a.M, m_begin + a.m_per_split);
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(a.x);
+  const bf16_t* __restrict__ DY = reinterpret_cast<const bf16_t*>(a.dy);
+
+  // block role
+  const bool isA = tid < A_BLK;
+  const bool isB = !isA && tid < A_BLK + B_BLK;
+  int cb = 0, mb = 0;  // column block, m block
+  if (isA) { cb = tid % (BM / 8); mb = tid / (BM / 8); }
+  if (isB) { const int t = tid - A_BLK; cb = t % (BN / 8); mb = t / (BN / 8); }
+  // B column decode (one tap, 8 channels)
+  int br = 0, bs = 0, bch = 0;
+  bool bok = false;
+  if (isB) {
+    const int j = bj + cb * 8;
+    bok = j < a.RRC;
+    const int jj = bok ? j : 0;
+    const int tap = jj / a.C;
+    bch = jj - tap * a.C;
+    br = tap / a.R;
+    bs = tap - br * a.R;
+  }
+  const bool aok = isA && (bk + cb * 8 < a.K);
+  const int pq = a.P * a.Q;
+
+  uint4 blk[8];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      blk[r] = make_uint4(0, 0, 0, 0);
+      const int m = m0 + mb * 8 + r;
+      if (m >= m_end) continue;
+      if (isA) {
+        if (aok) blk[r] = *reinterpret_cast<const uint4*>(DY + (long)m * a.ldy + bk + cb * 8);
+      } else if (isB && bok) {
+        const int n = m / pq;
+        const int rr = m - n * pq;
+        const int p = rr / a.Q, q = rr - (rr / a.Q) * a.Q;
+        int yy = p * a.stride - a.pad + br, xx = q * a.stride - a.pad + bs;
+        if (a.pad_mode == UM_PAD_REFLECT) {
+          yy = reflect_idx(yy, a.H);
+          xx = reflect_idx(xx, a.W);
+        } else if (yy < 0 || yy >= a.H || xx < 0 || xx >= a.W) {
+          continue;
+        }
+        blk[r] = *reinterpret_cast<const uint4*>(X + ((long)(n * a.H + yy) * a.W + xx) * a.ldx + bch);
+      }
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fk = (lane >> 4) * 8;
+  if (m_begin < m_end) load(m_begin);
+  for (int m0 = m_begin; m0 < m_end; m0 += WBK) {
+    uint4 tr[8];
+    transpose8x8_bf16(blk, tr);
+    __syncthreads();
+    if (isA || isB) {
+      bf16_t* dst = isA ? sA : sB;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        *reinterpret_cast<uint4*>(dst + (cb * 8 + e) * WLDK + mb * 8) = tr[e];
+    }
+    __syncthreads();
+    if (m0 + WBK < m_end) load(m0 + WBK);
+#pragma unroll
+    for (int kk = 0; kk < WBK; kk += 32) {
+      bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8_t*>(
+            &sA[(wm * (BM / WM) + i * 16 + frow) * WLDK + kk + fk]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8_t*>(
+            &sB[(wn * (BN / WN) + j * 16 + frow) * WLDK + kk + fk]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  float* out = a.slabs + (long)blockIdx.z * a.K * a.RRC;
+  const int col_l = lane & 15, row_g = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = bk + wm * (BM / WM) + i * 16 + row_g + r;
+        const int jj = bj + wn * (BN / WN) + j * 16 + col_l;
+        if (k < a.K && jj < a.RRC) out[(long)k * a.RRC + jj] = acc[i][j][r];
+      }
+}
+
+template <int BM>
+int launch_wgrad_bf16(const WgradArgs& a, int splits, hipStream_t st) {
+  dim3 grid(ceil_div(a.K, BM), ceil_div(a.RRC, 128), splits);
+  hipLaunchKernelGGL(wgrad_bf16_kernel<BM>, grid, dim3(256), 0, st, a);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int splits, int K, int Kreal,
                                     int R, int C, int Creal, float* __restrict__ dw,
-                                    int accumulate) {
-  // dw[k][c][r][s]  <-  sum_z slabs[z][k][(r*R+s)*C + c]   (slabs hold K >= Kreal rows)
-  const long total = (long)Kreal * Creal * R * R;
+                                    int accumulate, Segs sg) {
+  // slab index i = (k, r, s, c) [K][R][R][C] -> dw[k][c][r][s]; reads coalesced
   const long RRC = (long)R * R * C;
+  const long total = (long)Kreal * RRC;
+  const long zs = (long)K * RRC;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int s = i % R;
-    const int r = (i / R) % R;
-    const int c = (i / (R * R)) % Creal;
-    const int k = i / ((long)R * R * Creal);
-    const long src = (long)k * RRC + (r * R + s) * C + c;
-    float v = 0.f;
-    for (int z = 0; z < splits; ++z) v += slabs[z * (long)K * RRC + src];
-    dw[i] = accumulate ? dw[i] + v : v;
+    const int c = seg_src(sg, (int)(i % C));
+    if (c < 0) continue;
+    const int rs = (i / C) % (R * R);
+    const int k = i / RRC;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    int z = 0;
+    for (; z + 3 < splits; z += 4) {
+      v0 += slabs[z * zs + i];
+      v1 += slabs[(z + 1) * zs + i];
+      v2 += slabs[(z + 2) * zs + i];
+      v3 += slabs[(z + 3) * zs + i];
+    }
+    for (; z < splits; ++z) v0 += slabs[z * zs + i];
+    const float v = (v0 + v1) + (v2 + v3);
+    const long o = ((long)k * Creal + c) * R * R + rs;
+    dw[o] = accumulate ? dw[o] + v : v;
   }
 }
 
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ w, int K, int Creal, int R, int C,
-                                   T* __restrict__ wf, T* __restrict__ wT, int ldT) {
+                                   T* __restrict__ wf, T* __restrict__ wT, int ldT, Segs sg) {
   const long total = (long)K * R * R * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
@@ -522,45 +694,71 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int K, int Creal
     const int s = (i / C) % R;
     const int r = (i / ((long)C * R)) % R;
     const int k = i / ((long)C * R * R);
-    const float v = c < Creal ? w[(((long)k * Creal + c) * R + r) * R + s] : 0.f;
+    const int cs = seg_src(sg, c);
+    const float v = cs >= 0 ? w[(((long)k * Creal + cs) * R + r) * R + s] : 0.f;
     if (wf) wf[i] = from_f32<T>(v);
     if (wT) wT[((long)c * R * R + r * R + s) * ldT + k] = from_f32<T>(v);
   }
 }
 
+// per-block column sums of y[M][C] (C % 8 == 0) -> parts[blk][C]
 template <typename T>
-__global__ void colsum_kernel(const T* __restrict__ y, int M, int C, int ld,
-                              float* __restrict__ parts, int rows_per_block) {
-  // block: 256 threads = 8 row lanes x 32 channel lanes per channel tile
-  const int m0 = blockIdx.x * rows_per_block;
-  const int m1 = min(M, m0 + rows_per_block);
-  for (int c0 = 0; c0 < C; c0 += 32) {
-    const int c = c0 + (threadIdx.x & 31);
-    float s = 0.f;
-    if (c < C)
-      for (int m = m0 + (threadIdx.x >> 5); m < m1; m += 8) s += to_f32(y[(long)m * ld + c]);
-    __shared__ float red[8][33];
-    red[threadIdx.x >> 5][threadIdx.x & 31] = s;
-    __syncthreads();
-    if (threadIdx.x < 32 && c < C) {
-      float t = 0.f;
-      for (int r = 0; r < 8; ++r) t += red[r][threadIdx.x];
-      parts[(long)blockIdx.x * C + c] = t;
-    }
-    __syncthreads();
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ y, int M, int C,
+                                                     int ld, float* __restrict__ parts,
+                                                     int rows_per_block) {
+  __shared__ float red[256 * 8];
+  const int cg = C / 8;
+  const RowMap rm(cg);
+  const long m0 = (long)blockIdx.x * rows_per_block;
+  const long m1 = min((long)M, m0 + rows_per_block);
+  for (int g0 = 0; g0 < cg; g0 += rm.G) {
+    const int g = g0 + rm.g;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (rm.active() && g < cg)
+      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+        float v[8];
+        load8(y + m * ld + g * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+    lane_reduce<8>(red, rm, acc);
+    if (rm.lane == 0 && g < cg) store8(parts + (long)blockIdx.x * C + g * 8, acc);
   }
 }
 
-__global__ void reduce_rows_kernel(const float* __restrict__ p, int parts, int C, int stride,
-                                   float* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0;
-  for (int r = 0; r < parts; ++r) s += p[(long)r * stride + c];
-  out[c] = accumulate ? out[c] + (float)s : (float)s;
+// out[c] (+)= sum_r p[r*stride + c]: block = cl channel lanes x (256/cl) row
+// lanes, 4 independent accumulators per thread (latency hiding), f32 -> f64 at
+// the lane combine
+__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* __restrict__ p, int parts,
+                                                          int C, int stride,
+                                                          float* __restrict__ out,
+                                                          int accumulate) {
+  __shared__ double red[256];
+  const int cl = C < 64 ? C : 64;
+  const int lanes = 256 / cl;
+  const int c = blockIdx.x * cl + (threadIdx.x % cl);
+  const int lane = threadIdx.x / cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (lane < lanes && c < C) {
+    int r = lane;
+    for (; r + 3 * lanes < parts; r += 4 * lanes) {
+      s0 += p[(long)r * stride + c];
+      s1 += p[(long)(r + lanes) * stride + c];
+      s2 += p[(long)(r + 2 * lanes) * stride + c];
+      s3 += p[(long)(r + 3 * lanes) * stride + c];
+    }
+    for (; r < parts; r += lanes) s0 += p[(long)r * stride + c];
+  }
+  double s = (double)s0 + (double)s1 + (double)s2 + (double)s3;
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (lane == 0 && c < C) {
+    for (int q = 1; q < lanes; ++q) s += red[q * cl + (threadIdx.x % cl)];
+    out[c] = accumulate ? out[c] + (float)s : (float)s;
+  }
 }
 
-constexpr int COLSUM_ROWS = 1024;
+constexpr int COLSUM_ROWS = 256;
 
 }  // namespace
 
@@ -615,12 +813,15 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
                           : dispatch_conv<float, MODE_DGRAD>(a, st);
 }
 
+static int wgrad_bm(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
+
 int um_conv_wgrad_splits(int M, int K, int RRC) {
-  const long tiles = (long)ceil_div(K, 64) * ceil_div(RRC, 64);
-  long splits = (1024 + tiles - 1) / tiles;
-  const long max_by_m = (M + 511) / 512;  // >= 512 pixels per split
+  // tiles of the bf16 kernel (the f32 kernel uses 64x64 tiles; same split count)
+  const long tiles = (long)ceil_div(K, wgrad_bm(K)) * ceil_div(RRC, 128);
+  long splits = (768 + tiles - 1) / tiles;
+  const long max_by_m = (M + 1023) / 1024;  // >= 1024 pixels per split
   if (splits > max_by_m) splits = max_by_m;
-  const long max_by_bytes = (64l << 20) / ((long)K * RRC * 4);  // <= 64 MB of slabs
+  const long max_by_bytes = (32l << 20) / ((long)K * RRC * 4);  // <= 32 MB of slabs
   if (splits > max_by_bytes) splits = max_by_bytes;
   if (splits < 1) splits = 1;
   return (int)splits;
@@ -636,40 +837,81 @@ int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* 
   a.pad = pad; a.pad_mode = pad_mode; a.P = P; a.Q = Q; a.ldy = ldy;
   a.x = x; a.dy = dy; a.slabs = slabs;
   a.M = N * P * Q; a.RRC = R * R * C;
-  a.m_per_split = ceil_div(ceil_div(a.M, splits), BK) * BK;
-  if (dtype == UM_BF16) return launch_wgrad<bf16_t, 64, 64>(a, splits, st);
+  a.m_per_split = ceil_div(ceil_div(a.M, splits), WBK) * WBK;
+  if (dtype == UM_BF16) {
+    UM_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0, "um_conv2d_wgrad: ld %% 8");
+    const int bm = wgrad_bm(K);
+    if (bm == 32) return launch_wgrad_bf16<32>(a, splits, st);
+    if (bm == 64) return launch_wgrad_bf16<64>(a, splits, st);
+    return launch_wgrad_bf16<128>(a, splits, st);
+  }
   return launch_wgrad<float, 64, 64>(a, splits, st);
+}
+
+static int make_segs(Segs& g, int nseg, const int* src0, const int* dst0, const int* len,
+                     int Creal, int C) {
+  if (nseg <= 0) {
+    g.n = 1;
+    g.src0[0] = 0; g.dst0[0] = 0; g.len[0] = Creal;
+    return 1;
+  }
+  if (nseg > MAX_SEG) return 0;
+  g.n = nseg;
+  for (int i = 0; i < nseg; ++i) {
+    g.src0[i] = src0[i]; g.dst0[i] = dst0[i]; g.len[i] = len[i];
+    if (src0[i] + len[i] > Creal || dst0[i] + len[i] > C) return 0;
+  }
+  return 1;
+}
+
+int um_conv_wgrad_reduce_seg(const float* slabs, int splits, int K, int Kreal, int R, int C,
+                             int Creal, float* dw, int accumulate, int nseg, const int* src0,
+                             const int* dst0, const int* len, hipStream_t st) {
+  UM_CHECK_ARG(Kreal <= K && Creal <= C, "um_conv_wgrad_reduce: sizes");
+  Segs g{};
+  UM_CHECK_ARG(make_segs(g, nseg, src0, dst0, len, Creal, C), "um_conv_wgrad_reduce: segments");
+  const long total = (long)Kreal * R * R * C;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slabs, splits, K, Kreal,
+                     R, C, Creal, dw, accumulate, g);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
 }
 
 int um_conv_wgrad_reduce(const float* slabs, int splits, int K, int Kreal, int R, int C,
                          int Creal, float* dw, int accumulate, hipStream_t st) {
-  UM_CHECK_ARG(Kreal <= K && Creal <= C, "um_conv_wgrad_reduce: sizes");
-  const long total = (long)Kreal * Creal * R * R;
+  return um_conv_wgrad_reduce_seg(slabs, splits, K, Kreal, R, C, Creal, dw, accumulate, 0,
+                                  nullptr, nullptr, nullptr, st);
+}
+
+int um_pack_weight_seg(int dtype, const float* w, int K, int Creal, int R, int C, void* wf,
+                       void* wT, int ldT, int nseg, const int* src0, const int* dst0,
+                       const int* len, hipStream_t st) {
+  UM_CHECK_ARG(C >= Creal, "um_pack_weight: C < Creal");
+  Segs g{};
+  UM_CHECK_ARG(make_segs(g, nseg, src0, dst0, len, Creal, C), "um_pack_weight: segments");
+  const long total = (long)K * R * R * C;
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slabs, splits, K, Kreal,
-                     R, C, Creal, dw, accumulate);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, w, K, Creal,
+                       R, C, (bf16_t*)wf, (bf16_t*)wT, ldT, g);
+  else
+    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, st, w, K, Creal, R,
+                       C, (float*)wf, (float*)wT, ldT, g);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
 
 int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C, void* wf, void* wT,
                    int ldT, hipStream_t st) {
-  UM_CHECK_ARG(C >= Creal, "um_pack_weight: C < Creal");
-  const long total = (long)K * R * R * C;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-  if (dtype == UM_BF16)
-    hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, w, K, Creal,
-                       R, C, (bf16_t*)wf, (bf16_t*)wT, ldT);
-  else
-    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, st, w, K, Creal, R,
-                       C, (float*)wf, (float*)wT, ldT);
-  UM_LAUNCH_CHECK();
-  return UM_OK;
+  return um_pack_weight_seg(dtype, w, K, Creal, R, C, wf, wT, ldT, 0, nullptr, nullptr, nullptr,
+                            st);
 }
 
 int um_colsum_parts(int M) { return ceil_div(M, COLSUM_ROWS); }
 
 int um_colsum(int dtype, int M, int C, int ld, const void* y, float* parts, hipStream_t st) {
+  UM_CHECK_ARG(C % 8 == 0 && ld % 8 == 0, "um_colsum: C/ld %% 8");
   const int blocks = ceil_div(M, COLSUM_ROWS);
   if (blocks == 0) return UM_OK;
   if (dtype == UM_BF16)
@@ -684,7 +926,7 @@ int um_colsum(int dtype, int M, int C, int ld, const void* y, float* parts, hipS
 
 int um_reduce_rows(const float* partials, int parts, int C, int stride, float* out, int accumulate,
                    hipStream_t st) {
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, partials, parts,
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, st, partials, parts,
                      C, stride, out, accumulate);
   UM_LAUNCH_CHECK();
   return UM_OK;

@@ -51,76 +51,126 @@ __device__ __forceinline__ void st_any(void* p, long off, int dt, float v, int a
   }
 }
 
+// value of source s, channel cc, at destination pixel (n, y, x)
+__device__ __forceinline__ float cat_value(const CatSrc& s, int n, int y, int x, int H, int W,
+                                           int cc) {
+  float v;
+  if (s.op == UM_CAT_COPY) {
+    v = ld_any(s.ptr, ((long)(n * H + y) * W + x) * s.ld + cc, s.dtype);
+  } else if (s.op == UM_CAT_UP2) {
+    int y0, y1, x0, x1;
+    float ly, lx;
+    up_index(y, s.h, H, y0, y1, ly);
+    up_index(x, s.w, W, x0, x1, lx);
+    const long b = (long)n * s.h;
+    const float v00 = ld_any(s.ptr, ((b + y0) * s.w + x0) * s.ld + cc, s.dtype);
+    const float v01 = ld_any(s.ptr, ((b + y0) * s.w + x1) * s.ld + cc, s.dtype);
+    const float v10 = ld_any(s.ptr, ((b + y1) * s.w + x0) * s.ld + cc, s.dtype);
+    const float v11 = ld_any(s.ptr, ((b + y1) * s.w + x1) * s.ld + cc, s.dtype);
+    v = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+  } else {  // PSHUF: src [N][H/2][W/2][4C], channel cc*4 + (y&1)*2 + (x&1)
+    v = ld_any(s.ptr, ((long)(n * s.h + (y >> 1)) * s.w + (x >> 1)) * s.ld + cc * 4 +
+                          (y & 1) * 2 + (x & 1), s.dtype);
+  }
+  if (s.scale) v *= s.scale[n * s.C + cc];
+  return v;
+}
+
+__device__ __forceinline__ void ld8_any(const void* p, long off, int dt, float* v) {
+  if (dt == UM_BF16) load8(reinterpret_cast<const bf16_t*>(p) + off, v);
+  else load8(reinterpret_cast<const float*>(p) + off, v);
+}
+
+// one thread per (pixel, 8 destination channels); vector fast path when the
+// 8 channels come from one aligned COPY/UP2 source
 template <typename T>
 __global__ void concat_build_kernel(CatArgs a, int N, int H, int W, int Ctot, T* __restrict__ dst,
                                     int ld) {
-  const long total = (long)N * H * W * Ctot;
+  const int cg = Ctot / 8;
+  const long total = (long)N * H * W * cg;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int c = i % Ctot;
-    const long pix = i / Ctot;
+    const int c0 = (int)(i % cg) * 8;
+    const long pix = i / cg;
     const int x = pix % W;
     const int y = (pix / W) % H;
     const int n = pix / ((long)W * H);
-    float v = 0.f;
-    for (int k = 0; k < a.nsrc; ++k) {
+    float v[8];
+    int k = 0;
+    for (; k < a.nsrc; ++k)
+      if (c0 >= a.s[k].coff && c0 < a.s[k].coff + a.s[k].C) break;
+    const bool fast = k < a.nsrc && c0 + 8 <= a.s[k].coff + a.s[k].C &&
+                      ((c0 - a.s[k].coff) & 7) == 0 && (a.s[k].ld & 7) == 0 &&
+                      (a.s[k].C & 7) == 0 && a.s[k].op != UM_CAT_PSHUF;
+    if (fast) {
       const CatSrc& s = a.s[k];
-      const int cc = c - s.coff;
-      if (cc < 0 || cc >= s.C) continue;
+      const int cc = c0 - s.coff;
       if (s.op == UM_CAT_COPY) {
-        v = ld_any(s.ptr, ((long)(n * H + y) * W + x) * s.ld + cc, s.dtype);
-      } else if (s.op == UM_CAT_UP2) {
+        ld8_any(s.ptr, ((long)(n * H + y) * W + x) * s.ld + cc, s.dtype, v);
+      } else {
         int y0, y1, x0, x1;
         float ly, lx;
         up_index(y, s.h, H, y0, y1, ly);
         up_index(x, s.w, W, x0, x1, lx);
         const long b = (long)n * s.h;
-        const float v00 = ld_any(s.ptr, ((b + y0) * s.w + x0) * s.ld + cc, s.dtype);
-        const float v01 = ld_any(s.ptr, ((b + y0) * s.w + x1) * s.ld + cc, s.dtype);
-        const float v10 = ld_any(s.ptr, ((b + y1) * s.w + x0) * s.ld + cc, s.dtype);
-        const float v11 = ld_any(s.ptr, ((b + y1) * s.w + x1) * s.ld + cc, s.dtype);
-        v = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
-      } else {  // PSHUF: src [N][H/2][W/2][4C], channel cc*4 + (y&1)*2 + (x&1)
-        v = ld_any(s.ptr, ((long)(n * s.h + (y >> 1)) * s.w + (x >> 1)) * s.ld + cc * 4 +
-                              (y & 1) * 2 + (x & 1),
-                   s.dtype);
+        float v00[8], v01[8], v10[8], v11[8];
+        ld8_any(s.ptr, ((b + y0) * s.w + x0) * s.ld + cc, s.dtype, v00);
+        ld8_any(s.ptr, ((b + y0) * s.w + x1) * s.ld + cc, s.dtype, v01);
+        ld8_any(s.ptr, ((b + y1) * s.w + x0) * s.ld + cc, s.dtype, v10);
+        ld8_any(s.ptr, ((b + y1) * s.w + x1) * s.ld + cc, s.dtype, v11);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[e] = (1.f - ly) * ((1.f - lx) * v00[e] + lx * v01[e]) +
+                 ly * ((1.f - lx) * v10[e] + lx * v11[e]);
       }
-      if (s.scale) v *= s.scale[n * s.C + cc];
-      break;
+      if (s.scale) {
+        float sc[8];
+        load8(s.scale + n * s.C + cc, sc);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= sc[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        v[e] = 0.f;
+        for (int kk = 0; kk < a.nsrc; ++kk) {
+          const int cc = c - a.s[kk].coff;
+          if (cc >= 0 && cc < a.s[kk].C) {
+            v[e] = cat_value(a.s[kk], n, y, x, H, W, cc);
+            break;
+          }
+        }
+      }
     }
-    dst[pix * ld + c] = from_f32<T>(v);
+    store8(dst + pix * ld + c0, v);
   }
 }
 
-// ---- backward: block = 64 channels x 4 pixel lanes; grid (pixel chunks, C/64, N)
-constexpr int BWD_CHUNK = 256;  // source pixels per block
+// ---- backward: RowMap blocks (channel groups x pixel lanes) over a chunk of
+// BWD_CHUNK source pixels of one image n; grid (chunks, 1, N)
+constexpr int BWD_CHUNK = 256;
 
-template <typename T>
-__global__ void cat_bwd_copy_kernel(const T* __restrict__ g, int ldg, int coff, int H, int W,
-                                    CatSrc s, void* dsrc, int ldd, int dsd, int acc,
-                                    float* __restrict__ dscale) {
-  const int n = blockIdx.z;
-  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
-  const int pl = threadIdx.x >> 6;
-  const long P = (long)H * W;
-  const long p0 = (long)blockIdx.x * BWD_CHUNK, p1 = min(P, p0 + BWD_CHUNK);
-  float ds = 0.f;
-  if (c < s.C) {
-    const float sc = s.scale ? s.scale[n * s.C + c] : 1.f;
-    for (long p = p0 + pl; p < p1; p += 4) {
-      const long pix = (long)n * P + p;
-      const float gv = to_f32(g[pix * ldg + coff + c]);
-      if (dsrc) st_any(dsrc, pix * ldd + c, dsd, gv * sc, acc);
-      if (dscale) ds += gv * ld_any(s.ptr, pix * s.ld + c, s.dtype);
+__device__ __forceinline__ void st8_any(void* p, long off, int dt, const float* v, int acc) {
+  float o[8];
+  if (dt == UM_BF16) {
+    bf16_t* q = reinterpret_cast<bf16_t*>(p) + off;
+    if (acc) {
+      load8(q, o);
+      for (int e = 0; e < 8; ++e) o[e] += v[e];
+      store8(q, o);
+    } else {
+      store8(q, v);
     }
-  }
-  if (dscale) {
-    __shared__ float red[4][64];
-    red[pl][threadIdx.x & 63] = ds;
-    __syncthreads();
-    if (pl == 0 && c < s.C)
-      atomicAdd(&dscale[n * s.C + c], red[0][c & 63] + red[1][c & 63] + red[2][c & 63] +
-                                          red[3][c & 63]);
+  } else {
+    float* q = reinterpret_cast<float*>(p) + off;
+    if (acc) {
+      load8(q, o);
+      for (int e = 0; e < 8; ++e) o[e] += v[e];
+      store8(q, o);
+    } else {
+      store8(q, v);
+    }
   }
 }
 
@@ -150,40 +200,146 @@ __device__ __forceinline__ int up_adj(int j, int in, int out, int* idx, float* w
   return cnt;
 }
 
-template <typename T>
-__global__ void cat_bwd_up2_kernel(const T* __restrict__ g, int ldg, int coff, int H, int W,
-                                   CatSrc s, void* dsrc, int ldd, int dsd, int acc,
-                                   float* __restrict__ dscale) {
+// weight with which high-res index i samples low-res index j under the x2
+// align_corners=True upsample (in -> out); 0 outside [0, out)
+__device__ __forceinline__ float up_w(int i, int j, int in, int out) {
+  if (i < 0 || i >= out) return 0.f;
+  int i0, i1;
+  float l1;
+  up_index(i, in, out, i0, i1, l1);
+  float w = 0.f;
+  if (i0 == j) w += 1.f - l1;
+  if (i1 == j) w += l1;
+  return w;
+}
+
+// COPY (op 0) / UP2 (op 1) source gradient, vectorised over 8 channels:
+//   gv = (op==COPY) g[pix, coff+c] : sum_taps w * g[hi-res tap, coff+c]
+//   dsrc (+)= gv * gate ;  dgate[n][c] += sum_pix gv * src
+template <typename T, int OP>
+__global__ void __launch_bounds__(256) cat_bwd_kernel(const T* __restrict__ g, int ldg, int coff,
+                                                      int H, int W, CatSrc s, void* dsrc, int ldd,
+                                                      int dsd, int acc,
+                                                      float* __restrict__ dscale) {
+  __shared__ float red[256 * 8];
   const int n = blockIdx.z;
-  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
-  const int pl = threadIdx.x >> 6;
+  const int cg = s.C / 8;
+  const RowMap rm(cg);
   const long P = (long)s.h * s.w;
   const long p0 = (long)blockIdx.x * BWD_CHUNK, p1 = min(P, p0 + BWD_CHUNK);
-  float ds = 0.f;
-  if (c < s.C) {
-    const float sc = s.scale ? s.scale[n * s.C + c] : 1.f;
-    for (long p = p0 + pl; p < p1; p += 4) {
-      const int py = p / s.w, px = p % s.w;
-      int yi[8], xi[8];
-      float yw[8], xw[8];
-      const int ny = up_adj(py, s.h, H, yi, yw);
-      const int nx = up_adj(px, s.w, W, xi, xw);
-      float gv = 0.f;
-      for (int a = 0; a < ny; ++a)
-        for (int b = 0; b < nx; ++b)
-          gv += yw[a] * xw[b] * to_f32(g[((long)(n * H + yi[a]) * W + xi[b]) * ldg + coff + c]);
-      const long sp = (long)n * P + p;
-      if (dsrc) st_any(dsrc, sp * ldd + c, dsd, gv * sc, acc);
-      if (dscale) ds += gv * ld_any(s.ptr, sp * s.ld + c, s.dtype);
+  for (int g0 = 0; g0 < cg; g0 += rm.G) {
+    const int gi = g0 + rm.g;
+    const int c = gi * 8;
+    float ds[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (rm.active() && gi < cg) {
+      float sc[8] = {1, 1, 1, 1, 1, 1, 1, 1};
+      if (s.scale) load8(s.scale + n * s.C + c, sc);
+      for (long p = p0 + rm.lane; p < p1; p += rm.lanes) {
+        float gv[8];
+        if (OP == UM_CAT_COPY) {
+          load8(g + ((long)n * P + p) * ldg + coff + c, gv);
+        } else {
+          const int py = p / s.w, px = p % s.w;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gv[e] = 0.f;
+          // high-res rows/cols that sample low-res (py, px) lie in [2j-2, 2j+4]
+          float wx[7];
+#pragma unroll
+          for (int v = 0; v < 7; ++v) wx[v] = up_w(2 * px - 2 + v, px, s.w, W);
+#pragma unroll
+          for (int u = 0; u < 7; ++u) {
+            const float wy = up_w(2 * py - 2 + u, py, s.h, H);
+            if (wy == 0.f) continue;
+            const T* row = g + ((long)(n * H + 2 * py - 2 + u) * W + 2 * px - 2) * ldg + coff + c;
+#pragma unroll
+            for (int v = 0; v < 7; ++v) {
+              if (wx[v] == 0.f) continue;
+              float t[8];
+              load8(row + (long)v * ldg, t);
+              const float w = wy * wx[v];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) gv[e] += w * t[e];
+            }
+          }
+        }
+        const long sp = (long)n * P + p;
+        if (dsrc) {
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = gv[e] * sc[e];
+          st8_any(dsrc, sp * ldd + c, dsd, o, acc);
+        }
+        if (dscale) {
+          float sv[8];
+          ld8_any(s.ptr, sp * s.ld + c, s.dtype, sv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ds[e] += gv[e] * sv[e];
+        }
+      }
+    }
+    if (dscale) {
+      lane_reduce<8>(red, rm, ds);
+      if (rm.lane == 0 && gi < cg)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) atomicAdd(&dscale[n * s.C + c + e], ds[e]);
     }
   }
-  if (dscale) {
-    __shared__ float red[4][64];
-    red[pl][threadIdx.x & 63] = ds;
-    __syncthreads();
-    if (pl == 0 && c < s.C)
-      atomicAdd(&dscale[n * s.C + c], red[0][c & 63] + red[1][c & 63] + red[2][c & 63] +
-                                          red[3][c & 63]);
+}
+
+// scalar path for sources whose channels are not 8-aligned in the concat
+// (the 4-channel disparity; the skip placed after the 3-channel image):
+// thread = (channel c = t % Cl, pixel lane t / Cl), per-block gate sums.
+template <typename T, int OP>
+__global__ void __launch_bounds__(256) cat_bwd_scalar_kernel(const T* __restrict__ g, int ldg,
+                                                             int coff, int H, int W, CatSrc s,
+                                                             void* dsrc, int ldd, int dsd,
+                                                             int acc, float* __restrict__ dscale) {
+  __shared__ float red[256];
+  const int n = blockIdx.z;
+  const int Cl = s.C < 256 ? s.C : 256;
+  const int lanes = 256 / Cl;
+  const int cl = threadIdx.x % Cl, lane = threadIdx.x / Cl;
+  const long P = (long)s.h * s.w;
+  const long p0 = (long)blockIdx.x * BWD_CHUNK, p1 = min(P, p0 + BWD_CHUNK);
+  for (int c0 = 0; c0 < s.C; c0 += Cl) {
+    const int c = c0 + cl;
+    float ds = 0.f;
+    if (lane < lanes && c < s.C) {
+      const float sc = s.scale ? s.scale[n * s.C + c] : 1.f;
+      for (long p = p0 + lane; p < p1; p += lanes) {
+        float gv;
+        if (OP == UM_CAT_COPY) {
+          gv = to_f32(g[((long)n * P + p) * ldg + coff + c]);
+        } else {
+          const int py = p / s.w, px = p % s.w;
+          gv = 0.f;
+#pragma unroll
+          for (int u = 0; u < 7; ++u) {
+            const float wy = up_w(2 * py - 2 + u, py, s.h, H);
+            if (wy == 0.f) continue;
+#pragma unroll
+            for (int v = 0; v < 7; ++v) {
+              const float wx = up_w(2 * px - 2 + v, px, s.w, W);
+              if (wx == 0.f) continue;
+              gv += wy * wx * to_f32(g[((long)(n * H + 2 * py - 2 + u) * W + 2 * px - 2 + v) * ldg +
+                                       coff + c]);
+            }
+          }
+        }
+        const long sp = (long)n * P + p;
+        if (dsrc) st_any(dsrc, sp * ldd + c, dsd, gv * sc, acc);
+        if (dscale) ds += gv * ld_any(s.ptr, sp * s.ld + c, s.dtype);
+      }
+    }
+    if (dscale) {
+      red[threadIdx.x] = ds;
+      __syncthreads();
+      if (lane == 0 && c < s.C) {
+        for (int r = 1; r < lanes; ++r) ds += red[r * Cl + cl];
+        atomicAdd(&dscale[n * s.C + c], ds);
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -315,7 +471,8 @@ int um_concat_build(int dtype, int N, int H, int W, void* dst, int ld, int Ctot,
     UM_CHECK_ARG(s.op != UM_CAT_COPY || (s.h == H && s.w == W), "um_concat_build: copy size");
     UM_CHECK_ARG(s.op == UM_CAT_COPY || (2 * s.h == H && 2 * s.w == W), "um_concat_build: x2 size");
   }
-  const long total = (long)N * H * W * Ctot;
+  UM_CHECK_ARG(Ctot % 8 == 0 && ld % 8 == 0, "um_concat_build: Ctot/ld %% 8");
+  const long total = (long)N * H * W * (Ctot / 8);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(concat_build_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, a, N,
                        H, W, Ctot, (bf16_t*)dst, ld);
@@ -331,6 +488,7 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
                       float* dscale, hipStream_t st) {
   const um_cat_src& s0 = *src;
   CatSrc s{s0.ptr, s0.scale, s0.C, s0.ld, s0.op, s0.coff, s0.dtype, s0.h, s0.w};
+  UM_CHECK_ARG(ldg % 8 == 0, "um_concat_bwd_src: ldg %% 8");
   if (s.op == UM_CAT_PSHUF) {
     UM_CHECK_ARG(dsrc != nullptr && dscale == nullptr, "um_concat_bwd_src: pshuf args");
     const long per_n = (long)s.h * s.w * 4 * s.C;
@@ -341,24 +499,45 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
     else
       hipLaunchKernelGGL(cat_bwd_pshuf_kernel<float>, grid, dim3(256), 0, st, (const float*)g, ldg,
                          s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate);
-  } else {
-    const long P = (long)s.h * s.w;
-    dim3 grid(ceil_div(P, BWD_CHUNK), ceil_div(s.C, 64), N);
-    if (s.op == UM_CAT_COPY) {
-      if (dtype == UM_BF16)
-        hipLaunchKernelGGL(cat_bwd_copy_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)g,
-                           ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, dscale);
-      else
-        hipLaunchKernelGGL(cat_bwd_copy_kernel<float>, grid, dim3(256), 0, st, (const float*)g,
-                           ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, dscale);
+    UM_LAUNCH_CHECK();
+    return UM_OK;
+  }
+  const long P = (long)s.h * s.w;
+  const bool vec = (s.C % 8 == 0) && (s.coff % 8 == 0) && (ldd % 8 == 0 || !dsrc) &&
+                   (s.ld % 8 == 0 || !dscale);
+  if (!vec) {
+    dim3 grid(ceil_div(P, BWD_CHUNK), 1, N);
+#define UM_CAT_SCALAR(T_, OP_)                                                               \
+    hipLaunchKernelGGL((cat_bwd_scalar_kernel<T_, OP_>), grid, dim3(256), 0, st, (const T_*)g, \
+                       ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, dscale)
+    if (dtype == UM_BF16) {
+      if (s.op == UM_CAT_COPY) UM_CAT_SCALAR(bf16_t, UM_CAT_COPY); else UM_CAT_SCALAR(bf16_t, UM_CAT_UP2);
     } else {
-      if (dtype == UM_BF16)
-        hipLaunchKernelGGL(cat_bwd_up2_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)g,
-                           ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, dscale);
-      else
-        hipLaunchKernelGGL(cat_bwd_up2_kernel<float>, grid, dim3(256), 0, st, (const float*)g,
-                           ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, dscale);
+      if (s.op == UM_CAT_COPY) UM_CAT_SCALAR(float, UM_CAT_COPY); else UM_CAT_SCALAR(float, UM_CAT_UP2);
     }
+#undef UM_CAT_SCALAR
+    UM_LAUNCH_CHECK();
+    return UM_OK;
+  }
+  dim3 grid(ceil_div(P, BWD_CHUNK), 1, N);
+  if (s.op == UM_CAT_COPY) {
+    if (dtype == UM_BF16)
+      hipLaunchKernelGGL((cat_bwd_kernel<bf16_t, UM_CAT_COPY>), grid, dim3(256), 0, st,
+                         (const bf16_t*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
+                         accumulate, dscale);
+    else
+      hipLaunchKernelGGL((cat_bwd_kernel<float, UM_CAT_COPY>), grid, dim3(256), 0, st,
+                         (const float*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate,
+                         dscale);
+  } else {
+    if (dtype == UM_BF16)
+      hipLaunchKernelGGL((cat_bwd_kernel<bf16_t, UM_CAT_UP2>), grid, dim3(256), 0, st,
+                         (const bf16_t*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
+                         accumulate, dscale);
+    else
+      hipLaunchKernelGGL((cat_bwd_kernel<float, UM_CAT_UP2>), grid, dim3(256), 0, st,
+                         (const float*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate,
+                         dscale);
   }
   UM_LAUNCH_CHECK();
   return UM_OK;

@@ -59,12 +59,12 @@ class ConvELUBlock(nn.Module):
             nn.BatchNorm2d(out_channels) if batch_norm else nn.Identity(),
             nn.ELU(inplace=True))
 
-    def _fwd(self, x: Tensor, se: Optional['SELayer'] = None):
+    def _fwd(self, x: Tensor, se: Optional['SELayer'] = None, segs=None):
         conv_layer = self.layers[0]
         pad, mode = conv_layer.pad_args()
         bn = self.layers[1] if isinstance(self.layers[1], nn.modules.batchnorm._BatchNorm) \
             else None
-        return U.conv_bn_elu(x, conv_layer.layers[0], bn, pad, mode, se=se)
+        return U.conv_bn_elu(x, conv_layer.layers[0], bn, pad, mode, se=se, segs=segs)
 
     def forward(self, x: Tensor) -> Tensor:
         return to_nchw(self._fwd(to_nhwc(x)))
@@ -135,17 +135,17 @@ class DecoderStage(nn.Module):
         N, H, W, _ = feature_map.shape
         dtype = x.dtype
         skip_t, skip_g = skip if isinstance(skip, tuple) else (skip, None)
-        cat1 = U.concat([U.CatSource(feature_map, CAT_COPY, self.feature_in_channels),
-                         U.CatSource(skip_t, CAT_UP2, self.skip_in_channels, skip_g)],
-                        N, H, W, dtype)
-        u1, gate = self.squeeze_excite[0]._fwd(cat1, se=self.squeeze_excite[1])
+        cat1, segs1 = U.concat([U.CatSource(feature_map, CAT_COPY, self.feature_in_channels),
+                                U.CatSource(skip_t, CAT_UP2, self.skip_in_channels, skip_g)],
+                               N, H, W, dtype)
+        u1, gate = self.squeeze_excite[0]._fwd(cat1, se=self.squeeze_excite[1], segs=segs1)
         xu = self.upsample[0]._fwd(x)  # [N, H/2, W/2, 4*Cu]; pixel shuffle folded into cat2
         srcs = [U.CatSource(xu, CAT_PSHUF, self.upsample_channels),
                 U.CatSource(u1, CAT_COPY, self.skip_out_channels, gate)]
         if self.concat_disp:
             srcs.append(U.CatSource(disparity, CAT_UP2, self.disp_channels))
-        cat2 = U.concat(srcs, N, H, W, dtype)
-        out = self.iconv._fwd(cat2)
+        cat2, segs2 = U.concat(srcs, N, H, W, dtype)
+        out = self.iconv._fwd(cat2, segs=segs2)
         disp = U.disp_head(out, self.disp.layers[0], scale) if self.calculate_disp else None
         return out, (u1, gate), disp
 

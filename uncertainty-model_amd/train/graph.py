@@ -1,0 +1,74 @@
+"""Whole-step HIP graph capture of the training step.
+
+The eager step (train.train.train_step, reference train/train.py:116-129)
+issues ~1,300 small launches from Python; at B=8 x 256x512 the host cannot
+keep the GPU fed.  ``CapturedTrainStep`` captures the same step once and
+replays it:
+
+  graph 1: pyramid -> model forward -> reconstruct -> fused loss -> backward
+           (gradients land in static graph-pool tensors)
+  graph 2: fused Adam over those gradients (pointer table uploaded once,
+           step counter and lr read from device memory by the kernel)
+
+Inputs are copied into static device buffers before each replay.  Host-side
+state that the eager loop would change between steps must not change under
+a captured step: the disparity ``scale`` is fixed at capture (recapture when
+``adjust_disparity`` moves it) and the learning rate goes through
+``umamd.optim.Adam.set_lr``.  Single-process only: the DDP gradient
+all-reduce runs eagerly.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import utils as u
+
+
+class CapturedTrainStep:
+    def __init__(self, model, loss_function, optimiser, left, right, scale: float,
+                 scales: int = 4, warmup: int = 3):
+        if not hasattr(optimiser, 'prepare'):
+            raise TypeError('CapturedTrainStep needs umamd.optim.Adam (graph-replayable)')
+        self.model, self.loss_function, self.optimiser = model, loss_function, optimiser
+        self.scale, self.scales = float(scale), scales
+        self.left = left.detach().clone().contiguous()
+        self.right = right.detach().clone().contiguous()
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(warmup):  # eager steps: allocator warm-up, optimiser state
+                optimiser.zero_grad(set_to_none=True)
+                self._fwd_bwd()
+                optimiser.step()
+        cur.wait_stream(side)
+        torch.cuda.synchronize()
+        optimiser.zero_grad(set_to_none=True)
+        # capture on the warm-up stream so autograd's cached AccumulateGrad
+        # nodes see the stream they were created on
+        self.g_fb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fb, stream=side):
+            self.disp_loss, self.error_loss = self._fwd_bwd()
+        optimiser.prepare()  # tables for the graph-pool gradients, outside capture
+        torch.cuda.synchronize()
+        self.g_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool(), stream=side):
+            optimiser.step()
+
+    def _fwd_bwd(self):
+        images = torch.cat([self.left, self.right], dim=1)
+        pyramid = u.scale_pyramid(images, self.scales)
+        disparities = self.model(self.left, self.scale)
+        recon = u.reconstruct_pyramid(disparities, pyramid)
+        disp_loss, error_loss = self.loss_function(pyramid, disparities, recon, 0, None)
+        (disp_loss + error_loss).backward()
+        return disp_loss, error_loss
+
+    def __call__(self, left=None, right=None):
+        if left is not None:
+            self.left.copy_(left)
+        if right is not None:
+            self.right.copy_(right)
+        self.g_fb.replay()
+        self.g_opt.replay()
+        return self.disp_loss, self.error_loss

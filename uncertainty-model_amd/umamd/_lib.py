@@ -45,6 +45,8 @@ _SIG = {
                              _P, _I, 's']),
     'um_conv_wgrad_reduce': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, 's']),
     'um_pack_weight': (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _I, 's']),
+    'um_pack_weight_seg': (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P, 's']),
+    'um_conv_wgrad_reduce_seg': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, 's']),
     'um_colsum_parts': (_I, [_I]),
     'um_colsum': (_I, [_I, _I, _I, _I, _P, _P, 's']),
     'um_reduce_rows': (_I, [_P, _I, _I, _I, _P, _I, 's']),
@@ -56,7 +58,7 @@ _SIG = {
                                   's']),
     'um_bn_bwd_coeffs': (_I, [_P, _D, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, 's']),
     'um_bn_elu_bwd_apply': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P,
-                                 _P, _P, _P, _I, 's']),
+                                 _P, _P, _P, _I, _P, 's']),
     'um_merge_fwd': (_I, [_I, _I, _P, _P, _P, _P, _L, _P, 's']),
     'um_merge_parts': (_I, [_L]),
     'um_merge_bwd': (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _L, _P, _P, 's']),
@@ -84,6 +86,7 @@ _SIG = {
                                _F, _F, _P, 's']),
     'um_adam_chunk': (_I, []),
     'um_adam_step': (_I, [_P, _P, _I, _F, _F, _F, _F, _F, _I, 's']),
+    'um_adam_step_dev': (_I, [_P, _P, _I, _F, _P, _F, _F, _F, _F, _P, 's']),
 }
 
 _lib: Optional[ctypes.CDLL] = None

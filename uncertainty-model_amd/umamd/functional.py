@@ -39,8 +39,18 @@ def _dt(t: torch.Tensor) -> int:
 
 
 # --------------------------------------------------------------- helpers ----
-def _pack(weight: torch.Tensor, Cp: int, dtype: torch.dtype, wf=True, wT=True, ldT=None):
-    """Repack an NCHW f32 conv weight to [K][R][R][Cp] and [Cp][R][R][ldT]."""
+def _seg_arrays(segs):
+    if not segs:
+        return 0, None, None, None
+    n = len(segs)
+    return (n, (ctypes_i * n)(*[a for a, _, _ in segs]), (ctypes_i * n)(*[b for _, b, _ in segs]),
+            (ctypes_i * n)(*[c for _, _, c in segs]))
+
+
+def _pack(weight: torch.Tensor, Cp: int, dtype: torch.dtype, wf=True, wT=True, ldT=None,
+          segs=None):
+    """Repack an NCHW f32 conv weight to [K][R][R][Cp] and [Cp][R][R][ldT];
+    ``segs`` = [(ref_c0, packed_c0, len)] places input-channel ranges."""
     K, Creal, R, _ = weight.shape
     ldT = ldT or K
     w = weight.detach()
@@ -51,7 +61,9 @@ def _pack(weight: torch.Tensor, Cp: int, dtype: torch.dtype, wf=True, wT=True, l
     if wT:
         t = (torch.zeros if ldT != K else torch.empty)((Cp, R, R, ldT), dtype=dtype,
                                                         device=w.device)
-    call('um_pack_weight', L.dtype_code(dtype), ptr(w), K, Creal, R, Cp, ptr(f), ptr(t), ldT)
+    n, a0, b0, l0 = _seg_arrays(segs)
+    call('um_pack_weight_seg', L.dtype_code(dtype), ptr(w), K, Creal, R, Cp, ptr(f), ptr(t), ldT,
+         n, a0, b0, l0)
     return f, t
 
 
@@ -80,7 +92,7 @@ def _conv_dgrad(dy, wT, x_shape, K, R, stride, pad, pad_mode, dx=None, accumulat
     return dx
 
 
-def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None):
+def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=None):
     """dW in the reference NCHW layout [Kreal][Creal][R][R] (f32)."""
     N, H, W, C = x.shape
     _, P, Q, ldy = dy.shape
@@ -92,7 +104,9 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None):
          ptr(dy), ldy, ptr(slabs), splits)
     if dw is None:
         dw = torch.empty((Kreal, Creal, R, R), dtype=torch.float32, device=x.device)
-    call('um_conv_wgrad_reduce', ptr(slabs), splits, K, Kreal, R, C, Creal, ptr(dw), 0)
+    n, a0, b0, l0 = _seg_arrays(segs)
+    call('um_conv_wgrad_reduce_seg', ptr(slabs), splits, K, Kreal, R, C, Creal, ptr(dw), 0,
+         n, a0, b0, l0)
     return dw
 
 
@@ -156,7 +170,8 @@ class ConvSpec:
     """Static description of a conv block (non-tensor autograd argument)."""
 
     def __init__(self, conv: torch.nn.Conv2d, bn: Optional[torch.nn.Module], pad: int,
-                 pad_mode: int, elu: bool = True):
+                 pad_mode: int, elu: bool = True, segs=None):
+        self.segs = segs
         self.conv = conv
         self.bn = bn
         self.stride = conv.stride[0]
@@ -173,7 +188,7 @@ class ConvBNELUFn(torch.autograd.Function):
         K, Creal, R, _ = weight.shape
         bn = spec.bn
         dev = x.device
-        wf, wT = _pack(weight, Cp, x.dtype)
+        wf, wT = _pack(weight, Cp, x.dtype, segs=spec.segs)
         P = (H + 2 * spec.pad - R) // spec.stride + 1
         Q = (W + 2 * spec.pad - R) // spec.stride + 1
         M = N * P * Q
@@ -272,21 +287,29 @@ class ConvBNELUFn(torch.autograd.Function):
             if gamma is not None and spec.bn is not None:
                 raise NotImplementedError('backward through an eval-mode BatchNorm')
         dy = torch.empty(y.shape, dtype=adt, device=dev)
+        need_b = ctx.needs_input_grad[2]
+        nbp = query('um_bn_bwd_parts', M)
+        bparts = torch.empty((nbp, K), dtype=torch.float32, device=dev) if need_b else None
         call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
              ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1), ptr(k2),
-             ptr(k3), ptr(dy), K)
-        dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode)
-        dbias = _colsum(dy, K) if ctx.needs_input_grad[2] else None
+             ptr(k3), ptr(dy), K, ptr(bparts))
+        dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode,
+                         segs=spec.segs)
+        dbias = None
+        if need_b:
+            dbias = torch.empty(K, dtype=torch.float32, device=dev)
+            call('um_reduce_rows', ptr(bparts), nbp, K, K, ptr(dbias), 0)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _conv_dgrad(dy, wT, (N, H, W, Cp), K, R, spec.stride, spec.pad, spec.pad_mode)
         return dx, dW, dbias, dgamma, dbeta, dw1, dw2, None
 
 
-def conv_bn_elu(x, conv, bn, pad, pad_mode, se=None, elu=True):
+def conv_bn_elu(x, conv, bn, pad, pad_mode, se=None, elu=True, segs=None):
     """Conv2d -> BatchNorm2d (train: batch stats; eval: running stats; None:
-    identity) -> ELU [-> SE gate].  Returns a, or (a, gate) with ``se``."""
-    spec = ConvSpec(conv, bn, pad, pad_mode, elu)
+    identity) -> ELU [-> SE gate].  Returns a, or (a, gate) with ``se``.
+    ``segs``: input-channel placement of a concat input (see ``concat``)."""
+    spec = ConvSpec(conv, bn, pad, pad_mode, elu, segs)
     w1 = se.excite[0].weight if se is not None else None
     w2 = se.excite[2].weight if se is not None else None
     affine = bn is not None and bn.affine
@@ -436,7 +459,6 @@ class ConcatFn(torch.autograd.Function):
         N, H, W, Ctot, dtype = meta['out']
         srcs, it = [], iter(tensors)
         structs = (L.CatSrc * len(meta['srcs']))()
-        coff = 0
         saved = []
         for i, (op, C) in enumerate(meta['srcs']):
             t = next(it)
@@ -444,8 +466,7 @@ class ConcatFn(torch.autograd.Function):
             srcs.append((t, g))
             h, w = (H, W) if op == L.CAT_COPY else (H // 2, W // 2)
             structs[i] = L.CatSrc(t.data_ptr(), g.data_ptr() if g is not None else None, C,
-                                  t.shape[-1], op, coff, _dt(t), h, w)
-            coff += C
+                                  t.shape[-1], op, meta['coffs'][i], _dt(t), h, w)
             saved += [t] + ([g] if g is not None else [])
         out = torch.empty((N, H, W, Ctot), dtype=dtype, device=tensors[0].device)
         call('um_concat_build', L.dtype_code(dtype), N, H, W, ptr(out), Ctot, Ctot,
@@ -461,9 +482,9 @@ class ConcatFn(torch.autograd.Function):
         g = g.contiguous()
         saved = list(ctx.saved_tensors)
         grads = []
-        coff = 0
         k = 1  # index into needs_input_grad (0 = meta)
         for i, (op, C) in enumerate(meta['srcs']):
+            coff = meta['coffs'][i]
             t = saved.pop(0)
             gate = saved.pop(0) if meta['gates'][i] else None
             need_t = ctx.needs_input_grad[k]
@@ -480,20 +501,31 @@ class ConcatFn(torch.autograd.Function):
             if gate is not None:
                 grads.append(dg)
             k += 2 if gate is not None else 1
-            coff += C
         return (None, *grads)
 
 
 def concat(sources: Sequence[CatSource], N, H, W, dtype):
-    Ctot = ceil8(sum(s.C for s in sources))
+    """Materialise a decoder concat.  Every source starts at an 8-aligned
+    channel offset (vector loads/stores); returns (tensor, segs) where segs
+    maps the reference's input channels of the consuming conv to the packed
+    channels ([(ref_c0, packed_c0, len)], None when identical)."""
+    coffs, segs, ref, off = [], [], 0, 0
+    for s in sources:
+        coffs.append(off)
+        segs.append((ref, off, s.C))
+        ref += s.C
+        off = ceil8(off + s.C)
+    Ctot = ceil8(coffs[-1] + sources[-1].C)
+    if all(a == b for a, b, _ in segs):
+        segs = None
     meta = {'out': (N, H, W, Ctot, dtype), 'srcs': [(s.op, s.C) for s in sources],
-            'gates': [s.gate is not None for s in sources]}
+            'gates': [s.gate is not None for s in sources], 'coffs': coffs}
     tensors = []
     for s in sources:
         tensors.append(s.t)
         if s.gate is not None:
             tensors.append(s.gate)
-    return ConcatFn.apply(meta, *tensors)
+    return ConcatFn.apply(meta, *tensors), segs
 
 
 # ---------------------------------------------------------------- disp head --
@@ -522,7 +554,7 @@ class DispHeadFn(torch.autograd.Function):
         call('um_sigmoid_scale_bwd', _dt(dl), M, K, ptr(d), K, ptr(dd), dd.shape[-1], ctx.scale,
              ptr(dl), Kp)
         dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)
-        db = _colsum(dl, K)
+        db = _colsum(dl, Kp)[:K]  # channels K..Kp of dl are zero
         dx = _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT) \
             if ctx.needs_input_grad[0] else None
         return dx, dW, db, None
