@@ -72,8 +72,8 @@ def build(cfg, dtype, device, world):
     torch.manual_seed(0)
     m = M.RandomlyConnectedModel(**cfg['model'], dtype=dtype).to(device).train()
     if world > 1:
-        m = torch.nn.SyncBatchNorm.convert_sync_batchnorm(m)
-        m = torch.nn.parallel.DistributedDataParallel(m, device_ids=[device.index])
+        from train.parallel import data_parallel
+        m = data_parallel(m, device.index)
     lf = TukraUncertaintyLoss(**cfg['loss'])
     opt = Adam(m.parameters(), 1e-4)
     return m, lf, opt
@@ -101,44 +101,56 @@ def loss_bwd_bytes(N, H, W):
     return N * H * W * 4 * (6 + 6 + 4 + 2 + 4)
 
 
-def conv_flops(args):
-    # um_conv2d_fwd(dtype, N, H, W, C, ldx, x, wf, bias, K, R, stride, pad, mode, P, Q, ...)
-    N, C, K, R, P, Q = args[1], args[4], args[9], args[10], args[14], args[15]
-    return 2.0 * N * P * Q * K * R * R * C
+CONV_ENTRIES = {
+    # C-ABI entry -> the kernel templates it launches (rocprof names)
+    'um_conv2d_fwd': 'conv_gemm_kernel<T, 0, ...>',
+    'um_conv2d_dgrad': 'conv_gemm_kernel<T, 1, ...>',
+    'um_conv2d_wgrad': 'wgrad_bf16_kernel<BM> / wgrad_kernel<T,64,64>',
+}
 
 
 def measure_roofline(m, lf, opt, left, right, scale, dtype):
     """Time every launch of the candidate kernels with HIP events on the
-    launch stream; report the one with the largest total time."""
+    launch stream (one eager step); the entry with the largest total time is
+    the dominant kernel.  Conv work = algorithmic FLOPs with the real channel
+    counts (2*N*P*Q*K*R*R*C per pass, attached at each call site)."""
     from umamd import _lib
-    rec = _lib.Recorder({'um_conv2d_fwd', 'um_loss_bwd_scale'})
+    rec = _lib.Recorder(set(CONV_ENTRIES) | {'um_loss_bwd_scale'})
     with rec:
         step(m, lf, opt, left, right, scale)
     torch.cuda.synchronize()
     groups = {}
-    for name, args, ms in rec.results():
-        groups.setdefault(name, []).append((args, ms))
-    tot = {k: sum(ms for _, ms in v) for k, v in groups.items()}
-    dom = max(tot, key=tot.get)
-    items = groups[dom]
-    avg_ms = tot[dom] / len(items)
-    if dom == 'um_loss_bwd_scale':
-        # args: img, rec, pred, pld, N, H, W, ...
-        byts = sum(loss_bwd_bytes(a[4], a[5], a[6]) for a, _ in items) / len(items)
-        ach = byts / (avg_ms * 1e-3) / 1e9
-        return {'kernel': 'loss_bwd_kernel (um_loss_bwd_scale)', 'bound': 'hbm',
-                'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                'frac': round(ach / HBM_PEAK_GBS, 4), 'traffic': None,
-                'launches_per_step': len(items), 'avg_launch_ms': round(avg_ms, 4),
-                'all_kernels_ms': {k: round(v, 3) for k, v in tot.items()}}
-    flops = sum(conv_flops(a) for a, _ in items) / len(items)
-    ach = flops / (avg_ms * 1e-3) / 1e12
+    for name, args, ms, work in rec.results():
+        groups.setdefault(name, []).append((args, ms, work))
     peak = BF16_PEAK_TFLOPS if dtype == 'bf16' else F32_PEAK_TFLOPS
-    return {'kernel': 'conv_gemm_kernel fwd (um_conv2d_fwd)', 'bound': 'mfma',
-            'achieved': round(ach, 2), 'peak': peak, 'unit': 'TFLOP/s',
-            'frac': round(ach / peak, 4), 'traffic': None,
-            'launches_per_step': len(items), 'avg_launch_ms': round(avg_ms, 4),
-            'all_kernels_ms': {k: round(v, 3) for k, v in tot.items()}}
+    table = {}
+    for name, items in groups.items():
+        tot_ms = sum(ms for _, ms, _ in items)
+        if name == 'um_loss_bwd_scale':
+            # args: img, rec, pred, pld, N, H, W, ...
+            work = sum(loss_bwd_bytes(a[4], a[5], a[6]) for a, _, _ in items)
+            ach = work / (tot_ms * 1e-3) / 1e9
+            table[name] = {'kernel': 'loss_bwd_kernel', 'bound': 'hbm', 'achieved': round(ach, 1),
+                           'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                           'frac': round(ach / HBM_PEAK_GBS, 4)}
+        else:
+            work = sum(w for _, _, w in items)
+            ach = work / (tot_ms * 1e-3) / 1e12
+            table[name] = {'kernel': CONV_ENTRIES[name], 'bound': 'mfma',
+                           'achieved': round(ach, 2), 'peak': peak, 'unit': 'TFLOP/s',
+                           'frac': round(ach / peak, 4)}
+        table[name].update({'launches_per_step': len(items),
+                            'avg_launch_ms': round(tot_ms / len(items), 4),
+                            'total_ms_per_step': round(tot_ms, 3),
+                            'work_per_launch': work / len(items)})
+    dom = max(table, key=lambda k: table[k]['total_ms_per_step'])
+    out = dict(table[dom])
+    out['entry'] = dom
+    out['traffic'] = None
+    out['candidates'] = {k: {kk: v[kk] for kk in ('achieved', 'unit', 'frac', 'avg_launch_ms',
+                                                  'launches_per_step', 'total_ms_per_step')}
+                         for k, v in table.items()}
+    return out
 
 
 # --------------------------------------------------------- CPU baseline ----
@@ -182,7 +194,11 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
-        dist.init_process_group('nccl', init_method='env://')
+        # 'nccl' is RCCL; UMAMD_DIST_BACKEND=gloo rehearses the N>1 path with
+        # several ranks on one GPU (RCCL needs a GPU per rank)
+        dist.init_process_group(os.environ.get('UMAMD_DIST_BACKEND', 'nccl'),
+                                init_method='env://')
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device('cuda', local)
     cfg = load_cfg(a.config, a.loss_type)

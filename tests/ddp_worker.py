@@ -1,0 +1,116 @@
+"""Worker for the data-parallel tests (launched as a subprocess per rank by
+tests/test_ddp_cpu.py and tests/test_gpu_ddp.py; not collected by pytest).
+
+mode 'cpu'    : gloo, CPU only -- host logic of the DP wrapper: SyncBN
+                conversion, BNSync world detection, f64 stats all-reduce, DDP
+                construction and gradient averaging hooks on plain tensors.
+mode 'single' : one process, full batch on cuda:0, one train step.
+mode 'ddp'    : gloo ranks sharing cuda:0, each on its batch shard, one
+                DDP+SyncBN train step (SURVEY 8c golden (v): SyncBN identity).
+Writes results to <out>/<mode>_<rank>.pt (torch.save of tensors only).
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+for p in (os.path.join(REPO, 'uncertainty-model_amd'), REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import yaml  # noqa: E402
+
+
+def cfg():
+    with open(os.path.join(REPO, 'config.yml')) as f:
+        c = yaml.safe_load(f)
+    c['model']['encoder']['load_graph'] = os.path.join(REPO, c['model']['encoder']['load_graph'])
+    c['loss']['error_loss_config']['loss_type'] = 'bayesian'
+    return c
+
+
+def model_with_formula_weights(c, dtype='fp32'):
+    import model as M
+    from oracle import model as OM, step as OS
+    m = M.RandomlyConnectedModel(**c['model'], dtype=dtype)
+    specs = OS.param_specs(c['model'], OM.load_stage_graphs(c['model']['encoder']))
+    m.load_state_dict(OS.formula_state_dict(specs))
+    return m
+
+
+def batch(total=4, h=64, w=128):
+    g = torch.Generator().manual_seed(1234)
+    return torch.rand(total, 3, h, w, generator=g), torch.rand(total, 3, h, w, generator=g)
+
+
+def run_cpu(rank, world, out):
+    from train.parallel import count_sync_bn, data_parallel
+    from umamd.functional import BNSync
+    c = cfg()
+    sm = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model_with_formula_weights(c))
+    bns = [mod for mod in sm.modules() if isinstance(mod, torch.nn.SyncBatchNorm)]
+    st = torch.arange(6, dtype=torch.float64) * (rank + 1)
+    BNSync(bns[0]).all_reduce(st)
+    # torch's DDP refuses SyncBatchNorm on CPU modules and the model's
+    # forward is HIP-only: gradient averaging is checked on a small module
+    # through the same wrapper (gradient_as_bucket_view, buckets, hooks)
+    torch.manual_seed(0)
+    dp = data_parallel(torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Linear(16, 4)),
+                       sync_bn=False)
+    x = torch.ones(3, 8) * (rank + 1)
+    dp(x).sum().backward()
+    nparams = sum(p.numel() for p in model_with_formula_weights(c).parameters())
+    torch.save({'n_sync_bn': torch.tensor(count_sync_bn(sm)),
+                'world_seen': torch.tensor(BNSync(bns[0]).world),
+                'stats': st,
+                'grads': [p.grad.clone() for p in dp.parameters()],
+                'nparams': torch.tensor(nparams)},
+               os.path.join(out, f'cpu_{rank}.pt'))
+
+
+def run_step(mode, rank, world, out):
+    from train.loss import TukraUncertaintyLoss
+    from train.parallel import data_parallel, unwrap
+    from train.train import train_step
+    from umamd.optim import Adam
+    c = cfg()
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    m = model_with_formula_weights(c).to(dev).train()
+    if mode == 'ddp':
+        m = data_parallel(m, 0)
+    left, right = batch()
+    per = left.shape[0] // world
+    left = left[rank * per:(rank + 1) * per].to(dev)
+    right = right[rank * per:(rank + 1) * per].to(dev)
+    lf = TukraUncertaintyLoss(**c['loss'])
+    opt = Adam(m.parameters(), 1e-4)
+    dl, el = train_step(m, left, right, lf, opt, 0.3)
+    torch.cuda.synchronize()
+    # Adam reads .grad but does not modify it; under DDP these are the
+    # all-reduced (averaged) bucket views
+    grads = {n: p.grad.detach().clone().cpu() for n, p in unwrap(m).named_parameters()}
+    sd = {k: v.detach().clone().cpu() for k, v in unwrap(m).state_dict().items()}
+    torch.save({'disp': torch.tensor(float(dl)), 'err': torch.tensor(float(el)),
+                'grads': grads, 'state': sd}, os.path.join(out, f'{mode}_{rank}.pt'))
+
+
+def main():
+    mode, out = sys.argv[1], sys.argv[2]
+    rank = int(os.environ.get('RANK', '0'))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if mode in ('cpu', 'ddp'):
+        dist.init_process_group('gloo', init_method='env://', rank=rank, world_size=world)
+    if mode == 'cpu':
+        run_cpu(rank, world, out)
+    else:
+        run_step(mode, rank, world, out)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

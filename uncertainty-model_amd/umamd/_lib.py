@@ -145,16 +145,18 @@ class Recorder:
         Recorder._active = None
 
     def results(self):
-        """[(name, args, ms)] -- synchronises on the events."""
+        """[(name, args, ms, work)] -- synchronises on the events.  ``work``
+        is the algorithmic FLOP count the caller attached (or None)."""
         out = []
-        for name, args, e0, e1 in self.items:
+        for name, args, e0, e1, work in self.items:
             e1.synchronize()
-            out.append((name, args, e0.elapsed_time(e1)))
+            out.append((name, args, e0.elapsed_time(e1), work))
         return out
 
 
-def call(name: str, *args):
-    """Call a C-ABI entry; the trailing stream argument is appended."""
+def call(name: str, *args, work=None):
+    """Call a C-ABI entry; the trailing stream argument is appended.
+    ``work`` (algorithmic FLOPs of this launch) is only kept for a Recorder."""
     fn = getattr(lib(), name)
     rec = Recorder._active
     if rec is not None and name in rec.names:
@@ -163,7 +165,7 @@ def call(name: str, *args):
         e0.record()
         rc = fn(*args, stream())
         e1.record()
-        rec.items.append((name, args, e0, e1))
+        rec.items.append((name, args, e0, e1, work))
     else:
         rc = fn(*args, stream())
     if rc != 0:

@@ -67,8 +67,13 @@ def _pack(weight: torch.Tensor, Cp: int, dtype: torch.dtype, wf=True, wT=True, l
     return f, t
 
 
+def _conv_flops(N, P, Q, K, R, C):
+    """algorithmic FLOPs of a conv pass with the REAL (unpadded) channel counts"""
+    return 2.0 * N * P * Q * K * R * R * C
+
+
 def _conv_fwd(x, wf, bias, K, R, stride, pad, pad_mode, out_dtype=None, epi=L.EPI_NONE,
-              epi_scale=1.0, residual=None, stats=None, out=None, ldo=None):
+              epi_scale=1.0, residual=None, stats=None, out=None, ldo=None, creal=None):
     N, H, W, C = x.shape
     P = (H + 2 * pad - R) // stride + 1
     Q = (W + 2 * pad - R) // stride + 1
@@ -78,17 +83,20 @@ def _conv_fwd(x, wf, bias, K, R, stride, pad, pad_mode, out_dtype=None, epi=L.EP
         out = torch.empty((N, P, Q, ldo), dtype=od, device=x.device)
     call('um_conv2d_fwd', _dt(x), N, H, W, C, C, ptr(x), ptr(wf), ptr(bias), K, R, stride, pad,
          pad_mode, P, Q, L.dtype_code(od), ptr(out), out.shape[-1], epi, float(epi_scale),
-         ptr(residual), residual.shape[-1] if residual is not None else 0, ptr(stats))
+         ptr(residual), residual.shape[-1] if residual is not None else 0, ptr(stats),
+         work=_conv_flops(N, P, Q, K, R, creal or C))
     return out
 
 
-def _conv_dgrad(dy, wT, x_shape, K, R, stride, pad, pad_mode, dx=None, accumulate=False):
+def _conv_dgrad(dy, wT, x_shape, K, R, stride, pad, pad_mode, dx=None, accumulate=False,
+                creal=None, kreal=None):
     N, H, W, C = x_shape
     _, P, Q, ldy = dy.shape
     if dx is None:
         dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
     call('um_conv2d_dgrad', _dt(dy), N, H, W, C, C, ptr(dx), int(accumulate), ptr(wT), K, R,
-         stride, pad, pad_mode, P, Q, ptr(dy), ldy)
+         stride, pad, pad_mode, P, Q, ptr(dy), ldy,
+         work=_conv_flops(N, P, Q, kreal or K, R, creal or C))
     return dx
 
 
@@ -101,7 +109,7 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
     splits = query('um_conv_wgrad_splits', M, K, RRC)
     slabs = torch.empty((splits, K, RRC), dtype=torch.float32, device=x.device)
     call('um_conv2d_wgrad', _dt(x), N, H, W, C, C, ptr(x), K, R, stride, pad, pad_mode, P, Q,
-         ptr(dy), ldy, ptr(slabs), splits)
+         ptr(dy), ldy, ptr(slabs), splits, work=_conv_flops(N, P, Q, Kreal, R, Creal))
     if dw is None:
         dw = torch.empty((Kreal, Creal, R, R), dtype=torch.float32, device=x.device)
     n, a0, b0, l0 = _seg_arrays(segs)
@@ -200,14 +208,14 @@ class ConvBNELUFn(torch.autograd.Function):
             parts = torch.empty((nparts, K, 2), dtype=torch.float32, device=dev)
             y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
                           out_dtype=torch.float32,
-                          epi=L.EPI_STATS if training else L.EPI_NONE, stats=parts)
+                          epi=L.EPI_STATS if training else L.EPI_NONE, stats=parts, creal=Creal)
             mean, invstd, scale, shift = _bn_forward_coeffs(parts, nparts, K, M, bn, sync,
                                                             training, dev)
         else:  # ConvELUBlock(batch_norm=False): identity normalisation
             sync = None
             training = False
             y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
-                          out_dtype=torch.float32)
+                          out_dtype=torch.float32, creal=Creal)
             mean = torch.zeros(K, dtype=torch.float32, device=dev)
             shift = mean
             invstd = torch.ones(K, dtype=torch.float32, device=dev)
@@ -301,7 +309,8 @@ class ConvBNELUFn(torch.autograd.Function):
             call('um_reduce_rows', ptr(bparts), nbp, K, K, ptr(dbias), 0)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _conv_dgrad(dy, wT, (N, H, W, Cp), K, R, spec.stride, spec.pad, spec.pad_mode)
+            dx = _conv_dgrad(dy, wT, (N, H, W, Cp), K, R, spec.stride, spec.pad, spec.pad_mode,
+                             creal=Creal)
         return dx, dW, dbias, dgamma, dbeta, dw1, dw2, None
 
 
@@ -537,7 +546,8 @@ class DispHeadFn(torch.autograd.Function):
         Kp = ceil8(K)
         wf, wT = _pack(weight, Cp, x.dtype, ldT=Kp)
         d = _conv_fwd(x, wf, bias.detach().float().contiguous(), K, R, 1, 1, L.PAD_REFLECT,
-                      out_dtype=torch.float32, epi=L.EPI_SIGMOID_SCALE, epi_scale=scale)
+                      out_dtype=torch.float32, epi=L.EPI_SIGMOID_SCALE, epi_scale=scale,
+                      creal=Creal)
         ctx.scale = float(scale)
         ctx.save_for_backward(x, wT, d)
         ctx.geom = (K, Kp, Creal, R)
@@ -555,7 +565,8 @@ class DispHeadFn(torch.autograd.Function):
              ptr(dl), Kp)
         dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)
         db = _colsum(dl, Kp)[:K]  # channels K..Kp of dl are zero
-        dx = _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT) \
+        dx = _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT, creal=Creal,
+                         kreal=K) \
             if ctx.needs_input_grad[0] else None
         return dx, dW, db, None
 
