@@ -55,21 +55,30 @@ int um_version(void);
 /* number of BN partial rows written by um_conv2d_fwd with UM_EPI_STATS for M output pixels and K channels */
 int um_conv_stats_parts(int M, int K);
 
+/* split-K workspace (bytes) the kernels want for a shape; 0 = no split.
+ * Passing a smaller (or null) workspace is allowed: the split shrinks. */
+long um_conv_fwd_ws(int dtype, int N, int P, int Q, int K, int R, int C);
+long um_conv_dgrad_ws(int dtype, int N, int H, int W, int C, int R, int K, int stride);
+
 int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                   const void* wf, const float* bias, int K, int R, int stride,
                   int pad, int pad_mode, int P, int Q, int ydtype, void* y,
                   int ldy, int epilogue, float epi_scale, const void* residual,
-                  int ldr, float* stats_partials, hipStream_t stream);
+                  int ldr, float* stats_partials, void* ws, long ws_bytes,
+                  hipStream_t stream);
 
 /* data gradient: dx[N,H,W,C] (= or +=) conv^T(dy[N,P,Q,K], wT) incl. the
  * reflect-pad fold and the stride-2 scatter */
 int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx,
                     int accumulate, const void* wT, int K, int R, int stride,
                     int pad, int pad_mode, int P, int Q, const void* dy, int ldy,
-                    hipStream_t stream);
+                    void* ws, long ws_bytes, hipStream_t stream);
 
-/* weight gradient partial slabs [splits][K][R*R*C] (f32); splits from um_conv_wgrad_splits */
-int um_conv_wgrad_splits(int M, int K, int RRC);
+/* weight gradient partial slabs [splits][K][R*R*C] (f32); splits from
+ * um_conv_wgrad_splits (which also picks the kernel: the halo-tiled one for
+ * bf16 small-channel spatial convs, the implicit-GEMM one otherwise) */
+int um_conv_wgrad_splits(int dtype, int N, int H, int W, int C, int ldx, int K, int R,
+                         int stride, int pad, int pad_mode, int P, int Q, int ldy);
 int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                     int K, int R, int stride, int pad, int pad_mode, int P, int Q,
                     const void* dy, int ldy, float* slabs, int splits,

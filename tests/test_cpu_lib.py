@@ -34,7 +34,11 @@ def test_library_exports_header_symbols():
 def test_host_queries_without_gpu():
     from umamd._lib import query
     assert query('um_conv_stats_parts', 1000, 32) == 8
-    assert query('um_conv_wgrad_splits', 262144, 32, 1568) >= 1
+    # bf16 stage-1 7x7 conv (halo kernel) and an f32 one (implicit GEMM)
+    assert query('um_conv_wgrad_splits', 1, 8, 128, 256, 32, 32, 32, 7, 1, 3, 0, 128, 256, 32) >= 1
+    assert query('um_conv_wgrad_splits', 0, 8, 128, 256, 32, 32, 32, 7, 1, 3, 0, 128, 256, 32) >= 1
+    assert query('um_conv_fwd_ws', 1, 8, 8, 16, 512, 3, 512) > 0  # deep layer: split-K
+    assert query('um_conv_fwd_ws', 1, 8, 128, 256, 32, 7, 32) == 0
     assert query('um_adam_chunk') == 4096
 
 

@@ -230,7 +230,11 @@ def test_train_step_fp32(lt):
                     if _pre_bn_bias(name):
                         continue
                     got = float(sd[name].double().sum())
-                    assert abs(got - float(z[k])) <= 1e-4 * float(z['param_abs/' + name]) + 1e-5, name
+                    # Adam's first step is lr*sign(g): an element whose gradient is
+                    # within summation noise of zero moves by +-lr either way, so
+                    # allow two such sign flips (2 * 2lr) per tensor
+                    flips = 2 * 2 * 1e-4
+                    assert abs(got - float(z[k])) <= 1e-4 * float(z['param_abs/' + name]) + flips, name
 
 
 def test_train_step_bf16_loss_delta():

@@ -41,6 +41,10 @@ CONV_CASES = [
     (40, 48, 3, 1, 'reflect', 10, 14),
     (24, 40, 1, 1, 'zero', 6, 10),
     (16, 8, 3, 1, 'reflect', 4, 6),
+    # small-M deep layers: split-K partials + epilogue kernel (fwd and dgrad)
+    (256, 512, 3, 1, 'zero', 4, 6),
+    (128, 96, 3, 1, 'reflect', 6, 10),
+    (64, 32, 5, 1, 'zero', 3, 5),
 ]
 
 
@@ -290,3 +294,39 @@ def test_conv_large(dtype, case):
     print(f'conv_large {case} {dtype}: y {errs[0]:.3e} dx {errs[1]:.3e} dw {errs[2]:.3e}')
     tol = 1e-4 if dtype == torch.float32 else 3e-2
     assert errs[0] < tol and errs[1] < tol * 2 and errs[2] < tol * 2, errs
+
+
+# weight gradient against torch (f64 CPU) for the shapes the halo-tiled kernel
+# covers (bf16, Q >= 32): 7x7/5x5 encoder convs incl. stride 2, 3x3 reflect
+# decoder convs incl. the 4-channel disparity head, and a K=128 conv
+@pytest.mark.parametrize('case', [
+    (32, 32, 7, 1, 'zero', 12, 70),
+    (8, 32, 7, 2, 'zero', 20, 72),
+    (64, 64, 5, 1, 'zero', 9, 40),
+    (32, 64, 5, 2, 'zero', 16, 66),
+    (48, 32, 3, 1, 'reflect', 10, 36),
+    (32, 8, 3, 1, 'reflect', 7, 64),
+    (64, 128, 3, 1, 'reflect', 6, 33),
+])
+def test_wgrad(case):
+    from umamd import functional as U
+    from umamd._lib import PAD_REFLECT, PAD_ZERO, query
+    C, K, R, st, mode, H, W = case
+    N = 2
+    pad = (R - 1) // 2
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(N, C, H, W, generator=g) - 0.5
+    xp = F.pad(x.double(), (pad,) * 4, mode='reflect' if mode == 'reflect' else 'constant')
+    P = (H + 2 * pad - R) // st + 1
+    Q = (W + 2 * pad - R) // st + 1
+    dy = torch.randn(N, K, P, Q, generator=g)
+    xb = x.to(torch.bfloat16)
+    dyb = dy.to(torch.bfloat16)
+    xpb = F.pad(xb.double(), (pad,) * 4, mode='reflect' if mode == 'reflect' else 'constant')
+    ref = torch.nn.grad.conv2d_weight(xpb, (K, C, R, R), dyb.double(), stride=st)
+    pm = PAD_REFLECT if mode == 'reflect' else PAD_ZERO
+    got = U._conv_wgrad(_nhwc(xb).to(DEV), _nhwc(dyb).to(DEV), K, K, C, R, st, pad, pm)
+    splits = query('um_conv_wgrad_splits', 1, N, H, W, C, C, K, R, st, pad, pm, P, Q, K)
+    err = _rel(got, ref)
+    print(f'wgrad {case}: splits {splits} rel {err:.3e}')
+    assert err < 1e-4, err

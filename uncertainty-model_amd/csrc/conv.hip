@@ -1,6 +1,9 @@
-// Implicit-GEMM convolutions on MFMA for gfx950 (CDNA4).
+// Implicit-GEMM convolutions on MFMA for gfx950 (CDNA4): C-ABI entries, the
+// weight gradient, weight packing and column reductions.  Forward convs and
+// stride-1 data gradients run on the tap-major kernel of igemm.hip; the
+// general gather kernel below serves the stride-2 data gradient.
 //
-// One kernel template serves the forward conv and the data gradient:
+// General kernel (forward form kept for reference, dgrad form in use):
 //   forward  : Y[m=(n,p,q)][k]  = sum_{(r,s,c)} X[n, p*st-pad+r, q*st-pad+s, c] * Wf[k][r][s][c]
 //   dgrad    : DX[m=(n,h,w)][c] = sum_{(r,s,k)} DY[src(n,h,w,r,s)][k] * WT[c][r][s][k]
 // where src() inverts the forward gather: the stride-2 parity filter and the
@@ -18,6 +21,8 @@
 #include <algorithm>
 
 #include "common.h"
+#include "igemm.h"
+#include "wgrad_halo.h"
 
 namespace {
 
@@ -766,13 +771,22 @@ extern "C" {
 
 int um_conv_stats_parts(int M, int K) {
   (void)K;
-  return ceil_div(M, STATS_BM);
+  return ceil_div(M, STATS_BM);  // = igemm's STATS_ROWS blocks
+}
+
+long um_conv_fwd_ws(int dtype, int N, int P, int Q, int K, int R, int C) {
+  return umamd::igemm_ws_bytes(dtype, N * P * Q, K, R, C);
+}
+
+long um_conv_dgrad_ws(int dtype, int N, int H, int W, int C, int R, int K, int stride) {
+  return stride == 1 ? umamd::igemm_ws_bytes(dtype, N * H * W, C, R, K) : 0;
 }
 
 int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x, const void* wf,
                   const float* bias, int K, int R, int stride, int pad, int pad_mode, int P,
                   int Q, int ydtype, void* y, int ldy, int epilogue, float epi_scale,
-                  const void* residual, int ldr, float* stats, hipStream_t st) {
+                  const void* residual, int ldr, float* stats, void* ws, long ws_bytes,
+                  hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0 && ldx % 8 == 0, "um_conv2d_fwd: C (%d) and ldx (%d) must be multiples of 8", C, ldx);
   UM_CHECK_ARG(stride == 1 || stride == 2, "um_conv2d_fwd: stride %d", stride);
   UM_CHECK_ARG(P == (H + 2 * pad - R) / stride + 1 && Q == (W + 2 * pad - R) / stride + 1,
@@ -780,27 +794,44 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
   UM_CHECK_ARG(pad_mode == UM_PAD_ZERO || pad < H, "um_conv2d_fwd: reflect pad too large");
   UM_CHECK_ARG(epilogue != UM_EPI_STATS || stats != nullptr, "um_conv2d_fwd: stats buffer missing");
   UM_CHECK_ARG(epilogue != UM_EPI_RESIDUAL || residual != nullptr, "um_conv2d_fwd: residual missing");
-  ConvArgs a{};
-  a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx;
-  a.P = P; a.Q = Q; a.K = K; a.ldy = ldy;
-  a.R = R; a.stride = stride; a.pad = pad; a.pad_mode = pad_mode;
-  a.a_src = x; a.b_src = wf; a.bias = bias; a.out = y; a.ld_out = ldy;
-  a.M = N * P * Q; a.NC = K; a.KK = R * R * C;
-  a.epilogue = epilogue; a.accumulate = 0;
-  a.out_f32 = (ydtype == UM_F32);
-  a.epi_scale = epi_scale; a.residual = residual; a.ldr = ldr; a.stats = stats;
   UM_CHECK_ARG(ydtype == dtype || ydtype == UM_F32, "um_conv2d_fwd: ydtype must be dtype or f32");
-  if (a.M == 0) return UM_OK;
-  return dtype == UM_BF16 ? dispatch_conv<bf16_t, MODE_FWD>(a, st)
-                          : dispatch_conv<float, MODE_FWD>(a, st);
+  umamd::IgArgs a{};
+  a.a = x; a.ah = H; a.aw = W; a.ach = C; a.lda = ldx;
+  a.on = N; a.oh = P; a.ow = Q;
+  a.R = R; a.stride = stride; a.pad = pad;
+  a.pmode = pad_mode == UM_PAD_REFLECT ? umamd::IG_PAD_REFLECT : umamd::IG_PAD_ZERO;
+  a.fold_pad = 0; a.flip = 0;
+  a.b = wf; a.ldb = (long)R * R * C;
+  a.NC = K; a.M = N * P * Q;
+  a.bias = bias; a.out = y; a.ld_out = ldy; a.out_f32 = (ydtype == UM_F32);
+  a.epilogue = epilogue; a.accumulate = 0; a.epi_scale = epi_scale;
+  a.residual = residual; a.ldr = ldr; a.stats = stats;
+  return umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
 }
 
 int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, int accumulate,
                     const void* wT, int K, int R, int stride, int pad, int pad_mode, int P,
-                    int Q, const void* dy, int ldy, hipStream_t st) {
+                    int Q, const void* dy, int ldy, void* ws, long ws_bytes, hipStream_t st) {
   UM_CHECK_ARG(K % 8 == 0 && ldy % 8 == 0, "um_conv2d_dgrad: K (%d) and ldy (%d) must be multiples of 8", K, ldy);
   UM_CHECK_ARG(stride == 1 || stride == 2, "um_conv2d_dgrad: stride %d", stride);
   UM_CHECK_ARG(pad_mode == UM_PAD_ZERO || stride == 1, "um_conv2d_dgrad: reflect needs stride 1");
+  if (stride == 1) {
+    UM_CHECK_ARG(P == H + 2 * pad - R + 1 && Q == W + 2 * pad - R + 1, "um_conv2d_dgrad: size");
+    UM_CHECK_ARG(pad_mode == UM_PAD_ZERO || (P == H && Q == W && pad <= 1),
+                 "um_conv2d_dgrad: reflect transpose needs a same-size conv with pad <= 1");
+    umamd::IgArgs a{};
+    a.a = dy; a.ah = P; a.aw = Q; a.ach = K; a.lda = ldy;
+    a.on = N; a.oh = H; a.ow = W;
+    a.R = R; a.stride = 1; a.pad = R - 1 - pad;
+    a.pmode = pad_mode == UM_PAD_REFLECT ? umamd::IG_FOLD : umamd::IG_PAD_ZERO;
+    a.fold_pad = pad; a.flip = 1;
+    a.b = wT; a.ldb = (long)R * R * K;
+    a.NC = C; a.M = N * H * W;
+    a.bias = nullptr; a.out = dx; a.ld_out = ldx; a.out_f32 = (dtype == UM_F32);
+    a.epilogue = UM_EPI_NONE; a.accumulate = accumulate; a.epi_scale = 1.f;
+    a.residual = nullptr; a.ldr = 0; a.stats = nullptr;
+    return umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
+  }
   ConvArgs a{};
   a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx;
   a.P = P; a.Q = Q; a.K = K; a.ldy = ldy;
@@ -815,7 +846,7 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
 
 static int wgrad_bm(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
 
-int um_conv_wgrad_splits(int M, int K, int RRC) {
+static int generic_wgrad_splits(int M, int K, int RRC) {
   // tiles of the bf16 kernel (the f32 kernel uses 64x64 tiles; same split count)
   const long tiles = (long)ceil_div(K, wgrad_bm(K)) * ceil_div(RRC, 128);
   long splits = (768 + tiles - 1) / tiles;
@@ -827,11 +858,33 @@ int um_conv_wgrad_splits(int M, int K, int RRC) {
   return (int)splits;
 }
 
+int um_conv_wgrad_splits(int dtype, int N, int H, int W, int C, int ldx, int K, int R,
+                         int stride, int pad, int pad_mode, int P, int Q, int ldy) {
+  if (dtype == UM_BF16 && ldx % 8 == 0 && ldy % 8 == 0) {
+    const int h = umamd::hwgrad_splits(N, H, W, C, ldx, K, R, stride, pad,
+                                       pad_mode == UM_PAD_REFLECT, P, Q, ldy);
+    if (h > 0) return h;
+  }
+  return generic_wgrad_splits(N * P * Q, K, R * R * C);
+}
+
 int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* x, int K, int R,
                     int stride, int pad, int pad_mode, int P, int Q, const void* dy, int ldy,
                     float* slabs, int splits, hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0 && K % 8 == 0, "um_conv2d_wgrad: C (%d), K (%d) must be multiples of 8", C, K);
   UM_CHECK_ARG(splits >= 1, "um_conv2d_wgrad: splits");
+  UM_CHECK_ARG(splits == um_conv_wgrad_splits(dtype, N, H, W, C, ldx, K, R, stride, pad, pad_mode,
+                                              P, Q, ldy),
+               "um_conv2d_wgrad: splits must come from um_conv_wgrad_splits");
+  if (dtype == UM_BF16 && ldx % 8 == 0 && ldy % 8 == 0 &&
+      umamd::hwgrad_splits(N, H, W, C, ldx, K, R, stride, pad, pad_mode == UM_PAD_REFLECT, P, Q,
+                           ldy) == splits) {
+    if (umamd::hwgrad_run(x, N, H, W, C, ldx, K, R, stride, pad, pad_mode == UM_PAD_REFLECT, P,
+                          Q, dy, ldy, slabs, splits, st) == UM_OK)
+      return UM_OK;
+    umamd::set_error("um_conv2d_wgrad: halo kernel launch failed");
+    return UM_ERR_HIP;
+  }
   WgradArgs a{};
   a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx; a.K = K; a.R = R; a.stride = stride;
   a.pad = pad; a.pad_mode = pad_mode; a.P = P; a.Q = Q; a.ldy = ldy;

@@ -1,0 +1,38 @@
+// Internal interface of the tap-major implicit-GEMM convolution (igemm.hip),
+// used by the C-ABI conv entries in conv.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace umamd {
+
+enum { IG_PAD_ZERO = 0, IG_PAD_REFLECT = 1, IG_FOLD = 2 };
+
+struct IgArgs {
+  // gathered operand ("A"): NHWC image [on][ah][aw][ach], pixel stride lda
+  const void* a;
+  int ah, aw, ach, lda;
+  // output pixels: GEMM row m = (n, oy, ox) over [on][oh][ow]
+  int on, oh, ow;
+  // tap geometry: source row = oy*stride - pad + r (flipped taps for dgrad)
+  int R, stride, pad, pmode, fold_pad, flip;
+  // weights ("B"): row n (output channel) at b + n*ldb, element tap*ach + c
+  const void* b;
+  long ldb;
+  int NC, M;
+  // epilogue
+  const float* bias;
+  void* out;
+  int ld_out, out_f32, epilogue, accumulate;
+  float epi_scale;
+  const void* residual;
+  int ldr;
+  float* stats;
+};
+
+// workspace bytes the split-K heuristic wants for this shape (0: no split)
+long igemm_ws_bytes(int dtype, int M, int NC, int R, int ach);
+// launch; ws may be null (then no split)
+int igemm_run(int dtype, const IgArgs& a, float* ws, long ws_bytes, hipStream_t st);
+
+}  // namespace umamd

@@ -1,0 +1,520 @@
+// Tap-major implicit-GEMM convolution on MFMA (gfx950), forward and
+// stride-1 data gradient.
+//
+//   forward : Y[m=(n,p,q)][k] = sum_{r,s,c} X[n, p*st-pad+r, q*st-pad+s, c] * Wf[k][r][s][c]
+//   dgrad   : DX[m=(n,i,j)][c] = sum_{r',s',k} DY[n, i-p'+r', j-p'+s', k] * WT[c][R-1-r'][R-1-s'][k]
+//             (p' = R-1-pad: the transposed conv is a forward conv over DY
+//             with flipped taps; reflect padding adds the fold sources of
+//             the border pixels, see gather())
+//
+// Reduction order: taps (r, s) outer, channels inner in BK-wide chunks, so a
+// k-step is one tap and one channel chunk and the gather needs no division:
+// the source pixel of a GEMM row moves by (r, s) and the channel by c0.
+// Reference ops: every nn.Conv2d of model/layers/{encoder,decoder,attention}.py
+// and its input gradient.
+//
+// Block: 256 threads = 4 waves, BM x BN output tile, each wave a
+// (BM/WM) x (BN/WN) grid of 16x16 MFMA tiles.  A (pixels x BK) and B
+// (channels x BK) are register-staged into a double-buffered LDS image (one
+// barrier per k-step, next step's global loads in flight during the MFMAs).
+// bf16 images use 16-byte-chunk XOR swizzles that make every 16x16x32
+// fragment read (ds_read_b128) bank-conflict free (checked exhaustively
+// against the gfx950 lane groups).  Blocks are remapped so each XCD walks a
+// contiguous run of tiles (neighbouring pixel tiles share halo rows in L2).
+//
+// Split-K (small-M layers: deep encoder stages have 128-4096 pixels): the
+// k-steps are split over blockIdx.z, partial tiles go to an f32 workspace
+// [split][M][NC] and splitk_epilogue_kernel sums them and applies the
+// epilogue (bias, BN partial statistics, residual, sigmoid-scale).
+#include <algorithm>
+
+#include "common.h"
+#include "igemm.h"
+
+namespace {
+
+using umamd::IgArgs;
+
+constexpr int STATS_ROWS = 128;  // BN partial-statistics row block (um_conv_stats_parts)
+
+// ------------------------------------------------------------ LDS images --
+template <typename T, int BK> struct Img;
+template <> struct Img<bf16_t, 32> {  // 64-B rows; chunk ^ {0,3,2,1}[(row>>2)&3]
+  static constexpr int ROW = 32;
+  __device__ static int off(int row, int c8) {
+    return row * 32 + ((c8 ^ ((4 - ((row >> 2) & 3)) & 3)) << 3);
+  }
+};
+template <> struct Img<bf16_t, 64> {  // 128-B rows; chunk ^ (row & 7)
+  static constexpr int ROW = 64;
+  __device__ static int off(int row, int c8) { return row * 64 + ((c8 ^ (row & 7)) << 3); }
+};
+template <> struct Img<float, 32> {  // 144-B rows (padded)
+  static constexpr int ROW = 36;
+  __device__ static int off(int row, int c8) { return row * 36 + c8 * 8; }
+};
+
+template <typename T> struct Frag;
+template <> struct Frag<bf16_t> { bf16x8_t v; };
+template <> struct Frag<float> { float v[8]; };
+
+__device__ __forceinline__ void lds_frag(const bf16_t* p, Frag<bf16_t>& f) {
+  f.v = *reinterpret_cast<const bf16x8_t*>(p);
+}
+__device__ __forceinline__ void lds_frag(const float* p, Frag<float>& f) {
+  const float4 x = *reinterpret_cast<const float4*>(p);
+  const float4 y = *reinterpret_cast<const float4*>(p + 4);
+  f.v[0] = x.x; f.v[1] = x.y; f.v[2] = x.z; f.v[3] = x.w;
+  f.v[4] = y.x; f.v[5] = y.y; f.v[6] = y.z; f.v[7] = y.w;
+}
+__device__ __forceinline__ void mfma(f32x4_t& acc, const Frag<bf16_t>& x, const Frag<bf16_t>& y) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.v, y.v, acc, 0, 0, 0);
+}
+// f32: 8 x 16x16x4 with lane group g, element e -> k = 8g + e on both operands
+__device__ __forceinline__ void mfma(f32x4_t& acc, const Frag<float>& x, const Frag<float>& y) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.v[e], y.v[e], acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ void add8(const bf16_t* p, float* v) {
+  float t[8];
+  load8(p, t);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] += t[i];
+}
+__device__ __forceinline__ void add8(const float* p, float* v) {
+  float t[8];
+  load8(p, t);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] += t[i];
+}
+__device__ __forceinline__ void to_raw(const float* v, Raw8<bf16_t>& r) {
+  r.v.x = pack_bf16x2(v[0], v[1]);
+  r.v.y = pack_bf16x2(v[2], v[3]);
+  r.v.z = pack_bf16x2(v[4], v[5]);
+  r.v.w = pack_bf16x2(v[6], v[7]);
+}
+__device__ __forceinline__ void to_raw(const float* v, Raw8<float>& r) {
+  r.a = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                   __float_as_uint(v[3]));
+  r.b = make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]),
+                   __float_as_uint(v[7]));
+}
+
+// one A row (GEMM row = output pixel) as seen by the gather
+struct ARow {
+  long base;   // element offset of the image (n) in the source
+  int y0, x0;  // source coords of tap (0,0)
+  bool ok;
+};
+
+__device__ __forceinline__ ARow decode_row(const IgArgs& a, int m) {
+  ARow w;
+  w.ok = m < a.M;
+  const int mm = w.ok ? m : 0;
+  const int hw = a.oh * a.ow;
+  const int n = mm / hw;
+  const int rem = mm - n * hw;
+  const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
+  w.base = (long)n * a.ah * a.aw * a.lda;
+  w.y0 = oy * a.stride - a.pad;
+  w.x0 = ox * a.stride - a.pad;
+  return w;
+}
+
+template <typename T>
+__device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ src, const ARow& w,
+                                       int r, int s, int c, Raw8<T>& out) {
+  raw_zero(out);
+  if (!w.ok || c >= a.ach) return;
+  int yy = w.y0 + r, xx = w.x0 + s;
+  if (a.pmode == umamd::IG_PAD_REFLECT) {
+    yy = reflect_idx(yy, a.ah);
+    xx = reflect_idx(xx, a.aw);
+    raw_load8(src + w.base + ((long)yy * a.aw + xx) * a.lda + c, out);
+    return;
+  }
+  const bool iny = yy >= 0 && yy < a.ah, inx = xx >= 0 && xx < a.aw;
+  if (a.pmode == umamd::IG_PAD_ZERO) {
+    if (iny && inx) raw_load8(src + w.base + ((long)yy * a.aw + xx) * a.lda + c, out);
+    return;
+  }
+  // IG_FOLD (reflect-padded transpose).  The forward read X[refl(o + r - pad)],
+  // so output pixel i also receives from o = -i - p' + r' (1 <= i <= pad) and
+  // o = 2(H-1) - i - p' + r' (H-1-pad <= i <= H-2); here a.pad = p'.
+  const int oy = w.y0 + a.pad, ox = w.x0 + a.pad;
+  const int H = a.oh, W = a.ow, fp = a.fold_pad;
+  const bool lo_y = oy >= 1 && oy <= fp, hi_y = oy >= H - 1 - fp && oy <= H - 2;
+  const bool lo_x = ox >= 1 && ox <= fp, hi_x = ox >= W - 1 - fp && ox <= W - 2;
+  if (!(lo_y || hi_y || lo_x || hi_x)) {
+    if (iny && inx) raw_load8(src + w.base + ((long)yy * a.aw + xx) * a.lda + c, out);
+    return;
+  }
+  int ys[3], xs[3], ny = 0, nx = 0;
+  if (iny) ys[ny++] = yy;
+  if (lo_y) { const int t = -oy - a.pad + r; if (t >= 0 && t < a.ah) ys[ny++] = t; }
+  if (hi_y) { const int t = 2 * (H - 1) - oy - a.pad + r; if (t >= 0 && t < a.ah) ys[ny++] = t; }
+  if (inx) xs[nx++] = xx;
+  if (lo_x) { const int t = -ox - a.pad + s; if (t >= 0 && t < a.aw) xs[nx++] = t; }
+  if (hi_x) { const int t = 2 * (W - 1) - ox - a.pad + s; if (t >= 0 && t < a.aw) xs[nx++] = t; }
+  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int u = 0; u < ny; ++u)
+    for (int q = 0; q < nx; ++q) add8(src + w.base + ((long)ys[u] * a.aw + xs[q]) * a.lda + c, v);
+  to_raw(v, out);
+}
+
+template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT>
+__global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict__ ws,
+                                                     int steps, int steps_per_split, int ntn) {
+  using I = Img<T, BK>;
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  constexpr int CPR = BK / 8;  // 8-element chunks per LDS row
+  constexpr int A_CH = BM * CPR, B_CH = BN * CPR;
+  static_assert(A_CH % 256 == 0, "A chunks per thread");
+  constexpr int A_PER = A_CH / 256;
+  constexpr int B_PER = (B_CH + 255) / 256;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(BM % STATS_ROWS == 0 || STATS_ROWS % BM == 0, "stats rows");
+
+  __shared__ __attribute__((aligned(16))) T sA[2][BM * I::ROW];
+  __shared__ __attribute__((aligned(16))) T sB[2][BN * I::ROW];
+  __shared__ float sStat[WM][BN][2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // XCD-aware tile order: blocks b, b+8, b+16... (one XCD) take consecutive tiles
+  int t = blockIdx.x;
+  {
+    const int nb = gridDim.x;
+    if (nb >= 16) {
+      const int xcd = t & 7, q = nb >> 3, rr = nb & 7;
+      t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
+    }
+  }
+  const int bm = (t / ntn) * BM;
+  const int bn = (t - (t / ntn) * ntn) * BN;
+
+  const T* __restrict__ asrc = reinterpret_cast<const T*>(a.a);
+  const T* __restrict__ bsrc = reinterpret_cast<const T*>(a.b);
+
+  ARow arow[A_PER];
+  int akc[A_PER], arow_i[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int c = tid + i * 256;
+    arow_i[i] = c / CPR;
+    akc[i] = c % CPR;
+    arow[i] = decode_row(a, bm + arow_i[i]);
+  }
+  int brow_i[B_PER], bkc[B_PER];
+  bool bok[B_PER];
+#pragma unroll
+  for (int i = 0; i < B_PER; ++i) {
+    const int c = tid + i * 256;
+    brow_i[i] = c / CPR;
+    bkc[i] = c % CPR;
+    bok[i] = c < B_CH && bn + brow_i[i] < a.NC;
+  }
+
+  const int s_begin = SPLIT ? blockIdx.z * steps_per_split : 0;
+  const int s_end = SPLIT ? min(steps, s_begin + steps_per_split) : steps;
+  const int nchunk = (a.ach + BK - 1) / BK;
+  int tap = s_begin / nchunk;
+  int c0 = (s_begin - tap * nchunk) * BK;
+  int r = tap / a.R, s = tap - (tap / a.R) * a.R;
+
+  Raw8<T> ra[A_PER], rb[B_PER];
+  auto load = [&]() {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) gather(a, asrc, arow[i], r, s, c0 + akc[i] * 8, ra[i]);
+    const int btap = a.flip ? (a.R - 1 - r) * a.R + (a.R - 1 - s) : r * a.R + s;
+    const long boff = (long)btap * a.ach;
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      raw_zero(rb[i]);
+      const int c = c0 + bkc[i] * 8;
+      if (bok[i] && c < a.ach) raw_load8(bsrc + (long)(bn + brow_i[i]) * a.ldb + boff + c, rb[i]);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) raw_store8(&sA[buf][I::off(arow_i[i], akc[i])], ra[i]);
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i)
+      if (tid + i * 256 < B_CH) raw_store8(&sB[buf][I::off(brow_i[i], bkc[i])], rb[i]);
+  };
+  auto advance = [&]() {
+    c0 += BK;
+    if (c0 >= a.ach) {
+      c0 = 0;
+      if (++s == a.R) { s = 0; ++r; }
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fg = lane >> 4;
+  if (s_begin < s_end) {
+    load();
+    store(0);
+    advance();
+  }
+  __syncthreads();
+  for (int st = s_begin; st < s_end; ++st) {
+    const int cur = (st - s_begin) & 1;
+    const bool more = st + 1 < s_end;
+    if (more) load();
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      Frag<T> fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        lds_frag(&sA[cur][I::off(wm * (BM / WM) + i * 16 + frow, kk * 4 + fg)], fa[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        lds_frag(&sB[cur][I::off(wn * (BN / WN) + j * 16 + frow, kk * 4 + fg)], fb[j]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma(acc[i][j], fa[i], fb[j]);
+    }
+    if (more) {
+      store(cur ^ 1);
+      advance();
+    }
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------- epilogue --
+  const int col_l = lane & 15;
+  const int row_g = (lane >> 4) * 4;
+  if (SPLIT) {
+    float* o = ws + (long)blockIdx.z * a.M * a.NC;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = bn + wn * (BN / WN) + j * 16 + col_l;
+      if (n >= a.NC) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
+          if (m < a.M) o[(long)m * a.NC + n] = acc[i][j][q];
+        }
+    }
+    return;
+  }
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = bn + wn * (BN / WN) + j * 16 + col_l;
+    const bool nok = n < a.NC;
+    const float bv = (a.bias != nullptr && nok) ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
+        if (!nok || m >= a.M) continue;
+        float v = acc[i][j][q] + bv;
+        const long off = (long)m * a.ld_out + n;
+        if (a.epilogue == UM_EPI_RESIDUAL)
+          v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
+        if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
+        if (a.out_f32) {
+          float* o = reinterpret_cast<float*>(a.out) + off;
+          if (a.accumulate) v += *o;
+          *o = v;
+        } else {
+          T* o = reinterpret_cast<T*>(a.out) + off;
+          if (a.accumulate) v += to_f32(*o);
+          *o = from_f32<T>(v);
+        }
+        csum[j] += v;
+        csq[j] += v * v;
+      }
+  }
+  if (a.epilogue == UM_EPI_STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float sm = csum[j], sq = csq[j];
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      sq += __shfl_xor(sq, 16, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      if (lane < 16) {
+        sStat[wm][wn * (BN / WN) + j * 16 + lane][0] = sm;
+        sStat[wm][wn * (BN / WN) + j * 16 + lane][1] = sq;
+      }
+    }
+    __syncthreads();
+    // stats row blocks of STATS_ROWS rows: waves of rows [w*BM/WM, (w+1)*BM/WM)
+    constexpr int WROWS = BM / WM;
+    constexpr int NSB = BM >= STATS_ROWS ? BM / STATS_ROWS : 1;
+    for (int c = tid; c < BN * NSB; c += 256) {
+      const int col = c % BN, sb = c / BN;
+      const int n = bn + col;
+      if (n >= a.NC || bm + sb * STATS_ROWS >= a.M) continue;
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w)
+        if ((w * WROWS) / STATS_ROWS == sb) { sm += sStat[w][col][0]; sq += sStat[w][col][1]; }
+      float* o = a.stats + ((long)(bm / STATS_ROWS + sb) * a.NC + n) * 2;
+      o[0] = sm;
+      o[1] = sq;
+    }
+  }
+}
+
+// sum the split-K partials and apply the epilogue.  Block = STATS_ROWS rows x
+// 64 columns: thread (g, lane) owns columns 4g..4g+3 and rows lane, lane+16, ...
+constexpr int EPI_COLS = 64;
+template <typename T>
+__global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const float* __restrict__ ws,
+                                                               int splits) {
+  __shared__ float red[16][16][8];
+  const int g = threadIdx.x & 15, lane = threadIdx.x >> 4;
+  const int n = blockIdx.y * EPI_COLS + g * 4;  // NC % 4 == 0 (host-checked)
+  const long m0 = (long)blockIdx.x * STATS_ROWS;
+  const long m1 = min((long)a.M, m0 + STATS_ROWS);
+  const long zs = (long)a.M * a.NC;
+  const bool act = n < a.NC;
+  float sm[4] = {0, 0, 0, 0}, sq[4] = {0, 0, 0, 0};
+  if (act) {
+    float bv[4] = {0, 0, 0, 0};
+    if (a.bias)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = a.bias[n + e];
+    for (long m = m0 + lane; m < m1; m += 16) {
+      const float* p = ws + m * a.NC + n;
+      float4 x = *reinterpret_cast<const float4*>(p);
+      int z = 1;
+      for (; z + 1 < splits; z += 2) {  // two partials in flight
+        const float4 y0 = *reinterpret_cast<const float4*>(p + z * zs);
+        const float4 y1 = *reinterpret_cast<const float4*>(p + (z + 1) * zs);
+        x.x += y0.x + y1.x; x.y += y0.y + y1.y; x.z += y0.z + y1.z; x.w += y0.w + y1.w;
+      }
+      if (z < splits) {
+        const float4 y0 = *reinterpret_cast<const float4*>(p + z * zs);
+        x.x += y0.x; x.y += y0.y; x.z += y0.z; x.w += y0.w;
+      }
+      float v[4] = {x.x + bv[0], x.y + bv[1], x.z + bv[2], x.w + bv[3]};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (a.epilogue == UM_EPI_RESIDUAL)
+          v[e] += to_f32(reinterpret_cast<const T*>(a.residual)[m * a.ldr + n + e]);
+        if (a.epilogue == UM_EPI_SIGMOID_SCALE) v[e] = a.epi_scale * sigmoidf_(v[e]);
+        const long off = m * a.ld_out + n + e;
+        if (a.out_f32) {
+          float* o = reinterpret_cast<float*>(a.out) + off;
+          if (a.accumulate) v[e] += *o;
+          *o = v[e];
+        } else {
+          T* o = reinterpret_cast<T*>(a.out) + off;
+          if (a.accumulate) v[e] += to_f32(*o);
+          *o = from_f32<T>(v[e]);
+        }
+        sm[e] += v[e];
+        sq[e] += v[e] * v[e];
+      }
+    }
+  }
+  if (a.epilogue != UM_EPI_STATS) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { red[lane][g][e] = sm[e]; red[lane][g][4 + e] = sq[e]; }
+  __syncthreads();
+  if (lane == 0 && act) {
+    for (int l = 1; l < 16; ++l)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { sm[e] += red[l][g][e]; sq[e] += red[l][g][4 + e]; }
+    float* o = a.stats + ((long)blockIdx.x * a.NC + n) * 2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { o[2 * e] = sm[e]; o[2 * e + 1] = sq[e]; }
+  }
+}
+
+struct Plan {
+  int bk, bm, bn, wm, wn, splits, steps, per;
+};
+
+Plan make_plan(int dtype, int M, int NC, int R, int ach, long ws_bytes) {
+  Plan p{};
+  p.bk = 32;
+  if (NC <= 16) { p.bm = 256; p.bn = 16; p.wm = 4; p.wn = 1; }
+  else if (NC <= 32) { p.bm = 256; p.bn = 32; p.wm = 4; p.wn = 1; }
+  else if (NC <= 64) { p.bm = 256; p.bn = 64; p.wm = 4; p.wn = 1; }
+  else {
+    p.bm = 128; p.bn = 128; p.wm = 2; p.wn = 2;
+    if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;  // 64 KB of LDS: 2 blocks/CU
+  }
+  p.steps = R * R * ((ach + p.bk - 1) / p.bk);
+  // Split only grids that leave most CUs idle: the partials cost an f32
+  // write + read of splits*M*NC (about 1 us per 8 MB each way), so aim at
+  // ~320 blocks, >= 8 k-steps per split and <= 32 MB of partials.
+  const long tiles = (long)ceil_div(M, p.bm) * ceil_div(NC, p.bn);
+  p.splits = 1;
+  if (tiles < 160 && NC % 4 == 0) {
+    long sp = (320 + tiles - 1) / tiles;
+    sp = std::min<long>(sp, p.steps / 8);
+    sp = std::min<long>(sp, (32l << 20) / ((long)M * NC * 4));
+    if (ws_bytes >= 0) sp = std::min<long>(sp, ws_bytes / ((long)M * NC * 4));
+    if (sp >= 2) p.splits = (int)sp;
+  }
+  p.per = ceil_div(p.steps, p.splits);
+  p.splits = ceil_div(p.steps, p.per);  // no empty splits
+  return p;
+}
+
+template <typename T, int BK, int BM, int BN, int WM, int WN>
+int launch(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
+  const int ntm = ceil_div(a.M, BM), ntn = ceil_div(a.NC, BN);
+  if (p.splits > 1) {
+    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, true>), dim3(ntm * ntn, 1, p.splits),
+                       dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
+    hipLaunchKernelGGL(splitk_epilogue_kernel<T>,
+                       dim3(ceil_div(a.M, STATS_ROWS), ceil_div(a.NC, EPI_COLS)), dim3(256), 0, st,
+                       a, (const float*)ws, p.splits);
+  } else {
+    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, false>), dim3(ntm * ntn, 1, 1),
+                       dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
+  }
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+template <typename T>
+int dispatch_tiles(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
+  if (p.bn == 16) return launch<T, 32, 256, 16, 4, 1>(a, p, ws, st);
+  if (p.bn == 32) return launch<T, 32, 256, 32, 4, 1>(a, p, ws, st);
+  if (p.bn == 64) return launch<T, 32, 256, 64, 4, 1>(a, p, ws, st);
+  if constexpr (sizeof(T) == 2)
+    if (p.bk == 64) return launch<T, 64, 128, 128, 2, 2>(a, p, ws, st);
+  return launch<T, 32, 128, 128, 2, 2>(a, p, ws, st);
+}
+
+}  // namespace
+
+namespace umamd {
+
+long igemm_ws_bytes(int dtype, int M, int NC, int R, int ach) {
+  const Plan p = make_plan(dtype, M, NC, R, ach, -1);
+  return p.splits > 1 ? (long)p.splits * M * NC * 4 : 0;
+}
+
+int igemm_run(int dtype, const IgArgs& a, float* ws, long ws_bytes, hipStream_t st) {
+  if (a.M == 0) return UM_OK;
+  const Plan p = make_plan(dtype, a.M, a.NC, a.R, a.ach, ws ? ws_bytes : 0);
+  if (dtype == UM_BF16) return dispatch_tiles<bf16_t>(a, p, ws, st);
+  return dispatch_tiles<float>(a, p, ws, st);
+}
+
+}  // namespace umamd

@@ -37,10 +37,12 @@ _SIG = {
     'um_version': (_I, []),
     'um_conv_stats_parts': (_I, [_I, _I]),
     'um_conv2d_fwd': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I,
-                           _I, _P, _I, _I, _F, _P, _I, _P, 's']),
+                           _I, _P, _I, _I, _F, _P, _I, _P, _P, _L, 's']),
     'um_conv2d_dgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
-                             _P, _I, 's']),
-    'um_conv_wgrad_splits': (_I, [_I, _I, _I]),
+                             _P, _I, _P, _L, 's']),
+    'um_conv_fwd_ws': (_L, [_I, _I, _I, _I, _I, _I, _I]),
+    'um_conv_dgrad_ws': (_L, [_I, _I, _I, _I, _I, _I, _I, _I]),
+    'um_conv_wgrad_splits': (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     'um_conv2d_wgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I,
                              _P, _I, 's']),
     'um_conv_wgrad_reduce': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, 's']),

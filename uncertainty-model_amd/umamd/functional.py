@@ -81,10 +81,12 @@ def _conv_fwd(x, wf, bias, K, R, stride, pad, pad_mode, out_dtype=None, epi=L.EP
     if out is None:
         ldo = ldo or K
         out = torch.empty((N, P, Q, ldo), dtype=od, device=x.device)
+    wsb = query('um_conv_fwd_ws', _dt(x), N, P, Q, K, R, C)
+    ws = torch.empty((wsb // 4,), dtype=torch.float32, device=x.device) if wsb else None
     call('um_conv2d_fwd', _dt(x), N, H, W, C, C, ptr(x), ptr(wf), ptr(bias), K, R, stride, pad,
          pad_mode, P, Q, L.dtype_code(od), ptr(out), out.shape[-1], epi, float(epi_scale),
          ptr(residual), residual.shape[-1] if residual is not None else 0, ptr(stats),
-         work=_conv_flops(N, P, Q, K, R, creal or C))
+         ptr(ws), wsb, work=_conv_flops(N, P, Q, K, R, creal or C))
     return out
 
 
@@ -94,8 +96,10 @@ def _conv_dgrad(dy, wT, x_shape, K, R, stride, pad, pad_mode, dx=None, accumulat
     _, P, Q, ldy = dy.shape
     if dx is None:
         dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    wsb = query('um_conv_dgrad_ws', _dt(dy), N, H, W, C, R, K, stride)
+    ws = torch.empty((wsb // 4,), dtype=torch.float32, device=dy.device) if wsb else None
     call('um_conv2d_dgrad', _dt(dy), N, H, W, C, C, ptr(dx), int(accumulate), ptr(wT), K, R,
-         stride, pad, pad_mode, P, Q, ptr(dy), ldy,
+         stride, pad, pad_mode, P, Q, ptr(dy), ldy, ptr(ws), wsb,
          work=_conv_flops(N, P, Q, kreal or K, R, creal or C))
     return dx
 
@@ -106,7 +110,8 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
     _, P, Q, ldy = dy.shape
     M = N * P * Q
     RRC = R * R * C
-    splits = query('um_conv_wgrad_splits', M, K, RRC)
+    splits = query('um_conv_wgrad_splits', _dt(x), N, H, W, C, C, K, R, stride, pad, pad_mode,
+                   P, Q, ldy)
     slabs = torch.empty((splits, K, RRC), dtype=torch.float32, device=x.device)
     call('um_conv2d_wgrad', _dt(x), N, H, W, C, C, ptr(x), K, R, stride, pad, pad_mode, P, Q,
          ptr(dy), ldy, ptr(slabs), splits, work=_conv_flops(N, P, Q, Kreal, R, Creal))
