@@ -330,3 +330,30 @@ def test_wgrad(case):
     err = _rel(got, ref)
     print(f'wgrad {case}: splits {splits} rel {err:.3e}')
     assert err < 1e-4, err
+
+
+# x2 bilinear (align_corners=True) upsample of a concat source: forward and
+# the adjoint (branch-free 6x6 window for low-res sides >= 4, general path
+# below), with and without an SE gate, against torch
+@pytest.mark.parametrize('h,w', [(4, 5), (5, 7), (8, 33), (2, 3), (16, 16)])
+@pytest.mark.parametrize('gated', [False, True])
+def test_up2_concat_adjoint(h, w, gated):
+    from umamd import functional as U
+    from umamd._lib import CAT_UP2
+    N, C = 2, 16
+    x = torch.randn(N, C, h, w, dtype=torch.float64)
+    gate = torch.rand(N, C, dtype=torch.float64) if gated else None
+    xr = x.clone().requires_grad_(True)
+    gr = gate.clone().requires_grad_(True) if gated else None
+    src = xr * gr[:, :, None, None] if gated else xr
+    yr = F.interpolate(src, scale_factor=2, mode='bilinear', align_corners=True)
+    go = torch.randn_like(yr)
+    (yr * go).sum().backward()
+    xd = _nhwc(x.float()).requires_grad_(True)
+    gd = gate.float().to(DEV).requires_grad_(True) if gated else None
+    y, _ = U.concat([U.CatSource(xd, CAT_UP2, C, gd)], N, 2 * h, 2 * w, torch.float32)
+    (y.float() * _nhwc(go.float())).sum().backward()
+    assert _rel(_nchw(y), yr) < 1e-5
+    assert _rel(_nchw(xd.grad), xr.grad) < 1e-5
+    if gated:
+        assert _rel(gd.grad, gr.grad) < 1e-5

@@ -56,20 +56,6 @@ __device__ __forceinline__ float sample(const float* p, const Samp& t, int H, in
   return nw * (t.s * t.e) + ne * (t.s * t.w) + sw * (t.n * t.e) + se * (t.n * t.w);
 }
 
-// scatter g * weight into plane taps (atomic)
-__device__ __forceinline__ void scatter(float* p, const Samp& t, int H, int W, long st, float g) {
-  const int xs[2] = {t.x0, t.x0 + 1}, ys[2] = {t.y0, t.y0 + 1};
-  const float wx[2] = {t.e, t.w}, wy[2] = {t.s, t.n};
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int y = ys[a], x = xs[b];
-      if (x >= 0 && x < W && y >= 0 && y < H)
-        atomicAdd(&p[((long)y * W + x) * st], g * wy[a] * wx[b]);
-    }
-}
-
 __device__ __forceinline__ void up_index(int i, int in, int out, int& i0, int& i1, float& l1) {
   const float sc = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
   const float src = sc * (float)i;
@@ -307,7 +293,7 @@ __global__ void finalize_kernel(FinalP f, float* __restrict__ out) {
 // ---------------------------------------------------------------- backward --
 struct BwdP {
   LossP l;
-  float* dpred;  // [N][H][W][pld] f32, zeroed, accumulated atomically
+  float* dpred;  // [N][H][W][pld] f32: own terms stored, then the scatter pass adds
   const float* gout;  // [2]: d total / d disp_loss, d / d error_loss (device scalars)
   float w_wssim, w_cons, w_smooth, w_err;
   float smooth_div;  // 2^scale
@@ -421,7 +407,6 @@ __global__ void __launch_bounds__(256) loss_bwd_kernel(BwdP b) {
     }
   }
   // ---- disparity consistency (loss.py:154-188), d_v vs warp(d_opp, sign*d_v)
-  float* dopp = dp + (1 - v);
   {
     const float kc = (float)(gd * b.w_cons / npix);
     const float dv = p[v];
@@ -429,8 +414,7 @@ __global__ void __launch_bounds__(256) loss_bwd_kernel(BwdP b) {
     float dix;
     const float wv = sample(pp + (1 - v), t, H, W, pld, &dix);
     const float s = sgnf(dv - wv) * kc;
-    gdv += s * (1.f - dix * sign * (float)W);
-    if (s != 0.f) scatter(dopp, t, H, W, pld, -s);
+    gdv += s * (1.f - dix * sign * (float)W);  // the d_opp part: loss_scatter_kernel
   }
   // ---- error consistency: sigma_v vs warp(d_opp, sign*sigma_v) (F5)
   if (a.ecw != 0.f) {
@@ -441,23 +425,20 @@ __global__ void __launch_bounds__(256) loss_bwd_kernel(BwdP b) {
     const float wv = sample(pp + (1 - v), t, H, W, pld, &dix);
     const float s = sgnf(sv - wv) * kc;
     gsv += s * (1.f - dix * sign * (float)W);
-    if (s != 0.f) scatter(dopp, t, H, W, pld, -s);
   }
   // ---- smoothness (loss.py:191-264) of d_v (and sigma_v if weighted)
   {
-    auto wgt = [&](int yy, int xx, int dy, int dx) {
+    // edge weights from the staged image tile (tile index = pixel + 2)
+    auto wgt = [&](int ry, int rx, int dy, int dx) {
       float g = 0.f;
-      for (int c = 0; c < 3; ++c) {
-        const float* pl = a.img + ((long)n * 6 + v * 3 + c) * H * W;
-        g += fabsf(pl[(long)yy * W + xx] - pl[(long)(yy + dy) * W + xx + dx]);
-      }
+      for (int c = 0; c < 3; ++c) g += fabsf(sI[c][ry][rx] - sI[c][ry + dy][rx + dx]);
       return __expf(-g / 3.f);
     };
     float wxs[2] = {0.f, 0.f}, wys[2] = {0.f, 0.f};  // at q and q-1 (x), q and q-w (y)
-    if (x < W - 1) wxs[0] = wgt(y, x, 0, 1);
-    if (x > 0) wxs[1] = wgt(y, x - 1, 0, 1);
-    if (y < H - 1) wys[0] = wgt(y, x, 1, 0);
-    if (y > 0) wys[1] = wgt(y - 1, x, 1, 0);
+    if (x < W - 1) wxs[0] = wgt(ly + 2, lx + 2, 0, 1);
+    if (x > 0) wxs[1] = wgt(ly + 2, lx + 1, 0, 1);
+    if (y < H - 1) wys[0] = wgt(ly + 2, lx + 2, 1, 0);
+    if (y > 0) wys[1] = wgt(ly + 1, lx + 2, 1, 0);
     for (int k = 0; k < 2; ++k) {
       const int ch = v + 2 * k;
       float kc;
@@ -486,8 +467,73 @@ __global__ void __launch_bounds__(256) loss_bwd_kernel(BwdP b) {
     else g = sgnf(sg - ev);
     gsv += kn * g;
   }
-  atomicAdd(&dp[((long)y * W + x) * pld + v], gdv);
-  atomicAdd(&dp[((long)y * W + x) * pld + 2 + v], gsv);
+  dp[((long)y * W + x) * pld + v] = gdv;
+  dp[((long)y * W + x) * pld + 2 + v] = gsv;
+}
+
+// Consistency terms' gradient w.r.t. the OPPOSITE disparity (the warped
+// operand): a data-dependent scatter.  The warp moves rows by < 1 (sample
+// y = y*H/(H-1) - 0.5), so a strip of RS rows scatters into rows y0-1 ..
+// y0+RS only: accumulate them in LDS (ds_add_f32), then add rows no other
+// strip reaches with plain read-modify-writes and the 4 shared border rows
+// with global atomics.  Runs after loss_bwd_kernel (which stored the own terms).
+constexpr int RS = 8;
+__global__ void __launch_bounds__(256) loss_scatter_kernel(BwdP b) {
+  extern __shared__ float acc[];  // [2 channels][RS + 2][W]
+  const LossP& a = b.l;
+  const int H = a.H, W = a.W, pld = a.pld;
+  const int n = blockIdx.y;
+  const int y0 = blockIdx.x * RS;
+  const int nrow = RS + 2;
+  for (int i = threadIdx.x; i < 2 * nrow * W; i += 256) acc[i] = 0.f;
+  __syncthreads();
+  const float gd = b.gout[0], ge = b.gout[1];
+  const double npix = (double)a.N * H * W;
+  const float kcd = (float)(gd * b.w_cons / npix);
+  const float kce = (float)(ge * b.w_err * a.ecw / npix);
+  const float* pp = a.pred + (long)n * H * W * pld;
+  const int rows = min(RS, H - y0);
+  for (int i = threadIdx.x; i < 2 * rows * W; i += 256) {
+    const int v = i / (rows * W);
+    const int r = i - v * rows * W;
+    const int y = y0 + r / W, x = r % W;
+    const float sign = v == 0 ? -1.f : 1.f;
+    const float* p = pp + ((long)y * W + x) * pld;
+    float* buf = acc + (1 - v) * nrow * W;
+    for (int k = 0; k < 2; ++k) {
+      float kc, val;
+      if (k == 0) { kc = kcd; val = p[v]; }
+      else { if (a.ecw == 0.f) break; kc = kce; val = p[2 + v]; }
+      const Samp t = warp_at(x, y, sign * val, W, H);
+      const float wv = sample(pp + (1 - v), t, H, W, pld, nullptr);
+      const float g = -sgnf(val - wv) * kc;
+      if (g == 0.f) continue;
+      const int xs[2] = {t.x0, t.x0 + 1}, ys[2] = {t.y0, t.y0 + 1};
+      const float wx[2] = {t.e, t.w}, wy[2] = {t.s, t.n};
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int yy = ys[u], xx = xs[q];
+          if (xx >= 0 && xx < W && yy >= 0 && yy < H)
+            atomicAdd(&buf[(yy - (y0 - 1)) * W + xx], g * wy[u] * wx[q]);
+        }
+    }
+  }
+  __syncthreads();
+  float* dp = b.dpred + (long)n * H * W * pld;
+  for (int i = threadIdx.x; i < 2 * nrow * W; i += 256) {
+    const int ch = i / (nrow * W);
+    const int r = (i / W) % nrow;
+    const int x = i % W;
+    const int yy = y0 - 1 + r;
+    if (yy < 0 || yy >= H) continue;
+    const float v = acc[i];
+    if (v == 0.f) continue;
+    float* o = dp + ((long)yy * W + x) * pld + ch;
+    if (r >= 2 && r <= RS - 1) *o += v;  // rows y0+1 .. y0+RS-2: this strip only
+    else atomicAdd(o, v);
+  }
 }
 
 inline int grid_for(long n) {
@@ -563,6 +609,15 @@ int um_loss_bwd_scale(const float* img, const float* rec, const float* pred, int
   b.smooth_div = smooth_div;
   dim3 grid(ceil_div(W, TB), ceil_div(H, TB), N * 2);
   hipLaunchKernelGGL(loss_bwd_kernel, grid, dim3(256), 0, st, b);
+  const size_t lds = (size_t)2 * (RS + 2) * W * sizeof(float);
+  UM_CHECK_ARG(lds <= 150 * 1024, "um_loss_bwd_scale: width %d too large", W);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&loss_scatter_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(loss_scatter_kernel, dim3(ceil_div(H, RS), N), dim3(256), lds, st, b);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -149,7 +149,9 @@ class TukraLossFn(torch.autograd.Function):
         grads = []
         for i in range(n):
             N, H, W, pld = preds[i].shape
-            dp = torch.zeros((N, H, W, pld), dtype=torch.float32, device=dev)
+            # the kernel stores channels 0-3 of every pixel; only padding needs zeros
+            dp = (torch.empty if pld == 4 else torch.zeros)((N, H, W, pld), dtype=torch.float32,
+                                                             device=dev)
             call('um_loss_bwd_scale', ptr(pyr[i]), ptr(rec[i]), ptr(preds[i]), pld, N, H, W,
                  cfg['alpha'], cfg['loss_type'], cfg['esw'], cfg['ecw'], ptr(emaps[i]),
                  ptr(gout), cfg['w_wssim'], cfg['w_cons'], cfg['w_smooth'], cfg['w_err'],
