@@ -119,14 +119,42 @@ __global__ void ctx_kernel(const T* __restrict__ qkv, int ld, int S, int C, int 
 }
 
 // out[n][j] = sum_b parts[n][b][j]
-__global__ void sum_parts_kernel(const float* __restrict__ parts, int N, int B, int L,
-                                 float* __restrict__ out) {
-  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (i >= (long)N * L) return;
-  const int n = i / L, j = i % L;
-  float t = 0.f;
-  for (int b = 0; b < B; ++b) t += parts[((long)n * B + b) * L + j];
-  out[i] = t;
+// out[n][j] = sum_b parts[n][b][j]: block = (jl columns) x (256/jl b-lanes),
+// 4 accumulators per thread, lanes combined in LDS; grid (ceil(L/jl), N)
+__global__ void __launch_bounds__(256) sum_parts_kernel(const float* __restrict__ parts, int N,
+                                                        int B, int L, float* __restrict__ out,
+                                                        int jl) {
+  __shared__ float red[256];
+  const int lanes = 256 / jl;
+  const int n = blockIdx.y;
+  const int j = blockIdx.x * jl + (threadIdx.x % jl);
+  const int lane = threadIdx.x / jl;
+  float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+  if (j < L) {
+    const float* p = parts + (long)n * B * L + j;
+    int b = lane;
+    for (; b + 3 * lanes < B; b += 4 * lanes) {
+      t0 += p[(long)b * L];
+      t1 += p[(long)(b + lanes) * L];
+      t2 += p[(long)(b + 2 * lanes) * L];
+      t3 += p[(long)(b + 3 * lanes) * L];
+    }
+    for (; b < B; b += lanes) t0 += p[(long)b * L];
+  }
+  float t = (t0 + t1) + (t2 + t3);
+  red[threadIdx.x] = t;
+  __syncthreads();
+  if (lane == 0 && j < L) {
+    for (int q = 1; q < lanes; ++q) t += red[q * jl + (threadIdx.x % jl)];
+    out[(long)n * L + j] = t;
+  }
+}
+
+inline int sum_parts_cols(int L, int B) {  // columns per block: leave >= 8 b-lanes
+  int jl = 64;
+  while (jl > 1 && 256 / jl < 8) jl >>= 1;
+  while (jl > 1 && (256 / jl) * 4 < B && jl > 16) jl >>= 1;
+  return jl;
 }
 
 // ----------------------------------------------------------------- apply --
@@ -356,8 +384,11 @@ int um_attn_fwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
     hipLaunchKernelGGL(ctx_kernel<float>, dim3(nctx, heads, N), dim3(256), shm_ctx, st,
                        (const float*)qkv, ld, S, C, heads, kmax, ksum, cch, nctx, ws);
   const int L = heads * d * d;
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div((long)N * L, 256)), dim3(256), 0, st, ws, N,
-                     nctx, L, ctx);
+  {
+    const int jl = sum_parts_cols(L, nctx);
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div(L, jl), N), dim3(256), 0, st, ws, N, nctx,
+                       L, ctx, jl);
+  }
   const size_t shm_ap = ((size_t)d * d + PT * d) * sizeof(float);
   const dim3 g(ceil_div(S, PT), heads, N);
   if (dtype == UM_BF16)
@@ -388,8 +419,11 @@ int um_attn_bwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
     hipLaunchKernelGGL(apply_bwd_kernel<float>, g, dim3(256), shm_a, st, (const float*)qkv, ld, S,
                        C, heads, ctx, (const float*)datt, ldd, (float*)dqkv, ldq, nt, ws);
   const int L = heads * d * d;
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div((long)N * L, 256)), dim3(256), 0, st, ws, N,
-                     nt, L, dctx);
+  {
+    const int jl = sum_parts_cols(L, nt);
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div(L, jl), N), dim3(256), 0, st, ws, N, nt, L,
+                       dctx, jl);
+  }
   const size_t shm_k = ((size_t)d * d + 3 * PT * d) * sizeof(float);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(kv_bwd_kernel<bf16_t>, g, dim3(256), shm_k, st, (const bf16_t*)qkv, ld, S,
@@ -397,8 +431,11 @@ int um_attn_bwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
   else
     hipLaunchKernelGGL(kv_bwd_kernel<float>, g, dim3(256), shm_k, st, (const float*)qkv, ld, S, C,
                        heads, kmax, ksum, dctx, (float*)dqkv, ldq, dks_ws, nt, ws);
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div((long)N * C, 256)), dim3(256), 0, st, ws, N,
-                     nt, C, r);
+  {
+    const int jl = sum_parts_cols(C, nt);
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div(C, jl), N), dim3(256), 0, st, ws, N, nt, C,
+                       r, jl);
+  }
   const long M = (long)N * S;
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(k_bwd_kernel<bf16_t>, dim3(grid_for(M * C)), dim3(256), 0, st,

@@ -239,8 +239,6 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
   }
 }
 
-constexpr int BWD_ROWS = 256;
-
 inline int grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -284,7 +282,7 @@ int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float*
   return UM_OK;
 }
 
-int um_bn_bwd_parts(long M) { return (int)((M + BWD_ROWS - 1) / BWD_ROWS); }
+int um_bn_bwd_parts(long M) { return parts_for(M); }
 
 int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int ldda,
                          const void* y, int ldy, const float* mean, const float* invstd,
@@ -297,11 +295,11 @@ int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int 
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
                        (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, BWD_ROWS);
+                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M));
   else
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), shm, st,
                        (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, BWD_ROWS);
+                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M));
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -327,12 +325,12 @@ int um_bn_elu_bwd_apply(int dtype, long M, int C, long HW, const void* da, int l
     hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
                        (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
                        scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy, sum_parts,
-                       BWD_ROWS);
+                       rows_per_part(M));
   else
     hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, dim3(blocks), dim3(256), shm, st,
                        (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
                        scale, shift, add_nc, apply_elu, k1, k2, k3, (float*)dy, lddy, sum_parts,
-                       BWD_ROWS);
+                       rows_per_part(M));
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -660,31 +660,50 @@ int launch_wgrad_bf16(const WgradArgs& a, int splits, hipStream_t st) {
   return UM_OK;
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int splits, int K, int Kreal,
-                                    int R, int C, int Creal, float* __restrict__ dw,
-                                    int accumulate, Segs sg) {
-  // slab index i = (k, r, s, c) [K][R][R][C] -> dw[k][c][r][s]; reads coalesced
+// slab index i = (k, r, s, c) [K][R][R][C] -> dw[k][c][r][s].  Block = EB
+// elements x L split lanes (L * EB = 256); a thread sums splits lane,
+// lane + L, ... (4 accumulators), the L partial sums meet in LDS.  Reads are
+// coalesced along the elements.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slabs,
+                                                           int splits, int K, int Kreal, int R,
+                                                           int C, int Creal, float* __restrict__ dw,
+                                                           int accumulate, Segs sg, int L) {
+  __shared__ float red[256];
+  const int EB = 256 / L;
+  const int le = threadIdx.x % EB, lane = threadIdx.x / EB;
   const long RRC = (long)R * R * C;
   const long total = (long)Kreal * RRC;
   const long zs = (long)K * RRC;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const int c = seg_src(sg, (int)(i % C));
-    if (c < 0) continue;
-    const int rs = (i / C) % (R * R);
-    const int k = i / RRC;
+  for (long i0 = (long)blockIdx.x * EB; i0 < total; i0 += (long)gridDim.x * EB) {
+    const long i = i0 + le;
     float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
-    int z = 0;
-    for (; z + 3 < splits; z += 4) {
-      v0 += slabs[z * zs + i];
-      v1 += slabs[(z + 1) * zs + i];
-      v2 += slabs[(z + 2) * zs + i];
-      v3 += slabs[(z + 3) * zs + i];
+    if (i < total) {
+      int z = lane;
+      for (; z + 3 * L < splits; z += 4 * L) {
+        v0 += slabs[z * zs + i];
+        v1 += slabs[(z + L) * zs + i];
+        v2 += slabs[(z + 2 * L) * zs + i];
+        v3 += slabs[(z + 3 * L) * zs + i];
+      }
+      for (; z < splits; z += L) v0 += slabs[z * zs + i];
     }
-    for (; z < splits; ++z) v0 += slabs[z * zs + i];
-    const float v = (v0 + v1) + (v2 + v3);
-    const long o = ((long)k * Creal + c) * R * R + rs;
-    dw[o] = accumulate ? dw[o] + v : v;
+    float v = (v0 + v1) + (v2 + v3);
+    if (L > 1) {
+      red[threadIdx.x] = v;
+      __syncthreads();
+      if (lane == 0)
+        for (int q = 1; q < L; ++q) v += red[q * EB + le];
+      __syncthreads();
+    }
+    if (lane == 0 && i < total) {
+      const int c = seg_src(sg, (int)(i % C));
+      if (c >= 0) {
+        const int rs = (i / C) % (R * R);
+        const int k = i / RRC;
+        const long o = ((long)k * Creal + c) * R * R + rs;
+        dw[o] = accumulate ? dw[o] + v : v;
+      }
+    }
   }
 }
 
@@ -731,39 +750,35 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ y, in
   }
 }
 
-// out[c] (+)= sum_r p[r*stride + c]: block = cl channel lanes x (256/cl) row
-// lanes, 4 independent accumulators per thread (latency hiding), f32 -> f64 at
-// the lane combine
+// out[c] (+)= sum_r p[r*stride + c]: block = cl channel lanes (cl = C up to
+// 64, power of two) x 256/cl row lanes, 8 independent accumulators per
+// thread, f64 lane combine
 __global__ void __launch_bounds__(256) reduce_rows_kernel(const float* __restrict__ p, int parts,
                                                           int C, int stride,
                                                           float* __restrict__ out,
-                                                          int accumulate) {
+                                                          int accumulate, int cl) {
   __shared__ double red[256];
-  const int cl = C < 64 ? C : 64;
   const int lanes = 256 / cl;
   const int c = blockIdx.x * cl + (threadIdx.x % cl);
   const int lane = threadIdx.x / cl;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (lane < lanes && c < C) {
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c < C) {
     int r = lane;
-    for (; r + 3 * lanes < parts; r += 4 * lanes) {
-      s0 += p[(long)r * stride + c];
-      s1 += p[(long)(r + lanes) * stride + c];
-      s2 += p[(long)(r + 2 * lanes) * stride + c];
-      s3 += p[(long)(r + 3 * lanes) * stride + c];
-    }
-    for (; r < parts; r += lanes) s0 += p[(long)r * stride + c];
+    for (; r + 7 * lanes < parts; r += 8 * lanes)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += p[(long)(r + u * lanes) * stride + c];
+    for (int u = 0; r < parts; r += lanes, ++u) s[u & 7] += p[(long)r * stride + c];
   }
-  double s = (double)s0 + (double)s1 + (double)s2 + (double)s3;
-  red[threadIdx.x] = s;
+  double t = 0.0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) t += (double)s[u];
+  red[threadIdx.x] = t;
   __syncthreads();
   if (lane == 0 && c < C) {
-    for (int q = 1; q < lanes; ++q) s += red[q * cl + (threadIdx.x % cl)];
-    out[c] = accumulate ? out[c] + (float)s : (float)s;
+    for (int q = 1; q < lanes; ++q) t += red[q * cl + (threadIdx.x % cl)];
+    out[c] = accumulate ? out[c] + (float)t : (float)t;
   }
 }
-
-constexpr int COLSUM_ROWS = 256;
 
 }  // namespace
 
@@ -924,9 +939,14 @@ int um_conv_wgrad_reduce_seg(const float* slabs, int splits, int K, int Kreal, i
   Segs g{};
   UM_CHECK_ARG(make_segs(g, nseg, src0, dst0, len, Creal, C), "um_conv_wgrad_reduce: segments");
   const long total = (long)Kreal * R * R * C;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  // split lanes: enough that ~2048 blocks x EB elements cover the slab, and
+  // <= splits / 4 so each lane still sums >= 4 partials
+  int L = 1;
+  while (L < 32 && L * 4 <= splits && (total * L) / 256 < 2048) L <<= 1;
+  const int EB = 256 / L;
+  const int blocks = (int)std::min<long>((total + EB - 1) / EB, 8192);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slabs, splits, K, Kreal,
-                     R, C, Creal, dw, accumulate, g);
+                     R, C, Creal, dw, accumulate, g, L);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -961,26 +981,29 @@ int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C, vo
                             st);
 }
 
-int um_colsum_parts(int M) { return ceil_div(M, COLSUM_ROWS); }
+int um_colsum_parts(int M) { return parts_for(M); }
 
 int um_colsum(int dtype, int M, int C, int ld, const void* y, float* parts, hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0 && ld % 8 == 0, "um_colsum: C/ld %% 8");
-  const int blocks = ceil_div(M, COLSUM_ROWS);
-  if (blocks == 0) return UM_OK;
+  const int blocks = parts_for(M);
+  const int rows = rows_per_part(M);
+  if (M == 0) return UM_OK;
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)y, M,
-                       C, ld, parts, COLSUM_ROWS);
+                       C, ld, parts, rows);
   else
     hipLaunchKernelGGL(colsum_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)y, M,
-                       C, ld, parts, COLSUM_ROWS);
+                       C, ld, parts, rows);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
 
 int um_reduce_rows(const float* partials, int parts, int C, int stride, float* out, int accumulate,
                    hipStream_t st) {
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, st, partials, parts,
-                     C, stride, out, accumulate);
+  int cl = 1;
+  while (cl < C && cl < 64) cl <<= 1;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(ceil_div(C, cl)), dim3(256), 0, st, partials, parts,
+                     C, stride, out, accumulate, cl);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -396,22 +396,42 @@ __global__ void cat_bwd_pshuf_kernel(const T* __restrict__ g, int ldg, int coff,
 }
 
 // ---- SE
+constexpr int MEAN_PIX = 2048;  // pixels per block
+// out[n][c] += mean over a pixel chunk (out zeroed by the caller): thread =
+// (8-channel group, pixel lane), 16-byte loads, 2 pixels in flight
 template <typename T>
-__global__ void channel_mean_kernel(const T* __restrict__ x, int ld, long S, int C,
-                                    float* __restrict__ out) {
-  const int n = blockIdx.z;
-  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
-  const int pl = threadIdx.x >> 6;
-  const long p0 = (long)blockIdx.x * 1024, p1 = min(S, p0 + 1024);
-  float t = 0.f;
-  if (c < C)
-    for (long p = p0 + pl; p < p1; p += 4) t += to_f32(x[((long)n * S + p) * ld + c]);
-  __shared__ float red[4][64];
-  red[pl][threadIdx.x & 63] = t;
-  __syncthreads();
-  if (pl == 0 && c < C)
-    atomicAdd(&out[n * C + c],
-              (red[0][c & 63] + red[1][c & 63] + red[2][c & 63] + red[3][c & 63]) / (float)S);
+__global__ void __launch_bounds__(256) channel_mean_kernel(const T* __restrict__ x, int ld, long S,
+                                                            int C, float* __restrict__ out) {
+  __shared__ float red[256 * 8];
+  const int n = blockIdx.y;
+  const int cg = C / 8;
+  const RowMap rm(cg);
+  const long p0 = (long)blockIdx.x * MEAN_PIX, p1 = min(S, p0 + MEAN_PIX);
+  for (int g0 = 0; g0 < cg; g0 += rm.G) {
+    const int g = g0 + rm.g;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (rm.active() && g < cg) {
+      const T* base = x + (long)n * S * ld + g * 8;
+      long p = p0 + rm.lane;
+      for (; p + rm.lanes < p1; p += 2 * rm.lanes) {
+        float u[8], v[8];
+        load8(base + p * ld, u);
+        load8(base + (p + rm.lanes) * ld, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += u[e] + v[e];
+      }
+      if (p < p1) {
+        float u[8];
+        load8(base + p * ld, u);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += u[e];
+      }
+    }
+    lane_reduce<8>(red, rm, acc);
+    if (rm.lane == 0 && g < cg)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(&out[n * C + g * 8 + e], acc[e] / (float)S);
+  }
 }
 
 __global__ void se_mlp_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ w1,
@@ -577,7 +597,8 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
 
 int um_channel_mean(int dtype, int N, long S, int C, const void* x, int ld, float* out,
                     hipStream_t st) {
-  dim3 grid(ceil_div(S, 1024), ceil_div(C, 64), N);
+  UM_CHECK_ARG(C % 8 == 0 && ld % 8 == 0, "um_channel_mean: C/ld %% 8");
+  dim3 grid(ceil_div(S, MEAN_PIX), N);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(channel_mean_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, ld,
                        S, C, out);

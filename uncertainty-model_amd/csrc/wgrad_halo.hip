@@ -42,16 +42,19 @@ struct HwArgs {
   int P, Q, K, ldy;      // output-gradient
   int R, stride, pad, reflect;
   int cimg, kimg;        // image channel strides (16 * power of two)
-  int xm0, xm1, xm2;     // X image swizzle masks
-  int ym0, ym1, ym2;     // DY image swizzle masks
-  int TH, TW, HH, HWd;   // pixel tile and halo
+  int xm0, xm1, xm2;     // X image swizzle bit positions (31 = unused)
+  int ym0, ym1, ym2;     // DY image swizzle bit positions
+  int cshift, kshift;    // log2(cimg), log2(kimg)
+  int TH, TW, HH, HWd;   // pixel tile; halo rows and row stride (pixels, % 32 == 0)
+  int HWr, twshift;      // real halo row length, log2(TW)
   int tiles_x, tiles_y, ntiles;
   int taps_per_group;
 };
 
-__device__ __forceinline__ int par(int v) { return __popc(v) & 1; }
-__device__ __forceinline__ int swz(int pix, int m0, int m1, int m2) {
-  return par(pix & m0) | (par(pix & m1) << 1) | (par(pix & m2) << 2);
+// swizzle of 32-B channel chunks: bits (pix >> s_i) & 1 (masks are single
+// bits; unused entries shift by 31, which reads 0 for any pixel index)
+__device__ __forceinline__ int swz(int pix, int s0, int s1, int s2) {
+  return ((pix >> s0) & 1) | (((pix >> s1) & 1) << 1) | (((pix >> s2) & 1) << 2);
 }
 
 // element offset of 8-channel chunk c8 of pixel pix in a swizzled image
@@ -60,24 +63,16 @@ __device__ __forceinline__ int img_off(int pix, int c8, int cimg, int m0, int m1
   return pix * cimg + (c16 << 4) + ((c8 & 1) << 3);
 }
 
-// transposed fragment of 32 pixels x 16 channels: pixel rows pix0 + 8g + q
-// (+4), channels 16*ct + 4p .. +3; returns lane's 8 pixels of channel (l&15)
-__device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* img, int pixA, int pixB, int ct, int p,
-                                            int cimg, int m0, int m1, int m2) {
-  const int oa = pixA * cimg + (((ct ^ swz(pixA, m0, m1, m2)) << 4) + 4 * p);
-  const int ob = pixB * cimg + (((ct ^ swz(pixB, m0, m1, m2)) << 4) + 4 * p);
-  const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-      (__attribute__((address_space(3))) bf16x4_t*)(img + oa));
-  const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-      (__attribute__((address_space(3))) bf16x4_t*)(img + ob));
-  return bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+__device__ __forceinline__ bf16x4_t tr_read(const bf16_t* img, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (__attribute__((address_space(3))) bf16x4_t*)(img + off));
 }
 
 template <int KT, int CT, int TPW>
 __global__ void __launch_bounds__(512) hwgrad_kernel(HwArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   bf16_t* sY = smem;                              // [TH*TW][kimg]
-  bf16_t* sX = smem + a.TH * a.TW * a.kimg;       // [HH*HWd][cimg]
+  bf16_t* sX = smem + a.TH * a.TW * a.kimg;       // [HH][HWd][cimg], HWd % 32 == 0
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -86,14 +81,34 @@ __global__ void __launch_bounds__(512) hwgrad_kernel(HwArgs a) {
   const int tap1 = min(RR, tap0 + a.taps_per_group);
   const int st = a.stride;
 
-  int my_r[TPW], my_s[TPW];
+  // LDS element offsets of this lane's transposed reads relative to a
+  // chunk's base pixel.  Chunk bases are multiples of 32 pixels (tile rows
+  // of 32/64 and halo rows padded to HWd % 32 == 0), so the swizzle of the
+  // lane's pixel, which uses bits 0..4 only, is the same in every chunk:
+  // precompute it once per (tap, channel tile, read).
+  int xo[TPW][CT][2];
   bool my_ok[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
     const int t = tap0 + wave + 8 * i;
     my_ok[i] = t < tap1;
-    my_r[i] = my_ok[i] ? t / a.R : 0;
-    my_s[i] = my_ok[i] ? t - (t / a.R) * a.R : 0;
+    const int tt = my_ok[i] ? t : tap0;  // unused slots read a valid tap, never stored
+    const int r = tt / a.R, s = tt - (tt / a.R) * a.R;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pix = r * a.HWd + s + (8 * g + q + 4 * h) * st;
+      const int sw = swz(pix, a.xm0, a.xm1, a.xm2);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) xo[i][ct][h] = (pix << a.cshift) + 4 * p + ((ct ^ sw) << 4);
+    }
+  }
+  int yo[KT][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int pix = 8 * g + q + 4 * h;
+    const int sw = swz(pix, a.ym0, a.ym1, a.ym2);
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) yo[kt][h] = (pix << a.kshift) + 4 * p + ((kt ^ sw) << 4);
   }
   bool any = false;
 #pragma unroll
@@ -108,59 +123,84 @@ __global__ void __launch_bounds__(512) hwgrad_kernel(HwArgs a) {
       for (int ct = 0; ct < CT; ++ct) acc[i][kt][ct] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int tpi = a.tiles_x * a.tiles_y;
-  const int kc8 = a.kimg >> 3, cc8 = a.cimg >> 3;
+  const int kc8s = a.kshift - 3, cc8s = a.cshift - 3;  // log2 of 8-channel chunks per pixel
   const int tile_pix = a.TH * a.TW;
   const int chunks_per_row = a.TW >> 5;
+  const int ny = tile_pix << kc8s;          // DY elements (16 B each)
+  const int nxr = a.HWr << cc8s;            // X elements per halo row
+  const int nx = a.HH * nxr;
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     const int n = tile / tpi;
     const int tr = tile - n * tpi;
     const int py0 = (tr / a.tiles_x) * a.TH;
     const int qx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * a.TW;
-    // ---- stage DY tile
-    for (int i = tid; i < tile_pix * kc8; i += 512) {
-      const int pix = i / kc8, c8 = i - (i / kc8) * kc8;
-      const int py = py0 + pix / a.TW, qx = qx0 + pix % a.TW;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (py < a.P && qx < a.Q && c8 * 8 < a.K)
-        v = *reinterpret_cast<const uint4*>(a.dy + ((long)(n * a.P + py) * a.Q + qx) * a.ldy + c8 * 8);
-      *reinterpret_cast<uint4*>(sY + img_off(pix, c8, a.kimg, a.ym0, a.ym1, a.ym2)) = v;
-    }
-    // ---- stage X halo
     const int iy0 = py0 * st - a.pad, ix0 = qx0 * st - a.pad;
-    const int hpix = a.HH * a.HWd;
-    for (int i = tid; i < hpix * cc8; i += 512) {
-      const int pix = i / cc8, c8 = i - (i / cc8) * cc8;
-      int iy = iy0 + pix / a.HWd, ix = ix0 + pix % a.HWd;
-      if (a.reflect) {
-        iy = reflect_idx(iy, a.H);
-        ix = reflect_idx(ix, a.W);
+    // ---- stage DY tile and X halo: 4 loads in flight per thread before the
+    // LDS stores; index decode by shifts (power-of-two widths) and one
+    // division by the halo row length
+    for (int i0 = tid; i0 < ny + nx; i0 += 4 * 512) {
+      uint4 v[4];
+      int off[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 512;
+        v[u] = make_uint4(0, 0, 0, 0);
+        off[u] = -1;
+        if (i < ny) {
+          const int pix = i >> kc8s, c8 = i & ((1 << kc8s) - 1);
+          const int py = py0 + (pix >> a.twshift), qx = qx0 + (pix & (a.TW - 1));
+          off[u] = img_off(pix, c8, a.kimg, a.ym0, a.ym1, a.ym2);
+          if (py < a.P && qx < a.Q && c8 * 8 < a.K)
+            v[u] = *reinterpret_cast<const uint4*>(
+                a.dy + ((long)(n * a.P + py) * a.Q + qx) * a.ldy + c8 * 8);
+        } else if (i < ny + nx) {
+          const int j = i - ny;
+          const int hr = j / nxr;
+          const int jr = j - hr * nxr;
+          const int hc = jr >> cc8s, c8 = jr & ((1 << cc8s) - 1);
+          int iy = iy0 + hr, ix = ix0 + hc;
+          if (a.reflect) {
+            iy = reflect_idx(iy, a.H);
+            ix = reflect_idx(ix, a.W);
+          }
+          off[u] = a.TH * a.TW * a.kimg + img_off(hr * a.HWd + hc, c8, a.cimg, a.xm0, a.xm1, a.xm2);
+          if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c8 * 8 < a.C)
+            v[u] = *reinterpret_cast<const uint4*>(
+                a.x + ((long)(n * a.H + iy) * a.W + ix) * a.ldx + c8 * 8);
+        }
       }
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c8 * 8 < a.C)
-        v = *reinterpret_cast<const uint4*>(a.x + ((long)(n * a.H + iy) * a.W + ix) * a.ldx + c8 * 8);
-      *reinterpret_cast<uint4*>(sX + img_off(pix, c8, a.cimg, a.xm0, a.xm1, a.xm2)) = v;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (off[u] >= 0) *reinterpret_cast<uint4*>(smem + off[u]) = v[u];
     }
     __syncthreads();
     if (any) {
       for (int ch = 0; ch < tile_pix / 32; ++ch) {
         const int ty = ch / chunks_per_row, tx0 = (ch - ty * chunks_per_row) * 32;
-        const int ypix = ty * a.TW + tx0 + 8 * g + q;
+        const bf16_t* yb = sY + ((ty * a.TW + tx0) << a.kshift);
+        const bf16_t* xb = sX + ((ty * st * a.HWd + tx0 * st) << a.cshift);
         bf16x8_t fa[KT];
 #pragma unroll
-        for (int kt = 0; kt < KT; ++kt)
-          fa[kt] = tr_frag(sY, ypix, ypix + 4, kt, p, a.kimg, a.ym0, a.ym1, a.ym2);
+        for (int kt = 0; kt < KT; ++kt) {
+          const bf16x4_t lo = tr_read(yb, yo[kt][0]), hi = tr_read(yb, yo[kt][1]);
+          fa[kt] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+        bf16x8_t fb[TPW][CT];
 #pragma unroll
-        for (int i = 0; i < TPW; ++i) {
-          if (!my_ok[i]) continue;
-          const int xp = (ty * st + my_r[i]) * a.HWd + (tx0 + 8 * g + q) * st + my_s[i];
+        for (int i = 0; i < TPW; ++i)
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) {
-            const bf16x8_t fb = tr_frag(sX, xp, xp + 4 * st, ct, p, a.cimg, a.xm0, a.xm1, a.xm2);
+            const bf16x4_t lo = tr_read(xb, xo[i][ct][0]), hi = tr_read(xb, xo[i][ct][1]);
+            fb[i][ct] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int kt = 0; kt < KT; ++kt)
-              acc[i][kt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kt], fb, acc[i][kt][ct], 0, 0, 0);
-          }
-        }
+              acc[i][kt][ct] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kt], fb[i][ct], acc[i][kt][ct], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -195,15 +235,22 @@ int pow2_chunks(int ch) {  // 16-channel chunks rounded up to a power of two
   return p;
 }
 
-// bank-conflict-minimising swizzle masks (exhaustive search, see file header)
+// bank-conflict-minimising swizzle (exhaustive search over parity masks,
+// see file header; the winners are single bits): bit positions, 31 = unused
 void masks_for(int nch, int stride, int* m) {
-  m[0] = m[1] = m[2] = 0;
-  if (nch == 2) m[0] = stride == 1 ? 8 : 4;
-  if (nch == 4) { m[0] = 2; m[1] = stride == 1 ? 8 : 4; }
+  m[0] = m[1] = m[2] = 31;
+  if (nch == 2) m[0] = stride == 1 ? 3 : 2;
+  if (nch == 4) { m[0] = 1; m[1] = stride == 1 ? 3 : 2; }
   if (nch == 8) {
-    if (stride == 1) { m[0] = 1; m[1] = 2; m[2] = 8; }
-    else { m[0] = 2; m[1] = 4; m[2] = 16; }
+    if (stride == 1) { m[0] = 0; m[1] = 1; m[2] = 3; }
+    else { m[0] = 1; m[1] = 2; m[2] = 4; }
   }
+}
+
+int ilog2(int v) {
+  int r = 0;
+  while ((1 << r) < v) ++r;
+  return r;
 }
 
 struct HwPlan {
@@ -240,6 +287,8 @@ HwPlan plan(int N, int H, int W, int C, int ldx, int K, int R, int stride, int p
   a.R = R; a.stride = stride; a.pad = pad; a.reflect = reflect;
   a.cimg = 16 * nct;
   a.kimg = 16 * nkt;
+  a.cshift = ilog2(a.cimg);
+  a.kshift = ilog2(a.kimg);
   int m[3];
   masks_for(nct, stride, m);
   a.xm0 = m[0]; a.xm1 = m[1]; a.xm2 = m[2];
@@ -250,9 +299,11 @@ HwPlan plan(int N, int H, int W, int C, int ldx, int K, int R, int stride, int p
     a.TW = Q >= 64 ? 64 : 32;
     a.TH = tp / a.TW;
     a.HH = (a.TH - 1) * stride + R;
-    a.HWd = (a.TW - 1) * stride + R;
+    a.HWr = (a.TW - 1) * stride + R;
+    a.HWd = (a.HWr + 31) / 32 * 32;
+    a.twshift = ilog2(a.TW);
     h.lds = (size_t)2 * (a.TH * a.TW * a.kimg + a.HH * a.HWd * a.cimg);
-    if (h.lds <= 76 * 1024) break;
+    if (h.lds <= 80 * 1024) break;
   }
   if (h.lds > 150 * 1024) return h;
   a.tiles_x = (Q + a.TW - 1) / a.TW;
