@@ -194,9 +194,10 @@ int um_channel_mean(int dtype, int N, long S, int C, const void* x, int ld, floa
                     hipStream_t stream);
 int um_se_mlp_fwd(int N, int C, int R, const float* pooled, const float* w1, const float* w2,
                   float* z1, float* s, hipStream_t stream);
+/* dw1/dw2 accumulate (+=); dz: f32 [N][R] scratch */
 int um_se_mlp_bwd(int N, int C, int R, const float* ds, const float* s, const float* z1,
                   const float* pooled, const float* w1, const float* w2, float* dw1,
-                  float* dw2, float* dpool_scaled, float inv_S, hipStream_t stream);
+                  float* dw2, float* dpool_scaled, float* dz, float inv_S, hipStream_t stream);
 
 /* ---------------------------------------------------------------- loss ---
  * Loss stack: scale_pyramid (reference train/utils.py:27-50), reconstruct

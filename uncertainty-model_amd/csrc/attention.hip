@@ -165,17 +165,18 @@ __global__ void apply_kernel(const T* __restrict__ qkv, int ld, int S, int C, in
   const int d = C / heads;
   const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
   const int s0 = tile * PT, np = min(PT, S - s0);
+  const int dq = d + 1;      // padded rows: per-pixel loops stay bank-conflict free
   float* sC = sh;            // [d][d]
-  float* sQ = sh + d * d;    // [PT][d]
+  float* sQ = sh + d * d;    // [PT][d+1]
   const float* cg = ctx + ((long)n * heads + h) * d * d;
   for (int i = threadIdx.x; i < d * d; i += blockDim.x) sC[i] = cg[i];
   for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
     const int s = i / d, c = i % d;
-    sQ[i] = to_f32(qkv[((long)n * S + s0 + s) * ld + C + h * d + c]);
+    sQ[s * dq + c] = to_f32(qkv[((long)n * S + s0 + s) * ld + C + h * d + c]);
   }
   __syncthreads();
   if (threadIdx.x < np) {
-    float* q = sQ + threadIdx.x * d;
+    float* q = sQ + threadIdx.x * dq;
     float mx = -INFINITY;
     for (int c = 0; c < d; ++c) mx = fmaxf(mx, q[c]);
     float sum = 0.f;
@@ -190,7 +191,7 @@ __global__ void apply_kernel(const T* __restrict__ qkv, int ld, int S, int C, in
   for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
     const int s = i / d, cp = i % d;
     float acc = 0.f;
-    for (int c = 0; c < d; ++c) acc += sC[c * d + cp] * sQ[s * d + c];
+    for (int c = 0; c < d; ++c) acc += sC[c * d + cp] * sQ[s * dq + c];
     att[((long)n * S + s0 + s) * ldo + h * d + cp] = from_f32<T>(acc);
   }
 }
@@ -204,28 +205,29 @@ __global__ void apply_bwd_kernel(const T* __restrict__ qkv, int ld, int S, int C
                                  float* __restrict__ parts) {
   extern __shared__ float sh[];
   const int d = C / heads;
+  const int dq = d + 1;  // padded pixel rows (per-pixel loops conflict free)
   const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
   const int s0 = tile * PT, np = min(PT, S - s0);
-  float* sC = sh;                 // [d][d]
-  float* sQ = sC + d * d;         // [PT][d]  softmaxed q
-  float* sG = sQ + PT * d;        // [PT][d]  datt
-  float* sD = sG + PT * d;        // [PT][d]  dQs
+  float* sCt = sh;                // ctx^T [d][d]: sCt[cp][c] = ctx[c][cp]
+  float* sQ = sCt + d * d;        // [PT][d+1]  softmaxed q
+  float* sG = sQ + PT * dq;       // [PT][d+1]  datt
+  float* sD = sG + PT * dq;       // [PT][d+1]  dQs
   const float* cg = ctx + ((long)n * heads + h) * d * d;
-  for (int i = threadIdx.x; i < d * d; i += blockDim.x) sC[i] = cg[i];
+  for (int i = threadIdx.x; i < d * d; i += blockDim.x) sCt[(i % d) * d + i / d] = cg[i];
   for (int i = threadIdx.x; i < PT * d; i += blockDim.x) {
     const int s = i / d, c = i % d;
     if (s < np) {
       const long row = (long)n * S + s0 + s;
-      sQ[i] = to_f32(qkv[row * ld + C + h * d + c]);
-      sG[i] = to_f32(datt[row * ldd + h * d + c]);
+      sQ[s * dq + c] = to_f32(qkv[row * ld + C + h * d + c]);
+      sG[s * dq + c] = to_f32(datt[row * ldd + h * d + c]);
     } else {
-      sQ[i] = 0.f;
-      sG[i] = 0.f;
+      sQ[s * dq + c] = 0.f;
+      sG[s * dq + c] = 0.f;
     }
   }
   __syncthreads();
   if (threadIdx.x < np) {
-    float* q = sQ + threadIdx.x * d;
+    float* q = sQ + threadIdx.x * dq;
     float mx = -INFINITY;
     for (int c = 0; c < d; ++c) mx = fmaxf(mx, q[c]);
     float sum = 0.f;
@@ -241,25 +243,25 @@ __global__ void apply_bwd_kernel(const T* __restrict__ qkv, int ld, int S, int C
   for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
     const int s = i / d, c = i % d;
     float acc = 0.f;
-    for (int cp = 0; cp < d; ++cp) acc += sC[c * d + cp] * sG[s * d + cp];
-    sD[i] = acc;
+    for (int cp = 0; cp < d; ++cp) acc += sCt[cp * d + c] * sG[s * dq + cp];
+    sD[s * dq + c] = acc;
   }
   // dctx partial[c][c'] = sum_s qs[s][c] * datt[s][c']
   float* out = parts + (((long)n * ntiles + tile) * heads + h) * d * d;
   for (int o = threadIdx.x; o < d * d; o += blockDim.x) {
     const int c = o / d, cp = o % d;
     float acc = 0.f;
-    for (int s = 0; s < np; ++s) acc += sQ[s * d + c] * sG[s * d + cp];
+    for (int s = 0; s < np; ++s) acc += sQ[s * dq + c] * sG[s * dq + cp];
     out[o] = acc;
   }
   __syncthreads();
-  if (threadIdx.x < np) {
-    const int s = threadIdx.x;
+  // dq = qs * (dQs - <qs, dQs>): thread per (pixel, channel)
+  for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
+    const int s = i / d, c = i % d;
     float dot = 0.f;
-    for (int c = 0; c < d; ++c) dot += sQ[s * d + c] * sD[s * d + c];
+    for (int k = 0; k < d; ++k) dot += sQ[s * dq + k] * sD[s * dq + k];
     const long row = (long)n * S + s0 + s;
-    for (int c = 0; c < d; ++c)
-      dqkv[row * ldq + C + h * d + c] = from_f32<T>(sQ[s * d + c] * (sD[s * d + c] - dot));
+    dqkv[row * ldq + C + h * d + c] = from_f32<T>(sQ[s * dq + c] * (sD[s * dq + c] - dot));
   }
 }
 
@@ -275,11 +277,15 @@ __global__ void kv_bwd_kernel(const T* __restrict__ qkv, int ld, int S, int C, i
   const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
   const int s0 = tile * PT, np = min(PT, S - s0);
   float* sC = sh;             // dctx [d][d]
-  float* sK = sC + d * d;     // Ks [PT][d]
+  float* sCt = sC + d * d;    // dctx^T [d][d] (conflict-free reads along c)
+  float* sK = sCt + d * d;    // Ks [PT][d]
   float* sV = sK + PT * d;    // V  [PT][d]
   float* sP = sV + PT * d;    // Ks * dKs [PT][d]
   const float* cg = dctx + ((long)n * heads + h) * d * d;
-  for (int i = threadIdx.x; i < d * d; i += blockDim.x) sC[i] = cg[i];
+  for (int i = threadIdx.x; i < d * d; i += blockDim.x) {
+    sC[i] = cg[i];
+    sCt[(i % d) * d + i / d] = cg[i];
+  }
   for (int i = threadIdx.x; i < np * d; i += blockDim.x) {
     const int s = i / d, c = i % d;
     const long row = ((long)n * S + s0 + s) * ld;
@@ -293,7 +299,7 @@ __global__ void kv_bwd_kernel(const T* __restrict__ qkv, int ld, int S, int C, i
     const int s = i / d, c = i % d;
     float g = 0.f, dv = 0.f;
     for (int cp = 0; cp < d; ++cp) {
-      g += sC[c * d + cp] * sV[s * d + cp];    // dKs[s][c]
+      g += sCt[cp * d + c] * sV[s * d + cp];   // dKs[s][c]
       dv += sK[s * d + cp] * sC[cp * d + c];   // dV[s][c]
     }
     const long row = (long)n * S + s0 + s;
@@ -389,7 +395,7 @@ int um_attn_fwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
     hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div(L, jl), N), dim3(256), 0, st, ws, N, nctx,
                        L, ctx, jl);
   }
-  const size_t shm_ap = ((size_t)d * d + PT * d) * sizeof(float);
+  const size_t shm_ap = ((size_t)d * d + PT * (d + 1)) * sizeof(float);
   const dim3 g(ceil_div(S, PT), heads, N);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(apply_kernel<bf16_t>, g, dim3(256), shm_ap, st, (const bf16_t*)qkv, ld, S,
@@ -411,7 +417,17 @@ int um_attn_bwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
   UM_CHECK_ARG(d <= 64 && C % heads == 0, "um_attn_bwd: head dim");
   const int nt = ceil_div(S, PT);
   const dim3 g(nt, heads, N);
-  const size_t shm_a = ((size_t)d * d + 3 * PT * d) * sizeof(float);
+  const size_t shm_a = ((size_t)d * d + 3 * PT * (d + 1)) * sizeof(float);
+  static bool attr = false;  // d = 64 needs more than the default 64 KB of dynamic LDS
+  if (!attr) {
+    const void* ks[] = {reinterpret_cast<const void*>(&apply_bwd_kernel<bf16_t>),
+                        reinterpret_cast<const void*>(&apply_bwd_kernel<float>),
+                        reinterpret_cast<const void*>(&kv_bwd_kernel<bf16_t>),
+                        reinterpret_cast<const void*>(&kv_bwd_kernel<float>)};
+    for (const void* k : ks)
+      hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(apply_bwd_kernel<bf16_t>, g, dim3(256), shm_a, st, (const bf16_t*)qkv, ld,
                        S, C, heads, ctx, (const bf16_t*)datt, ldd, (bf16_t*)dqkv, ldq, nt, ws);
@@ -424,7 +440,7 @@ int um_attn_bwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
     hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div(L, jl), N), dim3(256), 0, st, ws, N, nt, L,
                        dctx, jl);
   }
-  const size_t shm_k = ((size_t)d * d + 3 * PT * d) * sizeof(float);
+  const size_t shm_k = ((size_t)2 * d * d + 3 * PT * d) * sizeof(float);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(kv_bwd_kernel<bf16_t>, g, dim3(256), shm_k, st, (const bf16_t*)qkv, ld, S,
                        C, heads, kmax, ksum, dctx, (bf16_t*)dqkv, ldq, dks_ws, nt, ws);

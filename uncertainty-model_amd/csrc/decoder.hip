@@ -81,75 +81,101 @@ __device__ __forceinline__ void ld8_any(const void* p, long off, int dt, float* 
   else load8(reinterpret_cast<const float*>(p) + off, v);
 }
 
-// one thread per (pixel, 8 destination channels); vector fast path when the
-// 8 channels come from one aligned COPY/UP2 source
-template <typename T>
-__global__ void concat_build_kernel(CatArgs a, int N, int H, int W, int Ctot, T* __restrict__ dst,
-                                    int ld) {
-  const int cg = Ctot / 8;
+// 8 channels [cc, cc+8) of source pixel `off` as f32, lanes >= C zeroed.
+// ld % 8 == 0: one 16/32-byte load (channels past C up to ceil8(C) <= ld
+// exist in the row); C <= 4 with an f32 row of 4 (the disparity): one float4.
+struct F8 {
+  float v[8];
+};
+__device__ __forceinline__ F8 src8(const CatSrc& s, long off, int cc) {
+  F8 r;
+  if ((s.ld & 7) == 0) {
+    if (s.dtype == UM_BF16) load8(reinterpret_cast<const bf16_t*>(s.ptr) + off + cc, r.v);
+    else load8(reinterpret_cast<const float*>(s.ptr) + off + cc, r.v);
+  } else {
+    const float4 q = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(s.ptr) + off);
+    r.v[0] = q.x; r.v[1] = q.y; r.v[2] = q.z; r.v[3] = q.w;
+    r.v[4] = r.v[5] = r.v[6] = r.v[7] = 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r.v[e] = (cc + e < s.C) ? r.v[e] : 0.f;
+  return r;
+}
+
+// One launch per concat source: thread per (pixel, 8 destination channels)
+// of the source's span [coff, coff + ceil8(C)) (sources start at 8-aligned
+// offsets, so the spans tile the concat; lanes >= C are written as 0).
+// Vector loads for COPY/UP2 rows with ld % 8 == 0 or the 4-channel f32
+// disparity, and for PSHUF (the 32 source channels 4cc .. 4cc+31 holding
+// the group's sub-pixel values); per-element fallback otherwise.
+template <typename T, int OP>
+__global__ void __launch_bounds__(256) cat_src_kernel(CatSrc s, int N, int H, int W,
+                                                       T* __restrict__ dst, int ld) {
+  const int cg = (s.C + 7) / 8;
   const long total = (long)N * H * W * cg;
+  const bool vec_ok = (OP == UM_CAT_PSHUF)
+                          ? ((s.ld & 7) == 0 && (s.C & 7) == 0)
+                          : ((s.ld & 7) == 0 || (s.C <= 4 && (s.ld & 3) == 0 && s.dtype == UM_F32));
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cg) * 8;
+    const int cc = (int)(i % cg) * 8;
     const long pix = i / cg;
     const int x = pix % W;
     const int y = (pix / W) % H;
     const int n = pix / ((long)W * H);
-    float v[8];
-    int k = 0;
-    for (; k < a.nsrc; ++k)
-      if (c0 >= a.s[k].coff && c0 < a.s[k].coff + a.s[k].C) break;
-    const bool fast = k < a.nsrc && c0 + 8 <= a.s[k].coff + a.s[k].C &&
-                      ((c0 - a.s[k].coff) & 7) == 0 && (a.s[k].ld & 7) == 0 &&
-                      (a.s[k].C & 7) == 0 && a.s[k].op != UM_CAT_PSHUF;
-    if (fast) {
-      const CatSrc& s = a.s[k];
-      const int cc = c0 - s.coff;
-      if (s.op == UM_CAT_COPY) {
-        ld8_any(s.ptr, ((long)(n * H + y) * W + x) * s.ld + cc, s.dtype, v);
-      } else {
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!vec_ok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (cc + e < s.C) v[e] = cat_value(s, n, y, x, H, W, cc + e);  // gate inside
+    } else {
+      if (OP == UM_CAT_COPY) {
+        const F8 t = src8(s, ((long)(n * H + y) * W + x) * s.ld, cc);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = t.v[e];
+      } else if (OP == UM_CAT_UP2) {
         int y0, y1, x0, x1;
         float ly, lx;
         up_index(y, s.h, H, y0, y1, ly);
         up_index(x, s.w, W, x0, x1, lx);
         const long b = (long)n * s.h;
-        float v00[8], v01[8], v10[8], v11[8];
-        ld8_any(s.ptr, ((b + y0) * s.w + x0) * s.ld + cc, s.dtype, v00);
-        ld8_any(s.ptr, ((b + y0) * s.w + x1) * s.ld + cc, s.dtype, v01);
-        ld8_any(s.ptr, ((b + y1) * s.w + x0) * s.ld + cc, s.dtype, v10);
-        ld8_any(s.ptr, ((b + y1) * s.w + x1) * s.ld + cc, s.dtype, v11);
+        const F8 v00 = src8(s, ((b + y0) * s.w + x0) * s.ld, cc);
+        const F8 v01 = src8(s, ((b + y0) * s.w + x1) * s.ld, cc);
+        const F8 v10 = src8(s, ((b + y1) * s.w + x0) * s.ld, cc);
+        const F8 v11 = src8(s, ((b + y1) * s.w + x1) * s.ld, cc);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          v[e] = (1.f - ly) * ((1.f - lx) * v00[e] + lx * v01[e]) +
-                 ly * ((1.f - lx) * v10[e] + lx * v11[e]);
+          v[e] = (1.f - ly) * ((1.f - lx) * v00.v[e] + lx * v01.v[e]) +
+                 ly * ((1.f - lx) * v10.v[e] + lx * v11.v[e]);
+      } else {  // PSHUF: src [N][H/2][W/2][4C], channel 4c + (y&1)*2 + (x&1)
+        const long off = ((long)(n * s.h + (y >> 1)) * s.w + (x >> 1)) * s.ld + 4 * cc;
+        const int sub = (y & 1) * 2 + (x & 1);
+        float q[32];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ld8_any(s.ptr, off + 8 * j, s.dtype, q + 8 * j);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)  // selects, not a dynamically indexed register array
+          v[e] = sub == 0 ? q[4 * e] : sub == 1 ? q[4 * e + 1] : sub == 2 ? q[4 * e + 2] : q[4 * e + 3];
       }
       if (s.scale) {
-        float sc[8];
-        load8(s.scale + n * s.C + cc, sc);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] *= sc[e];
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = c0 + e;
-        v[e] = 0.f;
-        for (int kk = 0; kk < a.nsrc; ++kk) {
-          const int cc = c - a.s[kk].coff;
-          if (cc >= 0 && cc < a.s[kk].C) {
-            v[e] = cat_value(a.s[kk], n, y, x, H, W, cc);
-            break;
-          }
-        }
+        for (int e = 0; e < 8; ++e)
+          if (cc + e < s.C) v[e] *= s.scale[n * s.C + cc + e];
       }
     }
-    store8(dst + pix * ld + c0, v);
+    store8(dst + pix * ld + s.coff + cc, v);
   }
 }
 
 // ---- backward: RowMap blocks (channel groups x pixel lanes) over a chunk of
-// BWD_CHUNK source pixels of one image n; grid (chunks, 1, N)
-constexpr int BWD_CHUNK = 256;
+// `chunk` source pixels of one image n (bwd_chunk); grid (chunks, 1, N)
+// source pixels per block: ~2048 blocks overall, 16..256 pixels each
+inline int bwd_chunk(long P, int N) {
+  const long want = ((long)P * N + 2047) / 2048;
+  int c = 16;
+  while (c < want && c < 256) c <<= 1;
+  return c;
+}
 
 __device__ __forceinline__ void st8_any(void* p, long off, int dt, const float* v, int acc) {
   float o[8];
@@ -220,13 +246,13 @@ template <typename T, int OP>
 __global__ void __launch_bounds__(256) cat_bwd_kernel(const T* __restrict__ g, int ldg, int coff,
                                                       int H, int W, CatSrc s, void* dsrc, int ldd,
                                                       int dsd, int acc,
-                                                      float* __restrict__ dscale) {
+                                                      float* __restrict__ dscale, int chunk) {
   __shared__ float red[256 * 8];
   const int n = blockIdx.z;
   const int cg = s.C / 8;
   const RowMap rm(cg);
   const long P = (long)s.h * s.w;
-  const long p0 = (long)blockIdx.x * BWD_CHUNK, p1 = min(P, p0 + BWD_CHUNK);
+  const long p0 = (long)blockIdx.x * chunk, p1 = min(P, p0 + chunk);
   for (int g0 = 0; g0 < cg; g0 += rm.G) {
     const int gi = g0 + rm.g;
     const int c = gi * 8;
@@ -325,14 +351,15 @@ template <typename T, int OP>
 __global__ void __launch_bounds__(256) cat_bwd_scalar_kernel(const T* __restrict__ g, int ldg,
                                                              int coff, int H, int W, CatSrc s,
                                                              void* dsrc, int ldd, int dsd,
-                                                             int acc, float* __restrict__ dscale) {
+                                                             int acc, float* __restrict__ dscale,
+                                                             int chunk) {
   __shared__ float red[256];
   const int n = blockIdx.z;
   const int Cl = s.C < 256 ? s.C : 256;
   const int lanes = 256 / Cl;
   const int cl = threadIdx.x % Cl, lane = threadIdx.x / Cl;
   const long P = (long)s.h * s.w;
-  const long p0 = (long)blockIdx.x * BWD_CHUNK, p1 = min(P, p0 + BWD_CHUNK);
+  const long p0 = (long)blockIdx.x * chunk, p1 = min(P, p0 + chunk);
   for (int c0 = 0; c0 < s.C; c0 += Cl) {
     const int c = c0 + cl;
     float ds = 0.f;
@@ -459,44 +486,61 @@ __global__ void se_mlp_fwd_kernel(const float* __restrict__ pooled, const float*
 }
 
 // single block; dw1 [R][C], dw2 [C][R] accumulated; dpool_scaled[n][c] = dpool / S
-__global__ void se_mlp_bwd_kernel(int N, int C, int R, const float* __restrict__ ds,
-                                  const float* __restrict__ s, const float* __restrict__ z1,
-                                  const float* __restrict__ pooled, const float* __restrict__ w1,
-                                  const float* __restrict__ w2, float* __restrict__ dw1,
-                                  float* __restrict__ dw2, float* __restrict__ dpool,
-                                  float inv_S) {
-  extern __shared__ float sh[];
-  float* dl2 = sh;            // [N][C]
-  float* dz = sh + N * C;     // [N][R]
-  for (int i = threadIdx.x; i < N * C; i += blockDim.x) {
-    const float sv = s[i];
-    dl2[i] = ds[i] * sv * (1.f - sv);
+// SE excite backward, two launches:
+//  (1) dz[n][r] = relu'(z1) * sum_c w2[c][r] * ds[n][c] s(1-s): one wave per
+//      (n, r), lanes over c;
+//  (2) one thread per output of dw2[c][r] += sum_n dl2[n][c] z1[n][r],
+//      dw1[r][c] += sum_n dz[n][r] pooled[n][c] and
+//      dpool[n][c] = inv_S * sum_r w1[r][c] dz[n][r]
+__global__ void __launch_bounds__(256) se_dz_kernel(int N, int C, int R, const float* __restrict__ ds,
+                                                     const float* __restrict__ s,
+                                                     const float* __restrict__ z1,
+                                                     const float* __restrict__ w2,
+                                                     float* __restrict__ dz) {
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (pair >= N * R) return;
+  const int n = pair / R, r = pair % R;
+  float t = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float sv = s[n * C + c];
+    t += w2[c * R + r] * ds[n * C + c] * sv * (1.f - sv);
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < N * R; i += blockDim.x) {
-    const int n = i / R, r = i % R;
+  t = wave_sum(t);
+  if (lane == 0) dz[pair] = z1[pair] > 0.f ? t : 0.f;
+}
+
+__global__ void __launch_bounds__(256) se_wgrad_kernel(int N, int C, int R, const float* __restrict__ ds,
+                                                        const float* __restrict__ s,
+                                                        const float* __restrict__ z1,
+                                                        const float* __restrict__ pooled,
+                                                        const float* __restrict__ w1,
+                                                        const float* __restrict__ dz,
+                                                        float* __restrict__ dw1,
+                                                        float* __restrict__ dw2,
+                                                        float* __restrict__ dpool, float inv_S) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long CR = (long)C * R;
+  if (i < CR) {  // dw2[c][r]
+    const int c = i / R, r = i % R;
     float t = 0.f;
-    for (int c = 0; c < C; ++c) t += w2[c * R + r] * dl2[n * C + c];
-    dz[i] = z1[i] > 0.f ? t : 0.f;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < C * R; i += blockDim.x) {
-    const int c = i / R, r = i % R;  // dw2[c][r]
-    float t = 0.f;
-    for (int n = 0; n < N; ++n) t += dl2[n * C + c] * z1[n * R + r];
+    for (int n = 0; n < N; ++n) {
+      const float sv = s[n * C + c];
+      t += ds[n * C + c] * sv * (1.f - sv) * z1[n * R + r];
+    }
     dw2[i] += t;
-  }
-  for (int i = threadIdx.x; i < R * C; i += blockDim.x) {
-    const int r = i / C, c = i % C;  // dw1[r][c]
+  } else if (i < 2 * CR) {  // dw1[r][c]
+    const long j = i - CR;
+    const int r = j / C, c = j % C;
     float t = 0.f;
     for (int n = 0; n < N; ++n) t += dz[n * R + r] * pooled[n * C + c];
-    dw1[i] += t;
-  }
-  for (int i = threadIdx.x; i < N * C; i += blockDim.x) {
-    const int n = i / C, c = i % C;
+    dw1[j] += t;
+  } else if (i < 2 * CR + (long)N * C) {  // dpool[n][c]
+    const long j = i - 2 * CR;
+    const int n = j / C, c = j % C;
     float t = 0.f;
     for (int r = 0; r < R; ++r) t += w1[r * C + c] * dz[n * R + r];
-    dpool[i] = t * inv_S;
+    dpool[j] = t * inv_S;
   }
 }
 
@@ -524,13 +568,27 @@ int um_concat_build(int dtype, int N, int H, int W, void* dst, int ld, int Ctot,
     UM_CHECK_ARG(s.op == UM_CAT_COPY || (2 * s.h == H && 2 * s.w == W), "um_concat_build: x2 size");
   }
   UM_CHECK_ARG(Ctot % 8 == 0 && ld % 8 == 0, "um_concat_build: Ctot/ld %% 8");
-  const long total = (long)N * H * W * (Ctot / 8);
-  if (dtype == UM_BF16)
-    hipLaunchKernelGGL(concat_build_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, a, N,
-                       H, W, Ctot, (bf16_t*)dst, ld);
-  else
-    hipLaunchKernelGGL(concat_build_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, a, N,
-                       H, W, Ctot, (float*)dst, ld);
+  int covered = 0;
+  for (int i = 0; i < nsrc; ++i) {
+    const CatSrc& s = a.s[i];
+    UM_CHECK_ARG(s.coff == covered && s.coff % 8 == 0,
+                 "um_concat_build: source %d must start at the 8-aligned end of the previous", i);
+    covered = s.coff + (s.C + 7) / 8 * 8;
+    const int g = grid_for((long)N * H * W * ((s.C + 7) / 8));
+#define CAT_LAUNCH(T, OP) \
+  hipLaunchKernelGGL((cat_src_kernel<T, OP>), dim3(g), dim3(256), 0, st, s, N, H, W, (T*)dst, ld)
+    if (dtype == UM_BF16) {
+      if (s.op == UM_CAT_COPY) CAT_LAUNCH(bf16_t, UM_CAT_COPY);
+      else if (s.op == UM_CAT_UP2) CAT_LAUNCH(bf16_t, UM_CAT_UP2);
+      else CAT_LAUNCH(bf16_t, UM_CAT_PSHUF);
+    } else {
+      if (s.op == UM_CAT_COPY) CAT_LAUNCH(float, UM_CAT_COPY);
+      else if (s.op == UM_CAT_UP2) CAT_LAUNCH(float, UM_CAT_UP2);
+      else CAT_LAUNCH(float, UM_CAT_PSHUF);
+    }
+#undef CAT_LAUNCH
+  }
+  UM_CHECK_ARG(covered == Ctot, "um_concat_build: sources cover %d of %d channels", covered, Ctot);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -557,11 +615,12 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
   const long P = (long)s.h * s.w;
   const bool vec = (s.C % 8 == 0) && (s.coff % 8 == 0) && (ldd % 8 == 0 || !dsrc) &&
                    (s.ld % 8 == 0 || !dscale);
+  const int chunk = bwd_chunk(P, N);
   if (!vec) {
-    dim3 grid(ceil_div(P, BWD_CHUNK), 1, N);
+    dim3 grid(ceil_div(P, chunk), 1, N);
 #define UM_CAT_SCALAR(T_, OP_)                                                               \
     hipLaunchKernelGGL((cat_bwd_scalar_kernel<T_, OP_>), grid, dim3(256), 0, st, (const T_*)g, \
-                       ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, dscale)
+                       ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, dscale, chunk)
     if (dtype == UM_BF16) {
       if (s.op == UM_CAT_COPY) UM_CAT_SCALAR(bf16_t, UM_CAT_COPY); else UM_CAT_SCALAR(bf16_t, UM_CAT_UP2);
     } else {
@@ -571,25 +630,25 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
     UM_LAUNCH_CHECK();
     return UM_OK;
   }
-  dim3 grid(ceil_div(P, BWD_CHUNK), 1, N);
+  dim3 grid(ceil_div(P, chunk), 1, N);
   if (s.op == UM_CAT_COPY) {
     if (dtype == UM_BF16)
       hipLaunchKernelGGL((cat_bwd_kernel<bf16_t, UM_CAT_COPY>), grid, dim3(256), 0, st,
                          (const bf16_t*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
-                         accumulate, dscale);
+                         accumulate, dscale, chunk);
     else
       hipLaunchKernelGGL((cat_bwd_kernel<float, UM_CAT_COPY>), grid, dim3(256), 0, st,
                          (const float*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate,
-                         dscale);
+                         dscale, chunk);
   } else {
     if (dtype == UM_BF16)
       hipLaunchKernelGGL((cat_bwd_kernel<bf16_t, UM_CAT_UP2>), grid, dim3(256), 0, st,
                          (const bf16_t*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
-                         accumulate, dscale);
+                         accumulate, dscale, chunk);
     else
       hipLaunchKernelGGL((cat_bwd_kernel<float, UM_CAT_UP2>), grid, dim3(256), 0, st,
                          (const float*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate,
-                         dscale);
+                         dscale, chunk);
   }
   UM_LAUNCH_CHECK();
   return UM_OK;
@@ -619,11 +678,12 @@ int um_se_mlp_fwd(int N, int C, int R, const float* pooled, const float* w1, con
 
 int um_se_mlp_bwd(int N, int C, int R, const float* ds, const float* s, const float* z1,
                   const float* pooled, const float* w1, const float* w2, float* dw1, float* dw2,
-                  float* dpool_scaled, float inv_S, hipStream_t st) {
-  const size_t shm = ((size_t)N * C + (size_t)N * R) * sizeof(float);
-  UM_CHECK_ARG(shm <= 64 * 1024, "um_se_mlp_bwd: N*C too large (%d x %d)", N, C);
-  hipLaunchKernelGGL(se_mlp_bwd_kernel, dim3(1), dim3(256), shm, st, N, C, R, ds, s, z1, pooled,
-                     w1, w2, dw1, dw2, dpool_scaled, inv_S);
+                  float* dpool_scaled, float* dz, float inv_S, hipStream_t st) {
+  hipLaunchKernelGGL(se_dz_kernel, dim3(ceil_div((long)N * R, 4)), dim3(256), 0, st, N, C, R, ds, s,
+                     z1, w2, dz);
+  const long outs = 2l * C * R + (long)N * C;
+  hipLaunchKernelGGL(se_wgrad_kernel, dim3(ceil_div(outs, 256)), dim3(256), 0, st, N, C, R, ds, s,
+                     z1, pooled, w1, dz, dw1, dw2, dpool_scaled, inv_S);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -78,7 +78,7 @@ _SIG = {
     'um_concat_bwd_src': (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _I, _P, 's']),
     'um_channel_mean': (_I, [_I, _I, _L, _I, _P, _I, _P, 's']),
     'um_se_mlp_fwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, 's']),
-    'um_se_mlp_bwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, 's']),
+    'um_se_mlp_bwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, 's']),
     'um_pyramid_level': (_I, [_P, _I, _I, _I, _P, _I, _I, 's']),
     'um_warp': (_I, [_P, _I, _I, _I, _I, _P, _L, _L, _F, _P, 's']),
     'um_loss_parts': (_I, [_I, _I, _I]),

@@ -267,10 +267,11 @@ class ConvBNELUFn(torch.autograd.Function):
             dw1 = torch.zeros(w1.shape, dtype=torch.float32, device=dev)
             dw2 = torch.zeros(w2.shape, dtype=torch.float32, device=dev)
             add_nc = torch.empty((N, K), dtype=torch.float32, device=dev)
+            dz = torch.empty((N, R1), dtype=torch.float32, device=dev)
             call('um_se_mlp_bwd', N, K, R1, ptr(ds.float().contiguous()), ptr(s), ptr(z1),
                  ptr(pooled), ptr(w1.detach().float().contiguous()),
                  ptr(w2.detach().float().contiguous()), ptr(dw1), ptr(dw2), ptr(add_nc),
-                 1.0 / (P * Q))
+                 ptr(dz), 1.0 / (P * Q))
         dgamma = dbeta = None
         k1 = torch.empty(K, dtype=torch.float32, device=dev)
         k2 = torch.empty_like(k1)
