@@ -187,9 +187,11 @@ typedef struct {
 } um_cat_src;
 int um_concat_build(int dtype, int N, int H, int W, void* dst, int ld, int Ctot, int nsrc,
                     const um_cat_src* srcs, hipStream_t stream);
+/* dscale (+=) needs ws: um_concat_bwd_ws(N, src.h, src.w, src.C) floats */
+long um_concat_bwd_ws(int N, int h, int w, int C);
 int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
                       const um_cat_src* src, void* dsrc, int ldd, int dsrc_dtype,
-                      int accumulate, float* dscale, hipStream_t stream);
+                      int accumulate, float* dscale, float* ws, hipStream_t stream);
 int um_channel_mean(int dtype, int N, long S, int C, const void* x, int ld, float* out,
                     hipStream_t stream);
 int um_se_mlp_fwd(int N, int C, int R, const float* pooled, const float* w1, const float* w2,

@@ -339,7 +339,8 @@ __global__ void __launch_bounds__(256) cat_bwd_kernel(const T* __restrict__ g, i
       lane_reduce<8>(red, rm, ds);
       if (rm.lane == 0 && gi < cg)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) atomicAdd(&dscale[n * s.C + c + e], ds[e]);
+        for (int e = 0; e < 8; ++e)  // per-block partial (no same-address atomics)
+          dscale[((long)n * gridDim.x + blockIdx.x) * s.C + c + e] = ds[e];
     }
   }
 }
@@ -395,7 +396,7 @@ __global__ void __launch_bounds__(256) cat_bwd_scalar_kernel(const T* __restrict
       __syncthreads();
       if (lane == 0 && c < s.C) {
         for (int r = 1; r < lanes; ++r) ds += red[r * Cl + cl];
-        atomicAdd(&dscale[n * s.C + c], ds);
+        dscale[((long)n * gridDim.x + blockIdx.x) * s.C + c] = ds;
       }
       __syncthreads();
     }
@@ -544,6 +545,34 @@ __global__ void __launch_bounds__(256) se_wgrad_kernel(int N, int C, int R, cons
   }
 }
 
+// dscale[n][c] += sum_b parts[n][b][c]: block = (cl channels) x (256/cl
+// b-lanes), grid (ceil(C/cl), N)
+__global__ void __launch_bounds__(256) parts_accum_kernel(const float* __restrict__ parts, int B,
+                                                          int C, float* __restrict__ out, int cl) {
+  __shared__ float red[256];
+  const int lanes = 256 / cl;
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * cl + (threadIdx.x % cl);
+  const int lane = threadIdx.x / cl;
+  float t0 = 0.f, t1 = 0.f;
+  if (c < C) {
+    const float* p = parts + (long)n * B * C + c;
+    int b = lane;
+    for (; b + lanes < B; b += 2 * lanes) {
+      t0 += p[(long)b * C];
+      t1 += p[(long)(b + lanes) * C];
+    }
+    if (b < B) t0 += p[(long)b * C];
+  }
+  float t = t0 + t1;
+  red[threadIdx.x] = t;
+  __syncthreads();
+  if (lane == 0 && c < C) {
+    for (int q = 1; q < lanes; ++q) t += red[q * cl + (threadIdx.x % cl)];
+    out[n * C + c] += t;
+  }
+}
+
 inline int grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -593,9 +622,14 @@ int um_concat_build(int dtype, int N, int H, int W, void* dst, int ld, int Ctot,
   return UM_OK;
 }
 
+long um_concat_bwd_ws(int N, int h, int w, int C) {
+  const long P = (long)h * w;
+  return (long)N * ceil_div(P, bwd_chunk(P, N)) * C;
+}
+
 int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
                       const um_cat_src* src, void* dsrc, int ldd, int dsrc_dtype, int accumulate,
-                      float* dscale, hipStream_t st) {
+                      float* dscale, float* ws, hipStream_t st) {
   const um_cat_src& s0 = *src;
   CatSrc s{s0.ptr, s0.scale, s0.C, s0.ld, s0.op, s0.coff, s0.dtype, s0.h, s0.w};
   UM_CHECK_ARG(ldg % 8 == 0, "um_concat_bwd_src: ldg %% 8");
@@ -616,39 +650,47 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
   const bool vec = (s.C % 8 == 0) && (s.coff % 8 == 0) && (ldd % 8 == 0 || !dsrc) &&
                    (s.ld % 8 == 0 || !dscale);
   const int chunk = bwd_chunk(P, N);
+  const int nblk = ceil_div(P, chunk);
+  UM_CHECK_ARG(!dscale || ws, "um_concat_bwd_src: gate gradient needs the workspace");
+  float* parts = dscale ? ws : nullptr;
   if (!vec) {
-    dim3 grid(ceil_div(P, chunk), 1, N);
+    dim3 grid(nblk, 1, N);
 #define UM_CAT_SCALAR(T_, OP_)                                                               \
     hipLaunchKernelGGL((cat_bwd_scalar_kernel<T_, OP_>), grid, dim3(256), 0, st, (const T_*)g, \
-                       ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, dscale, chunk)
+                       ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, parts, chunk)
     if (dtype == UM_BF16) {
       if (s.op == UM_CAT_COPY) UM_CAT_SCALAR(bf16_t, UM_CAT_COPY); else UM_CAT_SCALAR(bf16_t, UM_CAT_UP2);
     } else {
       if (s.op == UM_CAT_COPY) UM_CAT_SCALAR(float, UM_CAT_COPY); else UM_CAT_SCALAR(float, UM_CAT_UP2);
     }
 #undef UM_CAT_SCALAR
-    UM_LAUNCH_CHECK();
-    return UM_OK;
-  }
-  dim3 grid(ceil_div(P, chunk), 1, N);
-  if (s.op == UM_CAT_COPY) {
-    if (dtype == UM_BF16)
-      hipLaunchKernelGGL((cat_bwd_kernel<bf16_t, UM_CAT_COPY>), grid, dim3(256), 0, st,
-                         (const bf16_t*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
-                         accumulate, dscale, chunk);
-    else
-      hipLaunchKernelGGL((cat_bwd_kernel<float, UM_CAT_COPY>), grid, dim3(256), 0, st,
-                         (const float*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate,
-                         dscale, chunk);
   } else {
-    if (dtype == UM_BF16)
-      hipLaunchKernelGGL((cat_bwd_kernel<bf16_t, UM_CAT_UP2>), grid, dim3(256), 0, st,
-                         (const bf16_t*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
-                         accumulate, dscale, chunk);
-    else
-      hipLaunchKernelGGL((cat_bwd_kernel<float, UM_CAT_UP2>), grid, dim3(256), 0, st,
-                         (const float*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate,
-                         dscale, chunk);
+    dim3 grid(nblk, 1, N);
+    if (s.op == UM_CAT_COPY) {
+      if (dtype == UM_BF16)
+        hipLaunchKernelGGL((cat_bwd_kernel<bf16_t, UM_CAT_COPY>), grid, dim3(256), 0, st,
+                           (const bf16_t*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
+                           accumulate, parts, chunk);
+      else
+        hipLaunchKernelGGL((cat_bwd_kernel<float, UM_CAT_COPY>), grid, dim3(256), 0, st,
+                           (const float*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
+                           accumulate, parts, chunk);
+    } else {
+      if (dtype == UM_BF16)
+        hipLaunchKernelGGL((cat_bwd_kernel<bf16_t, UM_CAT_UP2>), grid, dim3(256), 0, st,
+                           (const bf16_t*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
+                           accumulate, parts, chunk);
+      else
+        hipLaunchKernelGGL((cat_bwd_kernel<float, UM_CAT_UP2>), grid, dim3(256), 0, st,
+                           (const float*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
+                           accumulate, parts, chunk);
+    }
+  }
+  if (dscale) {  // per-block partials -> dscale (+=)
+    int cl = 1;
+    while (cl < s.C && cl < 64) cl <<= 1;
+    hipLaunchKernelGGL(parts_accum_kernel, dim3(ceil_div(s.C, cl), N), dim3(256), 0, st, parts,
+                       nblk, s.C, dscale, cl);
   }
   UM_LAUNCH_CHECK();
   return UM_OK;

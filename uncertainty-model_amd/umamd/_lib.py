@@ -75,7 +75,8 @@ _SIG = {
     'um_attn_bwd': (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P, _I, _P, _P, _P,
                          _P, 's']),
     'um_concat_build': (_I, [_I, _I, _I, _I, _P, _I, _I, _I, _P, 's']),
-    'um_concat_bwd_src': (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _I, _P, 's']),
+    'um_concat_bwd_ws': (_L, [_I, _I, _I, _I]),
+    'um_concat_bwd_src': (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _I, _P, _P, 's']),
     'um_channel_mean': (_I, [_I, _I, _L, _I, _P, _I, _P, 's']),
     'um_se_mlp_fwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, 's']),
     'um_se_mlp_bwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, 's']),

@@ -510,8 +510,12 @@ class ConcatFn(torch.autograd.Function):
             dt_ = torch.empty_like(t) if need_t else None
             dg = torch.zeros_like(gate) if need_g else None
             if need_t or need_g:
+                ws = None
+                if need_g:
+                    nws = query('um_concat_bwd_ws', N, s.h, s.w, s.C)
+                    ws = torch.empty((nws,), dtype=torch.float32, device=g.device)
                 call('um_concat_bwd_src', L.dtype_code(dtype), N, H, W, ptr(g), Ctot,
-                     _ct.byref(s), ptr(dt_), t.shape[-1], _dt(t), 0, ptr(dg))
+                     _ct.byref(s), ptr(dt_), t.shape[-1], _dt(t), 0, ptr(dg), ptr(ws))
             grads.append(dt_)
             if gate is not None:
                 grads.append(dg)
