@@ -307,6 +307,11 @@ def test_conv_large(dtype, case):
     (48, 32, 3, 1, 'reflect', 10, 36),
     (32, 8, 3, 1, 'reflect', 7, 64),
     (64, 128, 3, 1, 'reflect', 6, 33),
+    # transposed-read implicit GEMM (K > 32, not halo-tiled)
+    (168, 128, 3, 1, 'reflect', 8, 16),
+    (256, 512, 3, 1, 'zero', 4, 8),
+    (32, 96, 1, 1, 'zero', 12, 40),
+    (128, 256, 3, 2, 'zero', 9, 17),
 ])
 def test_wgrad(case):
     from umamd import functional as U

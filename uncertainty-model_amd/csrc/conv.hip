@@ -23,6 +23,7 @@
 #include "common.h"
 #include "igemm.h"
 #include "wgrad_halo.h"
+#include "wgrad_tr.h"
 
 namespace {
 
@@ -861,11 +862,12 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
 
 static int wgrad_bm(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
 
-static int generic_wgrad_splits(int M, int K, int RRC) {
-  // tiles of the bf16 kernel (the f32 kernel uses 64x64 tiles; same split count)
-  const long tiles = (long)ceil_div(K, wgrad_bm(K)) * ceil_div(RRC, 128);
+static int generic_wgrad_splits(int M, int K, int RRC, bool tr) {
+  // tiles of the bf16 kernels (the f32 kernel uses 64x64 tiles; same split count)
+  const int bm = tr ? umamd::wgrad_tr_bm(K) : wgrad_bm(K);
+  const long tiles = (long)ceil_div(K, bm) * ceil_div(RRC, 128);
   long splits = (768 + tiles - 1) / tiles;
-  const long max_by_m = (M + 1023) / 1024;  // >= 1024 pixels per split
+  const long max_by_m = (M + 255) / 256;  // >= 256 pixels per split
   if (splits > max_by_m) splits = max_by_m;
   const long max_by_bytes = (32l << 20) / ((long)K * RRC * 4);  // <= 32 MB of slabs
   if (splits > max_by_bytes) splits = max_by_bytes;
@@ -880,7 +882,7 @@ int um_conv_wgrad_splits(int dtype, int N, int H, int W, int C, int ldx, int K, 
                                        pad_mode == UM_PAD_REFLECT, P, Q, ldy);
     if (h > 0) return h;
   }
-  return generic_wgrad_splits(N * P * Q, K, R * R * C);
+  return generic_wgrad_splits(N * P * Q, K, R * R * C, dtype == UM_BF16 && K > 32);
 }
 
 int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* x, int K, int R,
@@ -899,6 +901,11 @@ int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* 
       return UM_OK;
     umamd::set_error("um_conv2d_wgrad: halo kernel launch failed");
     return UM_ERR_HIP;
+  }
+  if (dtype == UM_BF16 && K > 32) {
+    UM_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0, "um_conv2d_wgrad: ld %% 8");
+    return umamd::wgrad_tr_run(x, N, H, W, C, ldx, K, R, stride, pad, pad_mode == UM_PAD_REFLECT,
+                               P, Q, dy, ldy, slabs, splits, st);
   }
   WgradArgs a{};
   a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx; a.K = K; a.R = R; a.stride = stride;
