@@ -97,6 +97,26 @@ int um_pack_weight_seg(int dtype, const float* w, int K, int Creal, int R, int C
                        void* wT, int ldT, int nseg, const int* src0, const int* dst0,
                        const int* len, hipStream_t stream);
 
+/* Batched repack of many conv weights in ONE launch (the per-step weight
+ * refresh of every conv in the model).  Each descriptor is one
+ * um_pack_weight_seg call; a descriptor covers um_pack_tiles(K, C, R)
+ * workgroups, numbered from `block0`;
+ * blk2desc[b] (device int array, nblocks entries) names the descriptor of
+ * workgroup b.  `table` and `blk2desc` are device memory (caller-owned). */
+#define UM_PACK_MAXSEG 4
+typedef struct {
+  const float* w;   /* [K][Creal][R][R] f32 */
+  void* wf;         /* [K][R][R][C] (nullable) */
+  void* wT;         /* [C][R][R][ldT] (nullable; column offset applied) */
+  int K, Creal, R, C, ldT, block0;
+  int nseg, src0[UM_PACK_MAXSEG], dst0[UM_PACK_MAXSEG], len[UM_PACK_MAXSEG];
+} um_pack_desc;
+int um_pack_batch(int dtype, const um_pack_desc* table, int ndesc, const int* blk2desc,
+                  int nblocks, hipStream_t stream);
+int um_pack_tiles(int K, int C, int R);
+/* sizeof(um_pack_desc), for bindings that build the table */
+int um_pack_desc_size(void);
+
 /* repack f32 NCHW weight [K][Creal][R][R] -> wf [K][R][R][C] (row stride ldf
  * elements) and wT [C][R][R][ldT] (column offset applied by the caller); C >= Creal, zero fill */
 int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C,
@@ -106,9 +126,12 @@ int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C,
 int um_colsum_parts(int M);
 int um_colsum(int dtype, int M, int C, int ld, const void* y, float* partials,
               hipStream_t stream);
-/* out[c] (+)= sum_p partials[p][c] (+ optional second partial set) */
+/* out[c] (+)= sum_p partials[p][c*1] (row stride `stride`), one launch;
+ * ws: um_colred_ws(parts, C, 1) bytes (f64 slab rows of the per-workgroup sums) */
 int um_reduce_rows(const float* partials, int parts, int C, int stride, float* out,
-                   int accumulate, hipStream_t stream);
+                   int accumulate, double* ws, hipStream_t stream);
+/* workspace bytes of the one-launch column reductions (nv values per channel) */
+long um_colred_ws(int nparts, int C, int nv);
 
 /* ------------------------------------------------------------------ BN ---
  * Training-mode nn.BatchNorm2d + nn.ELU, reference model/layers/encoder.py:43-44,
@@ -116,7 +139,22 @@ int um_reduce_rows(const float* partials, int parts, int C, int stride, float* o
  * all-reduces the f64 per-channel sums between the phases
  * (reference parallel_main.py:157).
  */
-int um_bn_stats_reduce(const float* parts, int nparts, int C, double* out, hipStream_t stream);
+/* f64 per-channel sums of [nparts][C][2] partials (the SyncBN path all-reduces them
+ * before um_bn_coeffs / um_bn_bwd_coeffs); ws: um_colred_ws(nparts, C, 2) bytes */
+int um_bn_stats_reduce(const float* parts, int nparts, int C, double* out, double* ws,
+                       hipStream_t stream);
+/* single-process BN: reduce the forward partials AND compute the coefficients
+ * (+ running statistics) in one launch (um_bn_stats_reduce + um_bn_coeffs) */
+int um_bn_stats_coeffs(const float* parts, int nparts, int C, double* ws, double count,
+                       const float* gamma, const float* beta, float eps, float momentum,
+                       float* running_mean, float* running_var, long long* num_batches_tracked,
+                       float* mean, float* invstd, float* scale, float* shift,
+                       hipStream_t stream);
+/* single-process BN backward: reduce the bwd partials and compute k1..k3,
+ * dgamma, dbeta in one launch (um_bn_stats_reduce + um_bn_bwd_coeffs) */
+int um_bn_bwd_stats_coeffs(const float* parts, int nparts, int C, double* ws, double count,
+                           const float* gamma, const float* invstd, float* dgamma,
+                           float* dbeta, float* k1, float* k2, float* k3, hipStream_t stream);
 int um_bn_coeffs(const double* stats, double count, int C, const float* gamma,
                  const float* beta, float eps, float momentum, float* running_mean,
                  float* running_var, long long* num_batches_tracked, float* mean,

@@ -40,6 +40,10 @@ def test_host_queries_without_gpu():
     assert query('um_conv_fwd_ws', 1, 8, 8, 16, 512, 3, 512) > 0  # deep layer: split-K
     assert query('um_conv_fwd_ws', 1, 8, 128, 256, 32, 7, 32) == 0
     assert query('um_adam_chunk') == 4096
+    from umamd.packer import PackDesc
+    import ctypes
+    assert query('um_pack_desc_size') == ctypes.sizeof(PackDesc)
+    assert query('um_colred_ws', 1000, 32, 2) > 0
 
 
 def test_kernel_call_fails_loudly_on_cpu_tensor():

@@ -259,3 +259,38 @@ def test_train_step_bf16_loss_delta():
     # ~1.3e-2 mean relative sigma deviation of bf16 operands (measured 1.6e-2)
     assert abs(res['bf16'][0] / res['fp32'][0] - 1) < 1e-2
     assert abs(res['bf16'][1] / res['fp32'][1] - 1) < 3e-2
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_batched_weight_pack_matches_per_site_pack(dtype):
+    """um_pack_batch (one launch for every conv weight, used from the 2nd
+    forward on) must leave exactly the buffers the per-site packing writes."""
+    from umamd.packer import _pack_one
+    cfg = _cfg()
+    m = _model(cfg, dtype).train()
+    x = torch.rand(2, 3, 64, 128, device=DEV)
+    with torch.no_grad():
+        m(x, 0.3)
+        pk = m._packer
+        assert pk.descs and not pk.batched
+        # perturb the parameters so a stale buffer would show, then refresh by batch
+        for p in m.parameters():
+            p.add_(0.01 * torch.randn_like(p))
+        m(x, 0.3)
+        assert pk.batched and not pk.dirty
+        torch.cuda.synchronize()
+        checked = 0
+        for key, (f, t) in pk.entries.items():
+            if key[0] != 'w':
+                continue
+            w = next(p for p in m.parameters() if p.data_ptr() == key[1])
+            Cp, dt, ldT, segs = key[3], key[4], key[5], key[6]
+            f2 = torch.empty_like(f) if f is not None else None
+            t2 = torch.zeros_like(t) if t is not None else None
+            _pack_one(w.detach(), f2, t2, Cp, ldT, list(segs) if segs else None, dt)
+            if f is not None:
+                assert torch.equal(f, f2), key
+            if t is not None:
+                assert torch.equal(t, t2), key
+            checked += 1
+        assert checked >= 40

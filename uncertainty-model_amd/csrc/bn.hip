@@ -19,36 +19,6 @@
 
 namespace {
 
-__global__ void stats_reduce_kernel(const float* __restrict__ parts, int nparts, int C,
-                                    double* __restrict__ out) {
-  // out[c][0..1] = sum_p parts[p][c][0..1]; one wave per channel
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  int p = lane;
-  for (; p + 64 < nparts; p += 128) {  // two rows in flight per lane
-    const float2 a = *reinterpret_cast<const float2*>(parts + ((long)p * C + c) * 2);
-    const float2 b = *reinterpret_cast<const float2*>(parts + ((long)(p + 64) * C + c) * 2);
-    s += (double)a.x + (double)b.x;
-    q += (double)a.y + (double)b.y;
-  }
-  for (; p < nparts; p += 64) {
-    const float2 a = *reinterpret_cast<const float2*>(parts + ((long)p * C + c) * 2);
-    s += a.x;
-    q += a.y;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    s += __shfl_xor(s, o, 64);
-    q += __shfl_xor(q, o, 64);
-  }
-  if (lane == 0) {
-    out[c * 2] = s;
-    out[c * 2 + 1] = q;
-  }
-}
-
 __global__ void coeffs_kernel(const double* __restrict__ st, double count, int C,
                               const float* __restrict__ gamma, const float* __restrict__ beta,
                               float eps, float momentum, float* running_mean, float* running_var,
@@ -249,13 +219,6 @@ inline int grid_for(long n) {
 }  // namespace
 
 extern "C" {
-
-int um_bn_stats_reduce(const float* parts, int nparts, int C, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3(ceil_div(C, 4)), dim3(256), 0, st, parts, nparts,
-                     C, out);
-  UM_LAUNCH_CHECK();
-  return UM_OK;
-}
 
 int um_bn_coeffs(const double* stats, double count, int C, const float* gamma, const float* beta,
                  float eps, float momentum, float* running_mean, float* running_var,

@@ -754,40 +754,12 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ y, in
 // out[c] (+)= sum_r p[r*stride + c]: block = cl channel lanes (cl = C up to
 // 64, power of two) x 256/cl row lanes, 8 independent accumulators per
 // thread, f64 lane combine
-__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* __restrict__ p, int parts,
-                                                          int C, int stride,
-                                                          float* __restrict__ out,
-                                                          int accumulate, int cl) {
-  __shared__ double red[256];
-  const int lanes = 256 / cl;
-  const int c = blockIdx.x * cl + (threadIdx.x % cl);
-  const int lane = threadIdx.x / cl;
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (c < C) {
-    int r = lane;
-    for (; r + 7 * lanes < parts; r += 8 * lanes)
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s[u] += p[(long)(r + u * lanes) * stride + c];
-    for (int u = 0; r < parts; r += lanes, ++u) s[u & 7] += p[(long)r * stride + c];
-  }
-  double t = 0.0;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) t += (double)s[u];
-  red[threadIdx.x] = t;
-  __syncthreads();
-  if (lane == 0 && c < C) {
-    for (int q = 1; q < lanes; ++q) t += red[q * cl + (threadIdx.x % cl)];
-    out[c] = accumulate ? out[c] + (float)t : (float)t;
-  }
-}
-
 }  // namespace
 
 extern "C" {
 
 int um_conv_stats_parts(int M, int K) {
-  (void)K;
-  return ceil_div(M, STATS_BM);  // = igemm's STATS_ROWS blocks
+  return ceil_div(M, umamd::igemm_stats_rows(M, K));
 }
 
 long um_conv_fwd_ws(int dtype, int N, int P, int Q, int K, int R, int C) {
@@ -1005,14 +977,88 @@ int um_colsum(int dtype, int M, int C, int ld, const void* y, float* parts, hipS
   return UM_OK;
 }
 
-int um_reduce_rows(const float* partials, int parts, int C, int stride, float* out, int accumulate,
-                   hipStream_t st) {
-  int cl = 1;
-  while (cl < C && cl < 64) cl <<= 1;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(ceil_div(C, cl)), dim3(256), 0, st, partials, parts,
-                     C, stride, out, accumulate, cl);
+}  // extern "C"
+
+// ------------------------------------------------------- batched repack --
+// One launch refreshes the packed copies of every conv weight (see
+// um_pack_batch in umamd.h).  Workgroup = 32 output channels (k) x ct(R)
+// input channels (c) x all R*R taps: the source block w[k][c0..c0+ct)[taps]
+// is one contiguous run per k (coalesced f32 reads), staged in LDS, then
+// written as wf rows (c contiguous) and, transposed, as wT rows (k
+// contiguous, 64-byte segments).
+namespace {
+
+constexpr int PK = 32;  // k per workgroup
+__host__ __device__ constexpr int pack_ct(int R) {  // c per workgroup: 32*ct*R*R <= 8192
+  return R <= 1 ? 64 : (R <= 3 ? 16 : (R <= 5 ? 8 : 4));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) pack_batch_kernel(const um_pack_desc* __restrict__ table,
+                                                         const int* __restrict__ blk2desc) {
+  __shared__ float tile[8192 + 64];
+  const um_pack_desc d = table[blk2desc[blockIdx.x]];
+  const int t = blockIdx.x - d.block0;
+  const int RR = d.R * d.R, CT = pack_ct(d.R);
+  const int nct = (d.C + CT - 1) / CT;
+  const int k0 = (t / nct) * PK, c0 = (t % nct) * CT;
+  const int per_k = CT * RR;  // staged values per k row
+  const int ldt = per_k + 1;  // odd LDS row stride
+  const int n = PK * per_k;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int kk = i / per_k, rem = i - kk * per_k;
+    const int cc = rem / RR, tap = rem - cc * RR;
+    const int k = k0 + kk, c = c0 + cc;
+    float v = 0.f;
+    if (k < d.K && c < d.C) {
+      int cs = -1;
+      if (d.nseg <= 0) cs = c < d.Creal ? c : -1;
+      else
+        for (int g = 0; g < d.nseg; ++g)
+          if (c >= d.dst0[g] && c < d.dst0[g] + d.len[g]) cs = d.src0[g] + c - d.dst0[g];
+      if (cs >= 0) v = d.w[((long)k * d.Creal + cs) * RR + tap];
+    }
+    tile[kk * ldt + cc * RR + tap] = v;
+  }
+  __syncthreads();
+  T* wf = reinterpret_cast<T*>(d.wf);
+  T* wT = reinterpret_cast<T*>(d.wT);
+  if (wf)
+    for (int i = threadIdx.x; i < n; i += 256) {  // (kk, tap, cc): c fastest
+      const int kk = i / per_k, rem = i - kk * per_k;
+      const int tap = rem / CT, cc = rem - tap * CT;
+      const int k = k0 + kk, c = c0 + cc;
+      if (k < d.K && c < d.C)
+        wf[((long)k * RR + tap) * d.C + c] = from_f32<T>(tile[kk * ldt + cc * RR + tap]);
+    }
+  if (wT)
+    for (int i = threadIdx.x; i < n; i += 256) {  // (cc, tap, kk): k fastest
+      const int cc = i / (RR * PK), rem = i - cc * (RR * PK);
+      const int tap = rem / PK, kk = rem - tap * PK;
+      const int k = k0 + kk, c = c0 + cc;
+      if (k < d.K && c < d.C)
+        wT[((long)c * RR + tap) * d.ldT + k] = from_f32<T>(tile[kk * ldt + cc * RR + tap]);
+    }
+}
+
+}  // namespace
+
+extern "C" int um_pack_tiles(int K, int C, int R) {
+  return ceil_div(K, PK) * ceil_div(C, pack_ct(R));
+}
+
+extern "C" int um_pack_batch(int dtype, const um_pack_desc* table, int ndesc,
+                             const int* blk2desc, int nblocks, hipStream_t st) {
+  UM_CHECK_ARG(table != nullptr && blk2desc != nullptr && ndesc > 0, "um_pack_batch: table");
+  if (nblocks <= 0) return UM_OK;
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(pack_batch_kernel<bf16_t>, dim3(nblocks), dim3(256), 0, st, table,
+                       blk2desc);
+  else
+    hipLaunchKernelGGL(pack_batch_kernel<float>, dim3(nblocks), dim3(256), 0, st, table,
+                       blk2desc);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
 
-}  // extern "C"
+extern "C" int um_pack_desc_size(void) { return (int)sizeof(um_pack_desc); }

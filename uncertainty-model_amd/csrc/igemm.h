@@ -28,7 +28,11 @@ struct IgArgs {
   const void* residual;
   int ldr;
   float* stats;
+  int stats_rows;  // set by igemm_run (igemm_stats_rows)
 };
+
+// rows per BN partial-statistics row of a stats epilogue (M, NC of the GEMM)
+int igemm_stats_rows(int M, int NC);
 
 // workspace bytes the split-K heuristic wants for this shape (0: no split)
 long igemm_ws_bytes(int dtype, int M, int NC, int R, int ach);

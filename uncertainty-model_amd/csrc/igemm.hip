@@ -27,6 +27,7 @@
 // [split][M][NC] and splitk_epilogue_kernel sums them and applies the
 // epilogue (bias, BN partial statistics, residual, sigmoid-scale).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "igemm.h"
@@ -35,7 +36,8 @@ namespace {
 
 using umamd::IgArgs;
 
-constexpr int STATS_ROWS = 128;  // BN partial-statistics row block (um_conv_stats_parts)
+// BN partial-statistics row block (um_conv_stats_parts): a.stats_rows, 128 or
+// 64 (the 64x64-tile plans); BM is a multiple of it.
 
 // ------------------------------------------------------------ LDS images --
 template <typename T, int BK> struct Img;
@@ -176,7 +178,6 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
   constexpr int A_PER = A_CH / 256;
   constexpr int B_PER = (B_CH + 255) / 256;
   static_assert(WM * WN == 4, "4 waves");
-  static_assert(BM % STATS_ROWS == 0 || STATS_ROWS % BM == 0, "stats rows");
 
   __shared__ __attribute__((aligned(16))) T sA[2][BM * I::ROW];
   __shared__ __attribute__((aligned(16))) T sB[2][BN * I::ROW];
@@ -357,25 +358,26 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
       }
     }
     __syncthreads();
-    // stats row blocks of STATS_ROWS rows: waves of rows [w*BM/WM, (w+1)*BM/WM)
+    // stats row blocks of SR rows (BM % SR == 0): waves of rows [w*BM/WM, (w+1)*BM/WM)
     constexpr int WROWS = BM / WM;
-    constexpr int NSB = BM >= STATS_ROWS ? BM / STATS_ROWS : 1;
+    const int SR = a.stats_rows;
+    const int NSB = BM / SR;
     for (int c = tid; c < BN * NSB; c += 256) {
       const int col = c % BN, sb = c / BN;
       const int n = bn + col;
-      if (n >= a.NC || bm + sb * STATS_ROWS >= a.M) continue;
+      if (n >= a.NC || bm + sb * SR >= a.M) continue;
       float sm = 0.f, sq = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w)
-        if ((w * WROWS) / STATS_ROWS == sb) { sm += sStat[w][col][0]; sq += sStat[w][col][1]; }
-      float* o = a.stats + ((long)(bm / STATS_ROWS + sb) * a.NC + n) * 2;
+        if ((w * WROWS) / SR == sb) { sm += sStat[w][col][0]; sq += sStat[w][col][1]; }
+      float* o = a.stats + ((long)(bm / SR + sb) * a.NC + n) * 2;
       o[0] = sm;
       o[1] = sq;
     }
   }
 }
 
-// sum the split-K partials and apply the epilogue.  Block = STATS_ROWS rows x
+// sum the split-K partials and apply the epilogue.  Block = a.stats_rows rows x
 // 64 columns: thread (g, lane) owns columns 4g..4g+3 and rows lane, lane+16, ...
 constexpr int EPI_COLS = 64;
 template <typename T>
@@ -384,8 +386,8 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const fl
   __shared__ float red[16][16][8];
   const int g = threadIdx.x & 15, lane = threadIdx.x >> 4;
   const int n = blockIdx.y * EPI_COLS + g * 4;  // NC % 4 == 0 (host-checked)
-  const long m0 = (long)blockIdx.x * STATS_ROWS;
-  const long m1 = min((long)a.M, m0 + STATS_ROWS);
+  const long m0 = (long)blockIdx.x * a.stats_rows;
+  const long m1 = min((long)a.M, m0 + a.stats_rows);
   const long zs = (long)a.M * a.NC;
   const bool act = n < a.NC;
   float sm[4] = {0, 0, 0, 0}, sq[4] = {0, 0, 0, 0};
@@ -446,13 +448,46 @@ struct Plan {
   int bk, bm, bn, wm, wn, splits, steps, per;
 };
 
+// tuning knobs (read once; UMAMD_IG_* environment variables for sweeps)
+struct Knobs {
+  int small, small_tiles, split_below, split_target, split_minsteps;
+  Knobs() {
+    auto env = [](const char* n, int d) {
+      const char* v = getenv(n);
+      return v ? atoi(v) : d;
+    };
+    small = env("UMAMD_IG_SMALL", 1);
+    small_tiles = env("UMAMD_IG_SMALL_TILES", 256);
+    split_below = env("UMAMD_IG_SPLIT_BELOW", 160);
+    split_target = env("UMAMD_IG_SPLIT_TARGET", 320);
+    split_minsteps = env("UMAMD_IG_SPLIT_MINSTEPS", 8);
+  }
+};
+const Knobs& knobs() {
+  static const Knobs k;
+  return k;
+}
+
+// Deep layers (few 128x128 tiles) use 64x64 tiles: 4x the workgroups, more of
+// them per CU (32 KB of LDS each), so more loads in flight per CU instead of
+// a split-K round trip through an f32 workspace.  Depends on (M, NC) only so
+// um_conv_stats_parts can follow it.
+bool small_tiles(int M, int NC) {
+  const Knobs& k = knobs();
+  return k.small && NC > 64 && (long)ceil_div(M, 128) * ceil_div(NC, 128) < k.small_tiles;
+}
+
 Plan make_plan(int dtype, int M, int NC, int R, int ach, long ws_bytes) {
+  const Knobs& kn = knobs();
   Plan p{};
   p.bk = 32;
   if (NC <= 16) { p.bm = 256; p.bn = 16; p.wm = 4; p.wn = 1; }
   else if (NC <= 32) { p.bm = 256; p.bn = 32; p.wm = 4; p.wn = 1; }
   else if (NC <= 64) { p.bm = 256; p.bn = 64; p.wm = 4; p.wn = 1; }
-  else {
+  else if (small_tiles(M, NC)) {
+    p.bm = 64; p.bn = 64; p.wm = 2; p.wn = 2;
+    if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;
+  } else {
     p.bm = 128; p.bn = 128; p.wm = 2; p.wn = 2;
     if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;  // 64 KB of LDS: 2 blocks/CU
   }
@@ -462,9 +497,9 @@ Plan make_plan(int dtype, int M, int NC, int R, int ach, long ws_bytes) {
   // ~320 blocks, >= 8 k-steps per split and <= 32 MB of partials.
   const long tiles = (long)ceil_div(M, p.bm) * ceil_div(NC, p.bn);
   p.splits = 1;
-  if (tiles < 160 && NC % 4 == 0) {
-    long sp = (320 + tiles - 1) / tiles;
-    sp = std::min<long>(sp, p.steps / 8);
+  if (tiles < kn.split_below && NC % 4 == 0) {
+    long sp = (kn.split_target + tiles - 1) / tiles;
+    sp = std::min<long>(sp, p.steps / kn.split_minsteps);
     sp = std::min<long>(sp, (32l << 20) / ((long)M * NC * 4));
     if (ws_bytes >= 0) sp = std::min<long>(sp, ws_bytes / ((long)M * NC * 4));
     if (sp >= 2) p.splits = (int)sp;
@@ -481,7 +516,7 @@ int launch(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
     hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, true>), dim3(ntm * ntn, 1, p.splits),
                        dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
     hipLaunchKernelGGL(splitk_epilogue_kernel<T>,
-                       dim3(ceil_div(a.M, STATS_ROWS), ceil_div(a.NC, EPI_COLS)), dim3(256), 0, st,
+                       dim3(ceil_div(a.M, a.stats_rows), ceil_div(a.NC, EPI_COLS)), dim3(256), 0, st,
                        a, (const float*)ws, p.splits);
   } else {
     hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, false>), dim3(ntm * ntn, 1, 1),
@@ -495,7 +530,12 @@ template <typename T>
 int dispatch_tiles(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
   if (p.bn == 16) return launch<T, 32, 256, 16, 4, 1>(a, p, ws, st);
   if (p.bn == 32) return launch<T, 32, 256, 32, 4, 1>(a, p, ws, st);
-  if (p.bn == 64) return launch<T, 32, 256, 64, 4, 1>(a, p, ws, st);
+  if (p.bn == 64 && p.bm == 256) return launch<T, 32, 256, 64, 4, 1>(a, p, ws, st);
+  if (p.bm == 64) {
+    if constexpr (sizeof(T) == 2)
+      if (p.bk == 64) return launch<T, 64, 64, 64, 2, 2>(a, p, ws, st);
+    return launch<T, 32, 64, 64, 2, 2>(a, p, ws, st);
+  }
   if constexpr (sizeof(T) == 2)
     if (p.bk == 64) return launch<T, 64, 128, 128, 2, 2>(a, p, ws, st);
   return launch<T, 32, 128, 128, 2, 2>(a, p, ws, st);
@@ -510,8 +550,12 @@ long igemm_ws_bytes(int dtype, int M, int NC, int R, int ach) {
   return p.splits > 1 ? (long)p.splits * M * NC * 4 : 0;
 }
 
-int igemm_run(int dtype, const IgArgs& a, float* ws, long ws_bytes, hipStream_t st) {
-  if (a.M == 0) return UM_OK;
+int igemm_stats_rows(int M, int NC) { return small_tiles(M, NC) ? 64 : 128; }
+
+int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream_t st) {
+  if (a_in.M == 0) return UM_OK;
+  IgArgs a = a_in;
+  a.stats_rows = igemm_stats_rows(a.M, a.NC);
   const Plan p = make_plan(dtype, a.M, a.NC, a.R, a.ach, ws ? ws_bytes : 0);
   if (dtype == UM_BF16) return dispatch_tiles<bf16_t>(a, p, ws, st);
   return dispatch_tiles<float>(a, p, ws, st);

@@ -256,17 +256,28 @@ struct FinalP {
 };
 
 // out: [0] disp_loss [1] error_loss [2] wssim [3] consistency [4] smoothness [5] error
-__global__ void finalize_kernel(FinalP f, float* __restrict__ out) {
+__global__ void __launch_bounds__(1024) finalize_kernel(FinalP f, float* __restrict__ out) {
+  // 16 waves; wave w sums (scale, term) pairs w and w + 16 over the partial rows
   __shared__ double tot[4][6];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (wave < f.nscales) {
-    for (int k = 0; k < 6; ++k) {
-      double t = 0.0;
-      for (int p = lane; p < f.nparts[wave]; p += 64) t += f.parts[wave][(long)p * 8 + k];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-      if (lane == 0) tot[wave][k] = t;
+  for (int pr = wave; pr < 4 * 6; pr += 16) {
+    const int sc = pr / 6, k = pr % 6;
+    if (sc >= f.nscales) continue;
+    const float* q = f.parts[sc] + k;
+    const int np = f.nparts[sc];
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+    int p = lane;
+    for (; p + 192 < np; p += 256) {
+      t0 += q[(long)p * 8];
+      t1 += q[(long)(p + 64) * 8];
+      t2 += q[(long)(p + 128) * 8];
+      t3 += q[(long)(p + 192) * 8];
     }
+    for (; p < np; p += 64) t0 += q[(long)p * 8];
+    double t = (t0 + t1) + (t2 + t3);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) tot[sc][k] = t;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -590,7 +601,7 @@ int um_loss_finalize(int nscales, const float* const* parts, const int* nparts,
   f.nscales = nscales;
   f.w_wssim = w_wssim; f.w_cons = w_cons; f.w_smooth = w_smooth; f.w_err = w_err;
   f.esw = esw; f.ecw = ecw; f.loss_type = loss_type;
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, st, f, out);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, st, f, out);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -13,6 +13,7 @@ from torch import Tensor
 
 import umamd
 from umamd import functional as U
+from umamd import packer as P
 
 from .decoder import DepthDecoder, DecoderOut
 from .encoder import RandomEncoder
@@ -24,14 +25,16 @@ class RandomlyConnectedModel(nn.Module):
         self.encoder = RandomEncoder(**encoder)
         self.decoder = DepthDecoder(**decoder)
         self.compute_dtype = umamd.resolve_dtype(dtype)
+        self._packer = P.WeightPacker()  # packed conv weights, one refresh launch per forward
 
     def forward(self, image: Tensor, scale: float = 1) -> DecoderOut:
         _, _, h, w = image.shape
         if h % 32 or w % 32:
             raise ValueError(f'image size {h}x{w}: height and width must be multiples of 32')
         x = U.image_to_nhwc(image, self.compute_dtype)
-        feats = self.encoder._fwd(x)
-        disps = self.decoder._fwd(x, *feats, scale=float(scale))
+        with P.scope(self._packer):
+            feats = self.encoder._fwd(x)
+            disps = self.decoder._fwd(x, *feats, scale=float(scale))
         disps = tuple(d.permute(0, 3, 1, 2) for d in disps)  # logical NCHW, NHWC memory
         return disps if self.training else disps[0]
 

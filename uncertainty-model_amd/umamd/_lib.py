@@ -47,12 +47,19 @@ _SIG = {
                              _P, _I, 's']),
     'um_conv_wgrad_reduce': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, 's']),
     'um_pack_weight': (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _I, 's']),
+    'um_pack_batch': (_I, [_I, _P, _I, _P, _I, 's']),
+    'um_pack_desc_size': (_I, []),
+    'um_pack_tiles': (_I, [_I, _I, _I]),
     'um_pack_weight_seg': (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P, 's']),
     'um_conv_wgrad_reduce_seg': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, 's']),
     'um_colsum_parts': (_I, [_I]),
     'um_colsum': (_I, [_I, _I, _I, _I, _P, _P, 's']),
-    'um_reduce_rows': (_I, [_P, _I, _I, _I, _P, _I, 's']),
-    'um_bn_stats_reduce': (_I, [_P, _I, _I, _P, 's']),
+    'um_reduce_rows': (_I, [_P, _I, _I, _I, _P, _I, _P, 's']),
+    'um_colred_ws': (_L, [_I, _I, _I]),
+    'um_bn_stats_reduce': (_I, [_P, _I, _I, _P, _P, 's']),
+    'um_bn_stats_coeffs': (_I, [_P, _I, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P,
+                                's']),
+    'um_bn_bwd_stats_coeffs': (_I, [_P, _I, _I, _P, _D, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_coeffs': (_I, [_P, _D, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, 's']),
     'um_bn_bwd_parts': (_I, [_L]),

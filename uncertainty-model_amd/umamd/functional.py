@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
+from . import packer as _packer
 from ._lib import call, ptr, query
 
 
@@ -51,6 +52,9 @@ def _pack(weight: torch.Tensor, Cp: int, dtype: torch.dtype, wf=True, wT=True, l
           segs=None):
     """Repack an NCHW f32 conv weight to [K][R][R][Cp] and [Cp][R][R][ldT];
     ``segs`` = [(ref_c0, packed_c0, len)] places input-channel ranges."""
+    pk = _packer.active()
+    if pk is not None:
+        return pk.pack(weight, Cp, dtype, wf=wf, wT=wT, ldT=ldT, segs=segs)
     K, Creal, R, _ = weight.shape
     ldT = ldT or K
     w = weight.detach()
@@ -123,6 +127,18 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
     return dw
 
 
+def _colred_ws(nparts, C, nv, device):
+    """f64 slab rows of the one-launch column reductions (um_colred_ws)"""
+    n = query('um_colred_ws', nparts, C, nv)
+    return torch.empty((max(n, 8) // 8,), dtype=torch.float64, device=device)
+
+
+def _reduce_rows(parts, nparts, C, out, accumulate=False):
+    call('um_reduce_rows', ptr(parts), nparts, C, C, ptr(out), int(accumulate),
+         ptr(_colred_ws(nparts, C, 1, parts.device)))
+    return out
+
+
 def _colsum(y, C):
     """sum over pixels of y[..., :C] -> f32 [C]"""
     M = y.numel() // y.shape[-1]
@@ -130,8 +146,7 @@ def _colsum(y, C):
     parts = torch.empty((parts_n, C), dtype=torch.float32, device=y.device)
     call('um_colsum', _dt(y), M, C, y.shape[-1], ptr(y), ptr(parts))
     out = torch.empty((C,), dtype=torch.float32, device=y.device)
-    call('um_reduce_rows', ptr(parts), parts_n, C, C, ptr(out), 0)
-    return out
+    return _reduce_rows(parts, parts_n, C, out)
 
 
 class BNSync:
@@ -159,17 +174,24 @@ def _bn_forward_coeffs(parts, nparts, K, count, bn, sync: BNSync, training: bool
     gamma = bn.weight if bn.affine else None
     beta = bn.bias if bn.affine else None
     if training or not bn.track_running_stats:
-        st = torch.empty((K, 2), dtype=torch.float64, device=device)
-        call('um_bn_stats_reduce', ptr(parts), nparts, K, ptr(st))
-        sync.all_reduce(st)
         upd = training and bn.track_running_stats and bn.running_mean is not None
         if upd and bn.momentum is None:
             raise NotImplementedError('BatchNorm momentum=None (cumulative average) is not supported')
-        call('um_bn_coeffs', ptr(st), float(count * sync.world), K, ptr(gamma), ptr(beta),
-             float(bn.eps), float(bn.momentum or 0.0),
-             ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
-             ptr(bn.num_batches_tracked) if upd and bn.num_batches_tracked is not None else None,
-             ptr(mean), ptr(invstd), ptr(scale), ptr(shift))
+        ws = _colred_ws(nparts, K, 2, device)
+        rs = (ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
+              ptr(bn.num_batches_tracked) if upd and bn.num_batches_tracked is not None else None)
+        if sync.world == 1:
+            # one launch: reduce the conv-epilogue partials and finish the coefficients
+            call('um_bn_stats_coeffs', ptr(parts), nparts, K, ptr(ws), float(count), ptr(gamma),
+                 ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs, ptr(mean),
+                 ptr(invstd), ptr(scale), ptr(shift))
+        else:
+            st = torch.empty((K, 2), dtype=torch.float64, device=device)
+            call('um_bn_stats_reduce', ptr(parts), nparts, K, ptr(st), ptr(ws))
+            sync.all_reduce(st)
+            call('um_bn_coeffs', ptr(st), float(count * sync.world), K, ptr(gamma), ptr(beta),
+                 float(bn.eps), float(bn.momentum or 0.0), *rs,
+                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift))
     else:
         # eval mode: normalise with the running statistics
         st = torch.stack([bn.running_mean.double(), (bn.running_var.double() + bn.running_mean.double() ** 2)], 1).contiguous()
@@ -281,18 +303,21 @@ class ConvBNELUFn(torch.autograd.Function):
             parts = torch.empty((nb, K, 2), dtype=torch.float32, device=dev)
             call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
                  ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(parts))
-            st = torch.empty((K, 2), dtype=torch.float64, device=dev)
-            call('um_bn_stats_reduce', ptr(parts), nb, K, ptr(st))
-            st_local = None
-            if ctx.sync is not None and ctx.sync.world > 1:
-                st_local = st.clone()
-                ctx.sync.all_reduce(st)
             world = ctx.sync.world if ctx.sync is not None else 1
             if gamma is not None:
                 dgamma = torch.empty(K, dtype=torch.float32, device=dev)
                 dbeta = torch.empty(K, dtype=torch.float32, device=dev)
-            call('um_bn_bwd_coeffs', ptr(st), float(M * world), K, ptr(gamma), ptr(invstd),
-                 ptr(st_local), ptr(dgamma), ptr(dbeta), 0, ptr(k1), ptr(k2), ptr(k3))
+            ws = _colred_ws(nb, K, 2, dev)
+            if world == 1:
+                call('um_bn_bwd_stats_coeffs', ptr(parts), nb, K, ptr(ws), float(M), ptr(gamma),
+                     ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(k1), ptr(k2), ptr(k3))
+            else:
+                st = torch.empty((K, 2), dtype=torch.float64, device=dev)
+                call('um_bn_stats_reduce', ptr(parts), nb, K, ptr(st), ptr(ws))
+                st_local = st.clone()
+                ctx.sync.all_reduce(st)
+                call('um_bn_bwd_coeffs', ptr(st), float(M * world), K, ptr(gamma), ptr(invstd),
+                     ptr(st_local), ptr(dgamma), ptr(dbeta), 0, ptr(k1), ptr(k2), ptr(k3))
         else:
             # no batch statistics (no BN, or BN in eval mode): dy = dz * scale
             k1.copy_(scale)
@@ -312,7 +337,7 @@ class ConvBNELUFn(torch.autograd.Function):
         dbias = None
         if need_b:
             dbias = torch.empty(K, dtype=torch.float32, device=dev)
-            call('um_reduce_rows', ptr(bparts), nbp, K, K, ptr(dbias), 0)
+            _reduce_rows(bparts, nbp, K, dbias)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _conv_dgrad(dy, wT, (N, H, W, Cp), K, R, spec.stride, spec.pad, spec.pad_mode,
@@ -399,13 +424,9 @@ class AttentionFn(torch.autograd.Function):
         S = H * W
         dt = x.dtype
         dev = x.device
-        wf = torch.empty((3 * C, 1, 1, C), dtype=dt, device=dev)
-        wT = torch.empty((C, 1, 1, 3 * C), dtype=dt, device=dev)
-        for i, wgt in enumerate((wk, wq, wv)):
-            # rows [iC, (i+1)C) of wf; columns [iC, (i+1)C) of wT (row stride 3C)
-            call('um_pack_weight', L.dtype_code(dt), ptr(wgt.detach().float().contiguous()), C,
-                 C, 1, C, wf[i * C].data_ptr(), wT.data_ptr() + i * C * wT.element_size(),
-                 3 * C)
+        pk = _packer.active() or _packer.WeightPacker()
+        # rows [iC, (i+1)C) of wf; columns [iC, (i+1)C) of wT (row stride 3C)
+        wf, wT = pk.pack_rows((wk, wq, wv), C, dt)
         bqkv = torch.cat([bk.detach(), bq.detach(), bv.detach()]).float().contiguous()
         qkv = _conv_fwd(x, wf, bqkv, 3 * C, 1, 1, 0, L.PAD_ZERO)
         kmax = torch.empty((N, C), dtype=torch.float32, device=dev)
