@@ -45,6 +45,10 @@ CONV_CASES = [
     (256, 512, 3, 1, 'zero', 4, 6),
     (128, 96, 3, 1, 'reflect', 6, 10),
     (64, 32, 5, 1, 'zero', 3, 5),
+    # stride-2 data gradient by parity classes: odd sizes, split-K classes
+    (64, 128, 3, 2, 'zero', 9, 11),
+    (256, 512, 3, 2, 'zero', 7, 9),
+    (32, 64, 5, 2, 'zero', 13, 15),
 ]
 
 

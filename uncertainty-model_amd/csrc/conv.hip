@@ -44,26 +44,6 @@ __device__ __forceinline__ int seg_src(const Segs& g, int c) {  // packed -> ref
 }
 constexpr int LDK = BK + 8;  // padded LDS row (elements)
 
-enum { MODE_FWD = 0, MODE_DGRAD = 1 };
-
-struct ConvArgs {
-  // "input" geometry of the GEMM A gather
-  int N, H, W, C, ldx;   // forward: X geometry.  dgrad: DX geometry (output)
-  int P, Q, K, ldy;      // forward: Y geometry.  dgrad: DY geometry (input)
-  int R, stride, pad, pad_mode;
-  const void* a_src;     // forward: X; dgrad: DY
-  const void* b_src;     // forward: Wf [K][RRC]; dgrad: WT [C][RRK]
-  const float* bias;
-  void* out;             // forward: Y; dgrad: DX
-  int ld_out;
-  int M, NC, KK;         // GEMM sizes: rows, cols, reduction
-  int epilogue, accumulate, out_f32;
-  float epi_scale;
-  const void* residual;
-  int ldr;
-  float* stats;
-};
-
 template <typename T> struct Frag;
 template <> struct Frag<bf16_t> { bf16x8_t v; };
 template <> struct Frag<float> { float v[8]; };
@@ -137,244 +117,6 @@ __device__ __forceinline__ int dgrad_sources(int i, int tap, int n_in, int n_out
   return cnt;
 }
 
-template <typename T, int MODE, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
-  constexpr int TM = BM / WM / 16;
-  constexpr int TN = BN / WN / 16;
-  constexpr int A_CHUNKS = BM * (BK / 8);
-  constexpr int B_CHUNKS = BN * (BK / 8);
-  constexpr int A_PER = (A_CHUNKS + 255) / 256;
-  constexpr int B_PER = (B_CHUNKS + 255) / 256;
-  static_assert(WM * WN == 4, "4 waves");
-
-  __shared__ __attribute__((aligned(16))) T sA[BM * LDK];
-  __shared__ __attribute__((aligned(16))) T sB[BN * LDK];
-  __shared__ float sStat[WM][BN][2];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int bm = blockIdx.x * BM;
-  const int bn = blockIdx.y * BN;
-
-  const T* __restrict__ asrc = reinterpret_cast<const T*>(a.a_src);
-  const T* __restrict__ bsrc = reinterpret_cast<const T*>(a.b_src);
-
-  // Per-thread A rows: decode pixel coordinates once.
-  int a_row[A_PER], a_kc[A_PER], a_n[A_PER], a_y[A_PER], a_x[A_PER];
-  bool a_ok[A_PER];
-#pragma unroll
-  for (int i = 0; i < A_PER; ++i) {
-    const int c = tid + i * 256;
-    a_row[i] = c / (BK / 8);
-    a_kc[i] = c % (BK / 8);
-    const int m = bm + a_row[i];
-    a_ok[i] = (c < A_CHUNKS) && (m < a.M);
-    const int mm = a_ok[i] ? m : 0;
-    if (MODE == MODE_FWD) {
-      const int pq = a.P * a.Q;
-      a_n[i] = mm / pq;
-      const int r = mm - a_n[i] * pq;
-      const int p = r / a.Q, q = r - (r / a.Q) * a.Q;
-      a_y[i] = p * a.stride - a.pad;
-      a_x[i] = q * a.stride - a.pad;
-    } else {
-      const int hw = a.H * a.W;
-      a_n[i] = mm / hw;
-      const int r = mm - a_n[i] * hw;
-      a_y[i] = r / a.W;
-      a_x[i] = r - a_y[i] * a.W;
-    }
-  }
-  int b_row[B_PER], b_kc[B_PER];
-  bool b_ok[B_PER];
-#pragma unroll
-  for (int i = 0; i < B_PER; ++i) {
-    const int c = tid + i * 256;
-    b_row[i] = c / (BK / 8);
-    b_kc[i] = c % (BK / 8);
-    b_ok[i] = (c < B_CHUNKS) && (bn + b_row[i] < a.NC);
-  }
-
-  // channel count of the gathered operand (per tap)
-  const int CH = (MODE == MODE_FWD) ? a.C : a.K;
-
-  Raw8<T> ra[A_PER], rb[B_PER];
-
-  auto load_tiles = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int kidx = k0 + a_kc[i] * 8;
-      raw_zero(ra[i]);
-      if (!a_ok[i] || kidx >= a.KK) continue;
-      const int tap = kidx / CH;
-      const int ch = kidx - tap * CH;
-      const int r = tap / a.R, s = tap - (tap / a.R) * a.R;
-      if (MODE == MODE_FWD) {
-        int yy = a_y[i] + r, xx = a_x[i] + s;
-        if (a.pad_mode == UM_PAD_REFLECT) {
-          yy = reflect_idx(yy, a.H);
-          xx = reflect_idx(xx, a.W);
-        } else if (yy < 0 || yy >= a.H || xx < 0 || xx >= a.W) {
-          continue;
-        }
-        raw_load8(asrc + ((long)(a_n[i] * a.H + yy) * a.W + xx) * a.ldx + ch, ra[i]);
-      } else {
-        int sy[3], sx[3];
-        const bool refl = a.pad_mode == UM_PAD_REFLECT;
-        const int ny = dgrad_sources(a_y[i], r, a.H, a.P, a.stride, a.pad, refl, sy);
-        const int nx = dgrad_sources(a_x[i], s, a.W, a.Q, a.stride, a.pad, refl, sx);
-        if (ny == 0 || nx == 0) continue;
-        if (ny == 1 && nx == 1) {
-          raw_load8(asrc + ((long)(a_n[i] * a.P + sy[0]) * a.Q + sx[0]) * a.ldy + ch, ra[i]);
-        } else {
-          float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-          for (int u = 0; u < ny; ++u)
-            for (int w = 0; w < nx; ++w)
-              accum8(asrc + ((long)(a_n[i] * a.P + sy[u]) * a.Q + sx[w]) * a.ldy + ch, v);
-          f32_to_raw(v, ra[i]);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int kidx = k0 + b_kc[i] * 8;
-      raw_zero(rb[i]);
-      if (!b_ok[i] || kidx >= a.KK) continue;
-      raw_load8(bsrc + (long)(bn + b_row[i]) * a.KK + kidx, rb[i]);
-    }
-  };
-
-  f32x4_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (a.KK + BK - 1) / BK;
-  load_tiles(0);
-  const int frow = lane & 15;
-  const int fk = (lane >> 4) * 8;
-  for (int kt = 0; kt < nk; ++kt) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i)
-      if (tid + i * 256 < A_CHUNKS) raw_store8(&sA[a_row[i] * LDK + a_kc[i] * 8], ra[i]);
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i)
-      if (tid + i * 256 < B_CHUNKS) raw_store8(&sB[b_row[i] * LDK + b_kc[i] * 8], rb[i]);
-    __syncthreads();
-    if (kt + 1 < nk) load_tiles((kt + 1) * BK);
-    Frag<T> fa[TM], fb[TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-      lds_frag(&sA[(wm * (BM / WM) + i * 16 + frow) * LDK + fk], fa[i]);
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-      lds_frag(&sB[(wn * (BN / WN) + j * 16 + frow) * LDK + fk], fb[j]);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) mfma(acc[i][j], fa[i], fb[j]);
-  }
-
-  // ------------------------------------------------------------- epilogue --
-  const int col_l = lane & 15;
-  const int row_g = (lane >> 4) * 4;
-  float csum[TN], csq[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
-
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = bn + wn * (BN / WN) + j * 16 + col_l;
-    const bool nok = n < a.NC;
-    const float bv = (a.bias != nullptr && nok) ? a.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = bm + wm * (BM / WM) + i * 16 + row_g + r;
-        if (!nok || m >= a.M) continue;
-        float v = acc[i][j][r] + bv;
-        const long off = (long)m * a.ld_out + n;
-        if (a.epilogue == UM_EPI_RESIDUAL)
-          v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
-        if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
-        if (a.out_f32) {
-          float* o = reinterpret_cast<float*>(a.out) + off;
-          if (a.accumulate) v += *o;
-          *o = v;
-        } else {
-          T* o = reinterpret_cast<T*>(a.out) + off;
-          if (a.accumulate) v += to_f32(*o);
-          *o = from_f32<T>(v);
-        }
-        csum[j] += v;
-        csq[j] += v * v;
-      }
-    }
-  }
-  if (a.epilogue == UM_EPI_STATS) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float s = csum[j], q = csq[j];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 16) {
-        sStat[wm][wn * (BN / WN) + j * 16 + lane][0] = s;
-        sStat[wm][wn * (BN / WN) + j * 16 + lane][1] = q;
-      }
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
-      const int n = bn + c;
-      if (n >= a.NC) continue;
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) { s += sStat[w][c][0]; q += sStat[w][c][1]; }
-      float* out = a.stats + ((long)blockIdx.x * a.NC + n) * 2;
-      out[0] = s;
-      out[1] = q;
-    }
-  }
-}
-
-template <typename T, int MODE, int BM, int BN, int WM, int WN>
-int launch_conv(const ConvArgs& a, hipStream_t st) {
-  dim3 grid(ceil_div(a.M, BM), ceil_div(a.NC, BN));
-  hipLaunchKernelGGL((conv_gemm_kernel<T, MODE, BM, BN, WM, WN>), grid, dim3(256), 0, st, a);
-  UM_LAUNCH_CHECK();
-  return UM_OK;
-}
-
-constexpr int STATS_BM = 128;  // fixed M tile whenever stats are requested
-
-template <typename T, int MODE>
-int dispatch_conv(const ConvArgs& a, hipStream_t st) {
-  if (a.epilogue == UM_EPI_STATS) {
-    // BM fixed to STATS_BM so the partial-row count is shape-independent
-    if (a.NC <= 32) return launch_conv<T, MODE, 128, 32, 4, 1>(a, st);
-    if (a.NC <= 64) return launch_conv<T, MODE, 128, 64, 2, 2>(a, st);
-    return launch_conv<T, MODE, 128, 128, 2, 2>(a, st);
-  }
-  if (a.NC <= 16) return launch_conv<T, MODE, 256, 16, 4, 1>(a, st);
-  if (a.NC <= 32) return launch_conv<T, MODE, 256, 32, 4, 1>(a, st);
-  const long big = (long)ceil_div(a.M, 128) * ceil_div(a.NC, 128);
-  if (a.NC <= 64 || big < 512) {
-    const long mid = (long)ceil_div(a.M, 128) * ceil_div(a.NC, 64);
-    if (mid >= 512) return launch_conv<T, MODE, 128, 64, 2, 2>(a, st);
-    return launch_conv<T, MODE, 64, 64, 2, 2>(a, st);
-  }
-  return launch_conv<T, MODE, 128, 128, 2, 2>(a, st);
-}
-
-// ------------------------------------------------------------ weight grad --
-// C[k][j] = sum_m DY[m][k] * X[m][j], j = (r, s, c); both operands are
-// staged transposed into LDS ([row][m]) so MFMA fragments read 8 consecutive m.
 struct WgradArgs {
   int N, H, W, C, ldx, K, R, stride, pad, pad_mode, P, Q, ldy;
   const void* x;
@@ -763,11 +505,15 @@ int um_conv_stats_parts(int M, int K) {
 }
 
 long um_conv_fwd_ws(int dtype, int N, int P, int Q, int K, int R, int C) {
-  return umamd::igemm_ws_bytes(dtype, N * P * Q, K, R, C);
+  return umamd::igemm_ws_bytes(dtype, N * P * Q, K, R * R, C);
 }
 
 long um_conv_dgrad_ws(int dtype, int N, int H, int W, int C, int R, int K, int stride) {
-  return stride == 1 ? umamd::igemm_ws_bytes(dtype, N * H * W, C, R, K) : 0;
+  if (stride == 1) return umamd::igemm_ws_bytes(dtype, N * H * W, C, R * R, K);
+  long b = 0;  // the largest parity class (the launches reuse one workspace)
+  const int taps = ((R + 1) / 2) * ((R + 1) / 2);
+  b = std::max(b, umamd::igemm_ws_bytes(dtype, N * ((H + 1) / 2) * ((W + 1) / 2), C, taps, K));
+  return b;
 }
 
 int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x, const void* wf,
@@ -787,6 +533,7 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
   a.a = x; a.ah = H; a.aw = W; a.ach = C; a.lda = ldx;
   a.on = N; a.oh = P; a.ow = Q;
   a.R = R; a.stride = stride; a.pad = pad;
+  a.Rx = R; a.padx = pad; a.tsign = 1; a.wR = R;
   a.pmode = pad_mode == UM_PAD_REFLECT ? umamd::IG_PAD_REFLECT : umamd::IG_PAD_ZERO;
   a.fold_pad = 0; a.flip = 0;
   a.b = wf; a.ldb = (long)R * R * C;
@@ -811,6 +558,7 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
     a.a = dy; a.ah = P; a.aw = Q; a.ach = K; a.lda = ldy;
     a.on = N; a.oh = H; a.ow = W;
     a.R = R; a.stride = 1; a.pad = R - 1 - pad;
+    a.Rx = R; a.padx = R - 1 - pad; a.tsign = 1; a.wR = R;
     a.pmode = pad_mode == UM_PAD_REFLECT ? umamd::IG_FOLD : umamd::IG_PAD_ZERO;
     a.fold_pad = pad; a.flip = 1;
     a.b = wT; a.ldb = (long)R * R * K;
@@ -820,16 +568,34 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
     a.residual = nullptr; a.ldr = 0; a.stats = nullptr;
     return umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
   }
-  ConvArgs a{};
-  a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx;
-  a.P = P; a.Q = Q; a.K = K; a.ldy = ldy;
-  a.R = R; a.stride = stride; a.pad = pad; a.pad_mode = pad_mode;
-  a.a_src = dy; a.b_src = wT; a.bias = nullptr; a.out = dx; a.ld_out = ldx;
-  a.M = N * H * W; a.NC = C; a.KK = R * R * K;
-  a.epilogue = UM_EPI_NONE; a.accumulate = accumulate; a.out_f32 = (dtype == UM_F32);
-  if (a.M == 0) return UM_OK;
-  return dtype == UM_BF16 ? dispatch_conv<bf16_t, MODE_DGRAD>(a, st)
-                          : dispatch_conv<float, MODE_DGRAD>(a, st);
+  // stride 2 (zero padding): four parity classes (ay, ax) of dx pixels, each
+  // a stride-1 gather over dy with the weight taps of matching parity:
+  // dx[2i'+ay] = sum_t dy[i' + offy - t] * w[r0y + 2t], r0y = (ay+pad) % 2,
+  // offy = (ay + pad - r0y) / 2 (and likewise in x)
+  UM_CHECK_ARG(P == (H + 2 * pad - R) / 2 + 1 && Q == (W + 2 * pad - R) / 2 + 1,
+               "um_conv2d_dgrad: size");
+  for (int ay = 0; ay < 2; ++ay)
+    for (int ax = 0; ax < 2; ++ax) {
+      umamd::IgArgs a{};
+      const int r0y = (ay + pad) & 1, r0x = (ax + pad) & 1;
+      const int nty = (R - r0y + 1) / 2, ntx = (R - r0x + 1) / 2;
+      const int Hc = (H - ay + 1) / 2, Wc = (W - ax + 1) / 2;
+      if (Hc <= 0 || Wc <= 0) continue;
+      a.a = dy; a.ah = P; a.aw = Q; a.ach = K; a.lda = ldy;
+      a.on = N; a.oh = Hc; a.ow = Wc;
+      a.R = nty; a.Rx = ntx; a.stride = 1; a.tsign = -1;
+      a.pad = -((ay + pad - r0y) / 2); a.padx = -((ax + pad - r0x) / 2);
+      a.pmode = umamd::IG_PAD_ZERO; a.fold_pad = 0; a.flip = 0;
+      a.cls = 1; a.wR = R; a.r0y = r0y; a.r0x = r0x; a.ay = ay; a.ax = ax; a.outH = H; a.outW = W;
+      a.b = wT; a.ldb = (long)R * R * K;
+      a.NC = C; a.M = N * Hc * Wc;
+      a.bias = nullptr; a.out = dx; a.ld_out = ldx; a.out_f32 = (dtype == UM_F32);
+      a.epilogue = UM_EPI_NONE; a.accumulate = accumulate; a.epi_scale = 1.f;
+      a.residual = nullptr; a.ldr = 0; a.stats = nullptr;
+      const int rc = umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
+      if (rc != UM_OK) return rc;
+    }
+  return UM_OK;
 }
 
 static int wgrad_bm(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }

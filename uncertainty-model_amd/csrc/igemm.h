@@ -14,8 +14,14 @@ struct IgArgs {
   int ah, aw, ach, lda;
   // output pixels: GEMM row m = (n, oy, ox) over [on][oh][ow]
   int on, oh, ow;
-  // tap geometry: source row = oy*stride - pad + r (flipped taps for dgrad)
+  // tap geometry: source row = oy*stride - pad + tsign*r, column ox*stride -
+  // padx + tsign*s, taps r < R, s < Rx (flipped weight taps for dgrad)
   int R, stride, pad, pmode, fold_pad, flip;
+  int Rx, padx, tsign;
+  // parity-class mode (stride-2 data gradient): weight tap (r0y + 2r, r0x + 2s)
+  // of the wR x wR kernel; output row (n, i', j') -> pixel (2i'+ay, 2j'+ax) of
+  // an outH x outW image
+  int cls, wR, r0y, r0x, ay, ax, outH, outW;
   // weights ("B"): row n (output channel) at b + n*ldb, element tap*ach + c
   const void* b;
   long ldb;
@@ -35,7 +41,7 @@ struct IgArgs {
 int igemm_stats_rows(int M, int NC);
 
 // workspace bytes the split-K heuristic wants for this shape (0: no split)
-long igemm_ws_bytes(int dtype, int M, int NC, int R, int ach);
+long igemm_ws_bytes(int dtype, int M, int NC, int taps, int ach);
 // launch; ws may be null (then no split)
 int igemm_run(int dtype, const IgArgs& a, float* ws, long ws_bytes, hipStream_t st);
 

@@ -111,6 +111,7 @@ struct ARow {
   bool ok;
 };
 
+template <bool CLS>
 __device__ __forceinline__ ARow decode_row(const IgArgs& a, int m) {
   ARow w;
   w.ok = m < a.M;
@@ -121,16 +122,27 @@ __device__ __forceinline__ ARow decode_row(const IgArgs& a, int m) {
   const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
   w.base = (long)n * a.ah * a.aw * a.lda;
   w.y0 = oy * a.stride - a.pad;
-  w.x0 = ox * a.stride - a.pad;
+  w.x0 = ox * a.stride - (CLS ? a.padx : a.pad);
   return w;
 }
 
-template <typename T>
+// element offset of output row m (class mode: the row (n, i', j') of parity
+// class (ay, ax) is output pixel (n, 2i'+ay, 2j'+ax) of the full image)
+template <bool CLS>
+__device__ __forceinline__ long out_row(const IgArgs& a, int m) {
+  if (!CLS) return (long)m * a.ld_out;
+  const int hw = a.oh * a.ow;
+  const int n = m / hw, rem = m - n * hw;
+  const int i = rem / a.ow, j = rem - (rem / a.ow) * a.ow;
+  return (((long)n * a.outH + 2 * i + a.ay) * a.outW + 2 * j + a.ax) * a.ld_out;
+}
+
+template <bool CLS, typename T>
 __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ src, const ARow& w,
                                        int r, int s, int c, Raw8<T>& out) {
   raw_zero(out);
   if (!w.ok || c >= a.ach) return;
-  int yy = w.y0 + r, xx = w.x0 + s;
+  int yy = CLS ? w.y0 - r : w.y0 + r, xx = CLS ? w.x0 - s : w.x0 + s;
   if (a.pmode == umamd::IG_PAD_REFLECT) {
     yy = reflect_idx(yy, a.ah);
     xx = reflect_idx(xx, a.aw);
@@ -166,7 +178,7 @@ __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ sr
   to_raw(v, out);
 }
 
-template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT>
+template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT, bool CLS>
 __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict__ ws,
                                                      int steps, int steps_per_split, int ntn) {
   using I = Img<T, BK>;
@@ -208,7 +220,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
     const int c = tid + i * 256;
     arow_i[i] = c / CPR;
     akc[i] = c % CPR;
-    arow[i] = decode_row(a, bm + arow_i[i]);
+    arow[i] = decode_row<CLS>(a, bm + arow_i[i]);
   }
   int brow_i[B_PER], bkc[B_PER];
   bool bok[B_PER];
@@ -225,13 +237,15 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
   const int nchunk = (a.ach + BK - 1) / BK;
   int tap = s_begin / nchunk;
   int c0 = (s_begin - tap * nchunk) * BK;
-  int r = tap / a.R, s = tap - (tap / a.R) * a.R;
+  const int RX = CLS ? a.Rx : a.R;
+  int r = tap / RX, s = tap - (tap / RX) * RX;
 
   Raw8<T> ra[A_PER], rb[B_PER];
   auto load = [&]() {
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) gather(a, asrc, arow[i], r, s, c0 + akc[i] * 8, ra[i]);
-    const int btap = a.flip ? (a.R - 1 - r) * a.R + (a.R - 1 - s) : r * a.R + s;
+    for (int i = 0; i < A_PER; ++i) gather<CLS>(a, asrc, arow[i], r, s, c0 + akc[i] * 8, ra[i]);
+    const int btap = CLS ? (a.r0y + 2 * r) * a.wR + (a.r0x + 2 * s)
+                         : (a.flip ? (a.R - 1 - r) * a.R + (a.R - 1 - s) : r * a.R + s);
     const long boff = (long)btap * a.ach;
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
@@ -251,7 +265,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
     c0 += BK;
     if (c0 >= a.ach) {
       c0 = 0;
-      if (++s == a.R) { s = 0; ++r; }
+      if (++s == RX) { s = 0; ++r; }
     }
   };
 
@@ -327,7 +341,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
         const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
         if (!nok || m >= a.M) continue;
         float v = acc[i][j][q] + bv;
-        const long off = (long)m * a.ld_out + n;
+        const long off = out_row<CLS>(a, m) + n;
         if (a.epilogue == UM_EPI_RESIDUAL)
           v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
         if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
@@ -380,7 +394,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
 // sum the split-K partials and apply the epilogue.  Block = a.stats_rows rows x
 // 64 columns: thread (g, lane) owns columns 4g..4g+3 and rows lane, lane+16, ...
 constexpr int EPI_COLS = 64;
-template <typename T>
+template <typename T, bool CLS>
 __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const float* __restrict__ ws,
                                                                int splits) {
   __shared__ float red[16][16][8];
@@ -415,7 +429,7 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const fl
         if (a.epilogue == UM_EPI_RESIDUAL)
           v[e] += to_f32(reinterpret_cast<const T*>(a.residual)[m * a.ldr + n + e]);
         if (a.epilogue == UM_EPI_SIGMOID_SCALE) v[e] = a.epi_scale * sigmoidf_(v[e]);
-        const long off = m * a.ld_out + n + e;
+        const long off = out_row<CLS>(a, (int)m) + n + e;
         if (a.out_f32) {
           float* o = reinterpret_cast<float*>(a.out) + off;
           if (a.accumulate) v[e] += *o;
@@ -477,7 +491,7 @@ bool small_tiles(int M, int NC) {
   return k.small && NC > 64 && (long)ceil_div(M, 128) * ceil_div(NC, 128) < k.small_tiles;
 }
 
-Plan make_plan(int dtype, int M, int NC, int R, int ach, long ws_bytes) {
+Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes) {
   const Knobs& kn = knobs();
   Plan p{};
   p.bk = 32;
@@ -491,7 +505,7 @@ Plan make_plan(int dtype, int M, int NC, int R, int ach, long ws_bytes) {
     p.bm = 128; p.bn = 128; p.wm = 2; p.wn = 2;
     if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;  // 64 KB of LDS: 2 blocks/CU
   }
-  p.steps = R * R * ((ach + p.bk - 1) / p.bk);
+  p.steps = taps * ((ach + p.bk - 1) / p.bk);
   // Split only grids that leave most CUs idle: the partials cost an f32
   // write + read of splits*M*NC (about 1 us per 8 MB each way), so aim at
   // ~320 blocks, >= 8 k-steps per split and <= 32 MB of partials.
@@ -509,21 +523,27 @@ Plan make_plan(int dtype, int M, int NC, int R, int ach, long ws_bytes) {
   return p;
 }
 
-template <typename T, int BK, int BM, int BN, int WM, int WN>
-int launch(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
+template <typename T, int BK, int BM, int BN, int WM, int WN, bool CLS>
+int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
   const int ntm = ceil_div(a.M, BM), ntn = ceil_div(a.NC, BN);
   if (p.splits > 1) {
-    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, true>), dim3(ntm * ntn, 1, p.splits),
-                       dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
-    hipLaunchKernelGGL(splitk_epilogue_kernel<T>,
+    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, true, CLS>),
+                       dim3(ntm * ntn, 1, p.splits), dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
+    hipLaunchKernelGGL((splitk_epilogue_kernel<T, CLS>),
                        dim3(ceil_div(a.M, a.stats_rows), ceil_div(a.NC, EPI_COLS)), dim3(256), 0, st,
                        a, (const float*)ws, p.splits);
   } else {
-    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, false>), dim3(ntm * ntn, 1, 1),
+    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, false, CLS>), dim3(ntm * ntn, 1, 1),
                        dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
   }
   UM_LAUNCH_CHECK();
   return UM_OK;
+}
+
+template <typename T, int BK, int BM, int BN, int WM, int WN>
+int launch(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
+  return a.cls ? launch_cls<T, BK, BM, BN, WM, WN, true>(a, p, ws, st)
+               : launch_cls<T, BK, BM, BN, WM, WN, false>(a, p, ws, st);
 }
 
 template <typename T>
@@ -545,8 +565,8 @@ int dispatch_tiles(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
 
 namespace umamd {
 
-long igemm_ws_bytes(int dtype, int M, int NC, int R, int ach) {
-  const Plan p = make_plan(dtype, M, NC, R, ach, -1);
+long igemm_ws_bytes(int dtype, int M, int NC, int taps, int ach) {
+  const Plan p = make_plan(dtype, M, NC, taps, ach, -1);
   return p.splits > 1 ? (long)p.splits * M * NC * 4 : 0;
 }
 
@@ -556,7 +576,7 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   if (a_in.M == 0) return UM_OK;
   IgArgs a = a_in;
   a.stats_rows = igemm_stats_rows(a.M, a.NC);
-  const Plan p = make_plan(dtype, a.M, a.NC, a.R, a.ach, ws ? ws_bytes : 0);
+  const Plan p = make_plan(dtype, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0);
   if (dtype == UM_BF16) return dispatch_tiles<bf16_t>(a, p, ws, st);
   return dispatch_tiles<float>(a, p, ws, st);
 }
