@@ -42,6 +42,10 @@ enum {
 
 const char* um_last_error(void);
 int um_version(void);
+/* kernel-selection knobs (tests force code paths, tuning sweeps): "halo",
+ * "halo_min_tiles", "small", "small_tiles", "split_below", "split_target",
+ * "split_minsteps".  Returns the previous value, -1 for an unknown key. */
+int um_set_tuning(const char* key, int value);
 
 /* ---------------------------------------------------------------- conv ---
  * Replaces nn.Conv2d forward/backward with its padding:

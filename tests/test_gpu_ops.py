@@ -52,6 +52,28 @@ CONV_CASES = [
 ]
 
 
+# shapes the halo-tiled direct conv takes (bf16, stride 1, "same" padding,
+# P % 8 == 0, Q % 32 == 0, K <= 64); the tile-count threshold is lowered so
+# these small images use it (forward + zero-pad data gradient)
+HALO_CASES = [
+    (32, 32, 7, 1, 'zero', 16, 32),
+    (64, 64, 5, 1, 'zero', 8, 64),
+    (40, 48, 3, 1, 'reflect', 8, 32),
+    (64, 16, 3, 1, 'zero', 16, 32),
+    (8, 32, 3, 1, 'reflect', 8, 64),
+]
+
+
+@pytest.mark.parametrize('case', HALO_CASES)
+def test_conv_bn_elu_halo(case):
+    from umamd._lib import lib
+    old = lib().um_set_tuning(b'halo_min_tiles', 1)
+    try:
+        test_conv_bn_elu(case, torch.bfloat16)
+    finally:
+        lib().um_set_tuning(b'halo_min_tiles', old)
+
+
 @pytest.mark.parametrize('case', CONV_CASES)
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 def test_conv_bn_elu(case, dtype):

@@ -1,0 +1,288 @@
+// Halo-tiled direct convolution on MFMA (gfx950) for the small-channel,
+// high-resolution 3x3 / 5x5 / 7x7 layers: forward (zero or reflect padding)
+// and the stride-1 data gradient of zero-padded convs (a forward conv of dy
+// with the flipped, transposed weights).
+//
+// The tap-major implicit GEMM (igemm.hip) re-gathers the input pixels from
+// L2 for every tap: R*R times the activation bytes, which for 32..64 output
+// channels is more than the MFMAs can consume (the 7x7 32->32 layers reached
+// ~290 TFLOP/s).  Here a workgroup owns an 8 x 32 output-pixel tile of one
+// image and up to 64 output channels, stages the (8+R-1) x (32+R-1) input
+// halo of one 32-channel chunk ONCE in LDS and runs all R*R taps from it:
+//   - A fragments (16 pixels x 32 channels) are ds_read_b128 of 16
+//     consecutive halo pixels; the 16-byte channel chunks of a pixel are
+//     XOR-swizzled by bits 2-3 of the pixel index, so any 16 consecutive
+//     pixels cover the 64 LDS banks exactly once (conflict-free);
+//   - the weights of one tap row (R taps x BN output channels x 32 channels)
+//     are staged in a double-buffered LDS image with the same swizzle (the
+//     next row is loaded to registers during the current row's MFMAs), so B
+//     fragments are ds_read_b128 too and the 4 waves share one copy;
+//   - the next chunk's halo is loaded to registers while the current one is
+//     computed; v_mfma_f32_16x16x32_bf16, f32 accumulation.
+// Epilogue as igemm's: bias, optional residual / sigmoid-scale / accumulate,
+// f32 or bf16 output, and the BN partial statistics (two 128-pixel rows per
+// tile, so um_conv_stats_parts counts them like the GEMM's).
+// Replaces nn.Conv2d forward / input-gradient of reference
+// model/layers/encoder.py:36-42 (7x7, 5x5, 3x3 zero padded) and
+// model/layers/decoder.py:30-52 (3x3 reflection padded, forward).
+#include "common.h"
+#include "halo_conv.h"
+
+namespace {
+
+using umamd::IgArgs;
+
+constexpr int TH = 8, TW = 32, CK = 32;
+
+// element offset of 8-channel chunk c (0..3) of halo pixel p
+__device__ __forceinline__ int himg(int p, int c) { return p * CK + ((c ^ ((p >> 2) & 3)) << 3); }
+
+template <int R, int BN, bool FLIP, bool REFLECT>
+__global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, int tiles_y) {
+  constexpr int HH = TH + R - 1, HWd = TW + R - 1, HP = HH * HWd;
+  constexpr int PIECES = HP * 4;                 // 16-byte pieces per chunk
+  constexpr int NP = (PIECES + 255) / 256;       // per thread
+  constexpr int TN = BN / 16;
+  constexpr int TM = 4;                          // 4 x 16 pixels per wave (2 tile rows)
+  constexpr int RR = R * R;
+  constexpr int WP = R * BN * 4;              // 16-byte weight pieces per tap row
+  constexpr int NW = (WP + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t sH[HP * CK];
+  __shared__ __attribute__((aligned(16))) bf16_t sW[2][R * BN * CK];
+  __shared__ float sStat[4][BN][2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int t = blockIdx.x;
+  const int bx = t % tiles_x;
+  t /= tiles_x;
+  const int by = t % tiles_y;
+  const int nimg = t / tiles_y;
+  const int ty0 = by * TH, tx0 = bx * TW;
+  const int bn = blockIdx.y * BN;
+  const int iy0 = ty0 - a.pad, ix0 = tx0 - a.pad;
+  const bf16_t* __restrict__ src = reinterpret_cast<const bf16_t*>(a.a);
+  const bf16_t* __restrict__ wsrc = reinterpret_cast<const bf16_t*>(a.b);
+  const long img_base = (long)nimg * a.ah * a.aw * a.lda;
+
+  uint4 hv[NP];
+  auto load_halo = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int i = tid + k * 256;
+      hv[k] = make_uint4(0, 0, 0, 0);
+      if (i < PIECES) {
+        const int p = i >> 2, c = i & 3;
+        const int hy = p / HWd, hx = p - (p / HWd) * HWd;
+        int y = iy0 + hy, x = ix0 + hx;
+        const int ch = c0 + c * 8;
+        bool ok = ch < a.ach;
+        if (REFLECT) {
+          y = reflect_idx(y, a.ah);
+          x = reflect_idx(x, a.aw);
+        } else {
+          ok = ok && y >= 0 && y < a.ah && x >= 0 && x < a.aw;
+        }
+        if (ok)
+          hv[k] = *reinterpret_cast<const uint4*>(src + img_base + ((long)y * a.aw + x) * a.lda + ch);
+      }
+    }
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int i = tid + k * 256;
+      if (i < PIECES) *reinterpret_cast<uint4*>(&sH[himg(i >> 2, i & 3)]) = hv[k];
+    }
+  };
+
+  // weight tap row r of chunk c0 -> registers: piece i = (s, n, c) of tap (r, s),
+  // output channel bn + n, reduction channels c0 + 8c .. + 8
+  const int ncol = lane & 15, kq = lane >> 4;
+  uint4 wv[NW];
+  auto load_wrow = [&](int r, int c0) {
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int i = tid + k * 256;
+      wv[k] = make_uint4(0, 0, 0, 0);
+      if (i < WP) {
+        const int c = i & 3, nn = (i >> 2) % BN, ss = (i >> 2) / BN;
+        const int n = bn + nn, ch = c0 + c * 8;
+        const int tap = r * R + ss;
+        const int btap = FLIP ? RR - 1 - tap : tap;
+        if (n < a.NC && ch < a.ach)
+          wv[k] = *reinterpret_cast<const uint4*>(wsrc + (long)n * a.ldb + (long)btap * a.ach + ch);
+      }
+    }
+  };
+  auto store_wrow = [&](int buf) {
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int i = tid + k * 256;
+      if (i < WP) {
+        const int c = i & 3, row = i >> 2;  // row = ss * BN + nn
+        *reinterpret_cast<uint4*>(&sW[buf][himg(row, c)]) = wv[k];
+      }
+    }
+  };
+  bool nok[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) nok[j] = bn + j * 16 + ncol < a.NC;
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // A fragment base pixel of fragment i: tile row 2*wave + (i >> 1), column (i & 1)*16 + row
+  int pbase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) pbase[i] = (2 * wave + (i >> 1)) * HWd + (i & 1) * 16 + ncol;
+
+  const int nchunk = (a.ach + CK - 1) / CK;
+  load_halo(0);
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int c0 = ch * CK;
+    __syncthreads();  // the previous chunk's fragment reads are done
+    store_halo();
+    __syncthreads();
+    load_wrow(0, c0);
+    if (ch + 1 < nchunk) load_halo(c0 + CK);
+    store_wrow(0);
+    __syncthreads();
+#pragma unroll 1
+    for (int r = 0; r < R; ++r) {
+      const int buf = r & 1;
+      if (r + 1 < R) load_wrow(r + 1, c0);
+#pragma unroll
+      for (int s = 0; s < R; ++s) {
+        bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8_t*>(&sH[himg(pbase[i] + r * HWd + s, kq)]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8_t*>(&sW[buf][himg(s * BN + j * 16 + ncol, kq)]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+      if (r + 1 < R) store_wrow(buf ^ 1);  // that buffer was last read in row r-1
+      __syncthreads();
+    }
+  }
+
+  // ---------------------------------------------------------------- epilogue --
+  const int row_g = (lane >> 4) * 4;
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = bn + j * 16 + ncol;
+    if (!nok[j]) continue;
+    const float bv = a.bias != nullptr ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ty = 2 * wave + (i >> 1);
+      const long mrow = ((long)nimg * a.oh + ty0 + ty) * a.ow + tx0 + (i & 1) * 16 + row_g;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const long m = mrow + q;
+        float v = acc[i][j][q] + bv;
+        const long off = m * a.ld_out + n;
+        if (a.epilogue == UM_EPI_RESIDUAL)
+          v += to_f32(reinterpret_cast<const bf16_t*>(a.residual)[m * a.ldr + n]);
+        if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
+        if (a.out_f32) {
+          float* o = reinterpret_cast<float*>(a.out) + off;
+          if (a.accumulate) v += *o;
+          *o = v;
+        } else {
+          bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + off;
+          if (a.accumulate) v += to_f32(*o);
+          *o = from_f32<bf16_t>(v);
+        }
+        csum[j] += v;
+        csq[j] += v * v;
+      }
+    }
+  }
+  if (a.epilogue == UM_EPI_STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float sm = csum[j], sq = csq[j];
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      sq += __shfl_xor(sq, 16, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      if (lane < 16) {
+        sStat[wave][j * 16 + lane][0] = sm;
+        sStat[wave][j * 16 + lane][1] = sq;
+      }
+    }
+    __syncthreads();
+    // two partial rows per tile: waves {0,1} (tile rows 0-3) and {2,3} (rows 4-7)
+    for (int c = tid; c < 2 * BN; c += 256) {
+      const int col = c % BN, half = c / BN;
+      const int n = bn + col;
+      if (n >= a.NC) continue;
+      const float sm = sStat[2 * half][col][0] + sStat[2 * half + 1][col][0];
+      const float sq = sStat[2 * half][col][1] + sStat[2 * half + 1][col][1];
+      float* o = a.stats + ((long)(2 * blockIdx.x + half) * a.NC + n) * 2;
+      o[0] = sm;
+      o[1] = sq;
+    }
+  }
+}
+
+template <int R, int BN>
+int launch_r(const IgArgs& a, hipStream_t st) {
+  const int tiles_x = a.ow / TW, tiles_y = a.oh / TH;
+  dim3 grid(a.on * tiles_y * tiles_x, (a.NC + BN - 1) / BN);
+  if (a.flip)
+    hipLaunchKernelGGL((halo_conv_kernel<R, BN, true, false>), grid, dim3(256), 0, st, a, tiles_x,
+                       tiles_y);
+  else if (a.pmode == umamd::IG_PAD_REFLECT)
+    hipLaunchKernelGGL((halo_conv_kernel<R, BN, false, true>), grid, dim3(256), 0, st, a, tiles_x,
+                       tiles_y);
+  else
+    hipLaunchKernelGGL((halo_conv_kernel<R, BN, false, false>), grid, dim3(256), 0, st, a,
+                       tiles_x, tiles_y);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+template <int R>
+int launch_bn(const IgArgs& a, hipStream_t st) {
+  if (a.NC <= 16) return launch_r<R, 16>(a, st);
+  if (a.NC <= 32) return launch_r<R, 32>(a, st);
+  return launch_r<R, 64>(a, st);
+}
+
+}  // namespace
+
+namespace umamd {
+
+bool halo_applicable(int dtype, const IgArgs& a, int min_tiles) {
+  if (dtype != UM_BF16 || a.stride != 1 || a.cls) return false;
+  if (a.R != 3 && a.R != 5 && a.R != 7) return false;
+  if (a.pmode == IG_FOLD) return false;                         // reflect transpose: igemm
+  if (a.flip && a.pmode != IG_PAD_ZERO) return false;
+  if (a.oh != a.ah || a.ow != a.aw || a.pad != (a.R - 1) / 2) return false;  // "same" conv
+  if (a.oh % TH || a.ow % TW) return false;
+  if (a.NC > 64 || a.ach % 8 || a.lda % 8) return false;
+  if (a.epilogue == UM_EPI_STATS && a.stats_rows != 128) return false;
+  // enough tiles to fill the chip
+  return (long)a.on * (a.oh / TH) * (a.ow / TW) >= min_tiles;
+}
+
+int halo_run(const IgArgs& a, hipStream_t st) {
+  if (a.R == 3) return launch_bn<3>(a, st);
+  if (a.R == 5) return launch_bn<5>(a, st);
+  return launch_bn<7>(a, st);
+}
+
+}  // namespace umamd

@@ -31,6 +31,7 @@
 
 #include "common.h"
 #include "igemm.h"
+#include "halo_conv.h"
 
 namespace {
 
@@ -464,7 +465,7 @@ struct Plan {
 
 // tuning knobs (read once; UMAMD_IG_* environment variables for sweeps)
 struct Knobs {
-  int small, small_tiles, split_below, split_target, split_minsteps;
+  int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles;
   Knobs() {
     auto env = [](const char* n, int d) {
       const char* v = getenv(n);
@@ -475,10 +476,12 @@ struct Knobs {
     split_below = env("UMAMD_IG_SPLIT_BELOW", 160);
     split_target = env("UMAMD_IG_SPLIT_TARGET", 320);
     split_minsteps = env("UMAMD_IG_SPLIT_MINSTEPS", 8);
+    halo = env("UMAMD_HALO", 1);
+    halo_min_tiles = env("UMAMD_HALO_MIN_TILES", 256);
   }
 };
-const Knobs& knobs() {
-  static const Knobs k;
+Knobs& knobs() {
+  static Knobs k;
   return k;
 }
 
@@ -576,9 +579,28 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   if (a_in.M == 0) return UM_OK;
   IgArgs a = a_in;
   a.stats_rows = igemm_stats_rows(a.M, a.NC);
+  if (knobs().halo && halo_applicable(dtype, a, knobs().halo_min_tiles)) return halo_run(a, st);
   const Plan p = make_plan(dtype, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0);
   if (dtype == UM_BF16) return dispatch_tiles<bf16_t>(a, p, ws, st);
   return dispatch_tiles<float>(a, p, ws, st);
 }
 
 }  // namespace umamd
+
+// tuning knobs at run time (tests force code paths; sweeps): returns the old
+// value, or -1 for an unknown key
+extern "C" int um_set_tuning(const char* key, int value) {
+  Knobs& k = knobs();
+  int* f = nullptr;
+  if (!strcmp(key, "halo")) f = &k.halo;
+  else if (!strcmp(key, "halo_min_tiles")) f = &k.halo_min_tiles;
+  else if (!strcmp(key, "small")) f = &k.small;
+  else if (!strcmp(key, "small_tiles")) f = &k.small_tiles;
+  else if (!strcmp(key, "split_below")) f = &k.split_below;
+  else if (!strcmp(key, "split_target")) f = &k.split_target;
+  else if (!strcmp(key, "split_minsteps")) f = &k.split_minsteps;
+  if (!f) return -1;
+  const int old = *f;
+  *f = value;
+  return old;
+}

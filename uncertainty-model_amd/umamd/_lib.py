@@ -35,6 +35,7 @@ class CatSrc(ctypes.Structure):
 _SIG = {
     'um_last_error': (ctypes.c_char_p, []),
     'um_version': (_I, []),
+    'um_set_tuning': (_I, [ctypes.c_char_p, _I]),
     'um_conv_stats_parts': (_I, [_I, _I]),
     'um_conv2d_fwd': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I,
                            _I, _P, _I, _I, _F, _P, _I, _P, _P, _L, 's']),
