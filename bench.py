@@ -103,9 +103,9 @@ def loss_bwd_bytes(N, H, W):
 
 CONV_ENTRIES = {
     # C-ABI entry -> the kernel templates it launches (rocprof names)
-    'um_conv2d_fwd': 'conv_gemm_kernel<T, 0, ...>',
-    'um_conv2d_dgrad': 'conv_gemm_kernel<T, 1, ...>',
-    'um_conv2d_wgrad': 'wgrad_bf16_kernel<BM> / wgrad_kernel<T,64,64>',
+    'um_conv2d_fwd': 'igemm_kernel<T,...,CLS=0> / halo_conv_kernel<R,BN,0,REFLECT>',
+    'um_conv2d_dgrad': 'igemm_kernel<T,...,CLS> (parity classes) / halo_conv_kernel<R,BN,1,...>',
+    'um_conv2d_wgrad': 'hwgrad (wgrad_halo) / wgrad_tr_kernel + wgrad_reduce',
 }
 
 

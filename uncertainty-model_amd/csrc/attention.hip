@@ -13,62 +13,73 @@
 
 namespace {
 
-constexpr int KS_CHUNK = 256;  // pixels per k-stat partial
 constexpr int PT = 64;         // pixels per apply tile
 
 // ---------------------------------------------------------------- k stats --
+// pixels per k-stat partial: at most ~64 chunks per image (16..256 pixels),
+// so the small bottleneck maps still spread over the chip
+static inline int ks_chunk(int S) {
+  int c = 16;
+  while (c < 256 && (long)c * 64 < S) c <<= 1;
+  return c;
+}
+
+// grid (chunk, n, 64-channel group): 4 pixel lanes x 64 channels per block
 template <typename T>
-__global__ void kstats_kernel(const T* __restrict__ qkv, int ld, int S, int C,
+__global__ void kstats_kernel(const T* __restrict__ qkv, int ld, int S, int C, int chunk_px,
                               float* __restrict__ parts, int nchunks) {
   const int n = blockIdx.y, chunk = blockIdx.x;
-  const int s0 = chunk * KS_CHUNK, s1 = min(S, s0 + KS_CHUNK);
+  const int s0 = chunk * chunk_px, s1 = min(S, s0 + chunk_px);
   __shared__ float sm[4][64], ss[4][64];
   const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
-  for (int c0 = 0; c0 < C; c0 += 64) {
-    const int c = c0 + cl;
-    float mx = -INFINITY, sum = 0.f;
-    if (c < C) {
-      for (int s = s0 + pl; s < s1; s += 4) {
-        const float v = to_f32(qkv[((long)n * S + s) * ld + c]);
-        if (v > mx) {
-          sum = sum * __expf(mx - v) + 1.f;
-          mx = v;
-        } else {
-          sum += __expf(v - mx);
-        }
+  const int c = blockIdx.z * 64 + cl;
+  float mx = -INFINITY, sum = 0.f;
+  if (c < C) {
+    for (int s = s0 + pl; s < s1; s += 4) {
+      const float v = to_f32(qkv[((long)n * S + s) * ld + c]);
+      if (v > mx) {
+        sum = sum * __expf(mx - v) + 1.f;
+        mx = v;
+      } else {
+        sum += __expf(v - mx);
       }
     }
-    sm[pl][cl] = mx;
-    ss[pl][cl] = sum;
-    __syncthreads();
-    if (pl == 0 && c < C) {
-      float M = sm[0][cl];
-      for (int r = 1; r < 4; ++r) M = fmaxf(M, sm[r][cl]);
-      float t = 0.f;
-      for (int r = 0; r < 4; ++r)
-        if (sm[r][cl] > -INFINITY) t += ss[r][cl] * __expf(sm[r][cl] - M);
-      float* o = parts + (((long)n * nchunks + chunk) * C + c) * 2;
-      o[0] = M;
-      o[1] = t;
-    }
-    __syncthreads();
+  }
+  sm[pl][cl] = mx;
+  ss[pl][cl] = sum;
+  __syncthreads();
+  if (pl == 0 && c < C) {
+    float M = sm[0][cl];
+    for (int r = 1; r < 4; ++r) M = fmaxf(M, sm[r][cl]);
+    float t = 0.f;
+    for (int r = 0; r < 4; ++r)
+      if (sm[r][cl] > -INFINITY) t += ss[r][cl] * __expf(sm[r][cl] - M);
+    float* o = parts + (((long)n * nchunks + chunk) * C + c) * 2;
+    o[0] = M;
+    o[1] = t;
   }
 }
 
+// one wave per (n, c); the lanes stride the chunk partials
 __global__ void kstats_combine_kernel(const float* __restrict__ parts, int N, int nchunks, int C,
                                       float* __restrict__ kmax, float* __restrict__ ksum) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N * C) return;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= N * C) return;  // wave-uniform
   const int n = i / C, c = i % C;
   float M = -INFINITY;
-  for (int k = 0; k < nchunks; ++k) M = fmaxf(M, parts[(((long)n * nchunks + k) * C + c) * 2]);
+  for (int k = lane; k < nchunks; k += 64)
+    M = fmaxf(M, parts[(((long)n * nchunks + k) * C + c) * 2]);
+  M = wave_max(M);
   float t = 0.f;
-  for (int k = 0; k < nchunks; ++k) {
+  for (int k = lane; k < nchunks; k += 64) {
     const float* p = parts + (((long)n * nchunks + k) * C + c) * 2;
     if (p[0] > -INFINITY) t += p[1] * __expf(p[0] - M);
   }
-  kmax[i] = M;
-  ksum[i] = t;
+  t = wave_sum(t);
+  if (lane == 0) {
+    kmax[i] = M;
+    ksum[i] = t;
+  }
 }
 
 // ------------------------------------------------------------------- ctx --
@@ -351,7 +362,7 @@ extern "C" {
 
 // workspace sizes (floats)
 long um_attn_ws_kstats(int N, int S, int C) {
-  return (long)N * ceil_div(S, KS_CHUNK) * C * 2;
+  return (long)N * ceil_div(S, ks_chunk(S)) * C * 2;
 }
 long um_attn_ws_ctx(int N, int S, int C, int heads) {
   const int d = C / heads;
@@ -370,17 +381,18 @@ int um_attn_fwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
   UM_CHECK_ARG(C % heads == 0, "um_attn_fwd: C %% heads");
   const int d = C / heads;
   UM_CHECK_ARG(d <= 64, "um_attn_fwd: head dim %d > 64", d);
-  const int nks = ceil_div(S, KS_CHUNK);
+  const int kch = ks_chunk(S);
+  const int nks = ceil_div(S, kch);
   const int cch = ctx_chunk(d);
   const int nctx = ceil_div(S, cch);
   if (dtype == UM_BF16) {
-    hipLaunchKernelGGL(kstats_kernel<bf16_t>, dim3(nks, N), dim3(256), 0, st,
-                       (const bf16_t*)qkv, ld, S, C, ws, nks);
+    hipLaunchKernelGGL(kstats_kernel<bf16_t>, dim3(nks, N, ceil_div(C, 64)), dim3(256), 0, st,
+                       (const bf16_t*)qkv, ld, S, C, kch, ws, nks);
   } else {
-    hipLaunchKernelGGL(kstats_kernel<float>, dim3(nks, N), dim3(256), 0, st, (const float*)qkv,
-                       ld, S, C, ws, nks);
+    hipLaunchKernelGGL(kstats_kernel<float>, dim3(nks, N, ceil_div(C, 64)), dim3(256), 0, st,
+                       (const float*)qkv, ld, S, C, kch, ws, nks);
   }
-  hipLaunchKernelGGL(kstats_combine_kernel, dim3(ceil_div(N * C, 256)), dim3(256), 0, st, ws, N,
+  hipLaunchKernelGGL(kstats_combine_kernel, dim3(ceil_div(N * C, 4)), dim3(256), 0, st, ws, N,
                      nks, C, kmax, ksum);
   const size_t shm_ctx = (2 * (size_t)cch * d + 256) * sizeof(float);
   if (dtype == UM_BF16)

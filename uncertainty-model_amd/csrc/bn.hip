@@ -92,6 +92,7 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
       load8(invstd + c, is);
       load8(scale + c, sc);
       load8(shift + c, sh);
+#pragma unroll 4
       for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
         float dv[8], yv[8], ad[8];
         load8(da + m * ldda + c, dv);
@@ -179,6 +180,7 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
           D[e] = -a1[e] * a2[e] + a1[e] * a3[e] * mu[e] * is[e];
         }
       }
+#pragma unroll 4
       for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
         float dv[8], yv[8], ad[8], o[8];
         load8(da + m * ldda + c, dv);

@@ -172,11 +172,12 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 // rows per block of the row-chunk reductions (RowMap kernels): aim at about
-// 1024 blocks (16..256 rows), so small deep layers still fill the chip
+// 512 blocks (16..1024 rows): small deep layers still fill the chip and the
+// full-resolution layers do not write thousands of partial rows
 static inline int rows_per_part(long M) {
-  const long r = (M + 1023) / 1024;
+  const long r = (M + 511) / 512;
   int p = 16;
-  while (p < r && p < 256) p <<= 1;
+  while (p < r && p < 1024) p <<= 1;
   return p;
 }
 static inline int parts_for(long M) { return (int)((M + rows_per_part(M) - 1) / rows_per_part(M)); }
