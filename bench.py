@@ -109,6 +109,22 @@ CONV_ENTRIES = {
 }
 
 
+def conv_min_bytes(name, a):
+    """Compulsory HBM bytes of one conv-entry launch (each operand touched
+    once): fwd reads x and the packed weights, writes y (f32 pre-BN or T);
+    dgrad reads dy and wT, writes dx (read-modify-write when accumulating).
+    None for the weight gradient (its f32 slabs are an implementation choice)."""
+    if name == 'um_conv2d_dgrad':
+        dt, N, H, W, C, _, _, acc, _, K, R, _, _, _, P, Q = a[:16]
+        es = 4 if dt == 0 else 2
+        return es * (N * P * Q * K + K * R * R * C + N * H * W * C * (2 if acc else 1))
+    if name == 'um_conv2d_fwd':
+        dt, N, H, W, C, _, _, _, _, K, R, _, _, _, P, Q, ydt = a[:17]
+        es = 4 if dt == 0 else 2
+        return es * (N * H * W * C + K * R * R * C) + (4 if ydt == 0 else 2) * N * P * Q * K
+    return None
+
+
 def measure_roofline(m, lf, opt, left, right, scale, dtype):
     """Time every launch of the candidate kernels with HIP events on the
     launch stream (one eager step); the entry with the largest total time is
@@ -139,6 +155,9 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
             table[name] = {'kernel': CONV_ENTRIES[name], 'bound': 'mfma',
                            'achieved': round(ach, 2), 'peak': peak, 'unit': 'TFLOP/s',
                            'frac': round(ach / peak, 4)}
+            mb = [conv_min_bytes(name, a) for a, _, _ in items]
+            if all(b is not None for b in mb):
+                table[name]['min_hbm_bytes_per_launch'] = round(sum(mb) / len(mb))
         table[name].update({'launches_per_step': len(items),
                             'avg_launch_ms': round(tot_ms / len(items), 4),
                             'total_ms_per_step': round(tot_ms, 3),
@@ -147,6 +166,15 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     out = dict(table[dom])
     out['entry'] = dom
     out['traffic'] = None
+    # HBM bytes per launch of this entry from the committed rocprofv3 PMC
+    # passes (tools/pmc_traffic.py: 2*FETCH_SIZE + WRITE_SIZE, separate passes)
+    pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            t = json.load(f)
+        if t.get('entry') == dom:
+            out['traffic'] = round(t['traffic_bytes_per_launch'])
+            out['traffic_unit'] = 'bytes/launch (rocprofv3 PMC, ' + t.get('source', '') + ')'
     out['candidates'] = {k: {kk: v[kk] for kk in ('achieved', 'unit', 'frac', 'avg_launch_ms',
                                                   'launches_per_step', 'total_ms_per_step')}
                          for k, v in table.items()}

@@ -90,3 +90,44 @@ def test_set_lr_reaches_graph():
     after = m.state_dict()
     for k, v in before.items():
         assert torch.equal(v, after[k]), k  # lr 0: Adam leaves weights unchanged
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_wgrad_side_stream_matches_single_stream(dtype):
+    """umamd.overlap.WgradStream (weight gradients on a side stream, joined
+    at the end of backward) gives the same gradients as the one-stream
+    backward from the same state; only the loss backward's float-atomic
+    summation order differs between two runs."""
+    from train.loss import TukraUncertaintyLoss
+    import train.utils as u
+    from umamd.overlap import WgradStream
+    cfg = _cfg()
+    left, right = _uniform_pair(2, 64, 128)
+    left, right = left.to(DEV), right.to(DEV)
+    lf = TukraUncertaintyLoss(**cfg['loss'])
+    m = _model(cfg, dtype).train()
+    named = [(k, p) for k, p in m.named_parameters() if p.requires_grad]
+    params = [p for _, p in named]
+    ov = WgradStream(params)
+    grads = []
+    for use in (False, True):
+        for p in params:
+            p.grad = None
+        pyr = u.scale_pyramid(torch.cat([left, right], 1), 4)
+        d = m(left, 0.3)
+        dl, el = lf(pyr, d, u.reconstruct_pyramid(d, pyr), 0, None)
+        if use:
+            with ov:
+                (dl + el).backward()
+        else:
+            (dl + el).backward()
+        torch.cuda.synchronize()
+        grads.append([p.grad.detach().clone() for p in params])
+    for (k, _), a, b in zip(named, grads[0], grads[1]):
+        d = float((a - b).norm())
+        assert d <= 1e-3 * float(a.norm()) + 1e-5, (k, d, float(a.norm()))
+    for p in params:
+        p.grad = torch.zeros_like(p)
+    with pytest.raises(RuntimeError):
+        with ov:
+            pass

@@ -7,6 +7,7 @@ replays it:
 
   graph 1: pyramid -> model forward -> reconstruct -> fused loss -> backward
            (gradients land in static graph-pool tensors)
+           (weight gradients on a parallel branch, umamd.overlap)
   graph 2: fused Adam over those gradients (pointer table uploaded once,
            step counter and lr read from device memory by the kernel)
 
@@ -19,7 +20,11 @@ all-reduce runs eagerly.
 """
 from __future__ import annotations
 
+import os
+
 import torch
+
+from umamd import overlap
 
 from . import utils as u
 
@@ -31,6 +36,11 @@ class CapturedTrainStep:
             raise TypeError('CapturedTrainStep needs umamd.optim.Adam (graph-replayable)')
         self.model, self.loss_function, self.optimiser = model, loss_function, optimiser
         self.scale, self.scales = float(scale), scales
+        # weight gradients on a side stream beside the dgrad chain (umamd.overlap);
+        # UMAMD_WGRAD_OVERLAP=0 keeps the whole backward on one stream
+        self.overlap = None
+        if os.environ.get('UMAMD_WGRAD_OVERLAP', '1') != '0':
+            self.overlap = overlap.WgradStream(p for p in model.parameters() if p.requires_grad)
         self.left = left.detach().clone().contiguous()
         self.right = right.detach().clone().contiguous()
         cur = torch.cuda.current_stream()
@@ -61,7 +71,11 @@ class CapturedTrainStep:
         disparities = self.model(self.left, self.scale)
         recon = u.reconstruct_pyramid(disparities, pyramid)
         disp_loss, error_loss = self.loss_function(pyramid, disparities, recon, 0, None)
-        (disp_loss + error_loss).backward()
+        if self.overlap is None:
+            (disp_loss + error_loss).backward()
+        else:
+            with self.overlap:
+                (disp_loss + error_loss).backward()
         return disp_loss, error_loss
 
     def __call__(self, left=None, right=None):

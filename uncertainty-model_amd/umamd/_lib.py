@@ -144,8 +144,13 @@ class Recorder:
 
     _active = None
 
-    def __init__(self, names):
+    def __init__(self, names, marker=False):
+        """``marker=True`` brackets each selected launch with a one-cycle
+        ``spin_kernel`` (torch.cuda._sleep) instead of timing it, so a
+        rocprofv3 ``--pmc`` pass can attribute the dispatches in between to
+        the entry (tools/pmc_traffic.py)."""
         self.names = set(names)
+        self.marker = marker
         self.items = []
 
     def __enter__(self):
@@ -170,7 +175,12 @@ def call(name: str, *args, work=None):
     ``work`` (algorithmic FLOPs of this launch) is only kept for a Recorder."""
     fn = getattr(lib(), name)
     rec = Recorder._active
-    if rec is not None and name in rec.names:
+    if rec is not None and name in rec.names and rec.marker:
+        torch.cuda._sleep(1)
+        rc = fn(*args, stream())
+        torch.cuda._sleep(1)
+        rec.items.append((name, args, None, None, work))
+    elif rec is not None and name in rec.names:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()

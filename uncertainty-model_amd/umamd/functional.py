@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
+from . import overlap as _overlap
 from . import packer as _packer
 from ._lib import call, ptr, query
 
@@ -109,7 +110,25 @@ def _conv_dgrad(dy, wT, x_shape, K, R, stride, pad, pad_mode, dx=None, accumulat
 
 
 def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=None):
-    """dW in the reference NCHW layout [Kreal][Creal][R][R] (f32)."""
+    """dW in the reference NCHW layout [Kreal][Creal][R][R] (f32).  Under
+    ``overlap.WgradStream`` it is issued on the side stream (see there)."""
+    ov = _overlap.active()
+    if dw is None:
+        dw = torch.empty((Kreal, Creal, R, R), dtype=torch.float32, device=x.device)
+    if ov is None:
+        _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, ptr(dw), segs)
+        return dw
+    # the queued launch holds dw's address, not the tensor: an extra reference
+    # would make AccumulateGrad copy the (not yet written) gradient on the
+    # launch stream instead of taking it over.  dw stays alive as param.grad.
+    dw.record_stream(ov.stream)
+    dw_ptr = ptr(dw)
+    ov.defer((x, dy), lambda: _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad,
+                                             pad_mode, dw_ptr, segs))
+    return dw
+
+
+def _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw_ptr, segs):
     N, H, W, C = x.shape
     _, P, Q, ldy = dy.shape
     M = N * P * Q
@@ -119,12 +138,9 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
     slabs = torch.empty((splits, K, RRC), dtype=torch.float32, device=x.device)
     call('um_conv2d_wgrad', _dt(x), N, H, W, C, C, ptr(x), K, R, stride, pad, pad_mode, P, Q,
          ptr(dy), ldy, ptr(slabs), splits, work=_conv_flops(N, P, Q, Kreal, R, Creal))
-    if dw is None:
-        dw = torch.empty((Kreal, Creal, R, R), dtype=torch.float32, device=x.device)
     n, a0, b0, l0 = _seg_arrays(segs)
-    call('um_conv_wgrad_reduce_seg', ptr(slabs), splits, K, Kreal, R, C, Creal, ptr(dw), 0,
+    call('um_conv_wgrad_reduce_seg', ptr(slabs), splits, K, Kreal, R, C, Creal, dw_ptr, 0,
          n, a0, b0, l0)
-    return dw
 
 
 def _colred_ws(nparts, C, nv, device):

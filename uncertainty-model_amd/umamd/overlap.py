@@ -1,0 +1,84 @@
+"""Weight gradients on a side HIP stream, overlapped with the data-gradient
+chain of the backward pass.
+
+In the reference backward (autograd over nn.Conv2d, train/train.py:126) each
+conv's weight gradient and data gradient run back to back.  Only the data
+gradient is on the critical path: the next layer's backward needs dx, while
+dW is consumed by the optimiser after the whole backward.  Inside
+``WgradStream`` every ``functional._conv_wgrad`` (the weight-gradient kernel
++ its slab reduce) is issued on a side stream that first waits for the
+launch stream (dy is ready there), so it runs beside the following BN/dgrad
+kernels, which under-fill the chip at this model's channel counts.  Leaving
+the context joins the side stream back into the launch stream, before the
+optimiser reads the gradients.
+
+Inside a HIP graph capture the fork/join becomes parallel graph branches.
+Tensors the side stream reads (x, dy) are marked with ``record_stream`` so
+the caching allocator does not hand their memory to the launch stream while
+the side stream still reads it (during capture it defers those frees to the
+end of capture).
+
+Single-process only (``train.graph.CapturedTrainStep``): DDP's reducer reads
+gradients from its hooks during backward and is left on the launch stream.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+
+class WgradStream:
+    _active: Optional['WgradStream'] = None
+
+    def __init__(self, params=(), batch=None):
+        """``params``: the leaves whose gradients the backward produces.
+        They must have ``.grad is None`` on entry (``zero_grad(set_to_none=
+        True)``): AccumulateGrad then stores the side-stream tensor without a
+        launch-stream kernel reading it before the join."""
+        self.stream = torch.cuda.Stream()
+        self.params = list(params)
+        self.batch = batch or int(os.environ.get('UMAMD_WGRAD_BATCH', '24'))
+        self._launch = None
+        self._pending = []
+
+    def __enter__(self):
+        if WgradStream._active is not None:
+            raise RuntimeError('WgradStream contexts do not nest')
+        if any(p.grad is not None for p in self.params):
+            raise RuntimeError('WgradStream needs gradients set to None before backward '
+                               '(zero_grad(set_to_none=True))')
+        self._launch = torch.cuda.current_stream()
+        WgradStream._active = self
+        return self
+
+    def defer(self, tensors, launch):
+        """Queue one weight gradient (``launch`` issues its kernels on the
+        current stream; ``tensors`` are the ones it touches) and flush the
+        queue onto the side stream every ``batch`` entries: one fork per
+        batch instead of one per conv."""
+        self._pending.append((tensors, launch))
+        if len(self._pending) >= self.batch:
+            self._flush()
+
+    def _flush(self):
+        if not self._pending:
+            return
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            for _, launch in self._pending:
+                launch()
+        for tensors, _ in self._pending:
+            for t in tensors:
+                t.record_stream(self.stream)
+        self._pending = []
+
+    def __exit__(self, *exc):
+        WgradStream._active = None
+        self._flush()
+        self._launch.wait_stream(self.stream)
+
+
+def active() -> Optional[WgradStream]:
+    return WgradStream._active
