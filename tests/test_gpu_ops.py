@@ -388,3 +388,41 @@ def test_up2_concat_adjoint(h, w, gated):
     assert _rel(_nchw(xd.grad), xr.grad) < 1e-5
     if gated:
         assert _rel(gd.grad, gr.grad) < 1e-5
+
+
+# data gradient through the 48/96/160-wide tiles (NC = the conv's input
+# channels: the decoder-concat counts 40/88/160/168/320), against f64 torch on
+# the same bf16/f32 operands, with each shape checked under the odd-width tile
+# and under the 64/128-wide tile it replaces (UMAMD_IG_ODD_BN = 0).  M is large
+# enough that the 128-row plan (not the 64x64 deep-layer plan) is taken.
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [(40, 32, 3, 2, 96, 128), (88, 64, 3, 2, 128, 128),
+                                  (168, 128, 3, 2, 128, 128), (160, 64, 1, 2, 128, 128),
+                                  (320, 256, 3, 2, 64, 96), (72, 32, 1, 2, 128, 160)])
+def test_dgrad_odd_tiles(dtype, case):
+    from umamd import functional as U
+    from umamd._lib import PAD_ZERO, lib
+    C, K, R, N, H, W = case
+    pad = (R - 1) // 2
+    g = torch.Generator().manual_seed(11)
+    w = (torch.rand(K, C, R, R, generator=g) - 0.5) * 0.2
+    dy = torch.randn(N, K, H, W, generator=g)
+    wq = w.to(dtype).double()
+    dyq = dy.to(dtype).double()
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), wq, dyq, padding=pad)
+    _, wT = U._pack(w.to(DEV), C, dtype, wf=False)
+    outs = []
+    for odd in (1, 0):
+        old = lib().um_set_tuning(b'odd_bn', odd)
+        old_h = lib().um_set_tuning(b'halo', 0)
+        try:
+            dx = U._conv_dgrad(_nhwc(dy).to(dtype), wT, (N, H, W, C), K, R, 1, pad, PAD_ZERO)
+            torch.cuda.synchronize()
+        finally:
+            lib().um_set_tuning(b'odd_bn', old)
+            lib().um_set_tuning(b'halo', old_h)
+        outs.append(_nchw(dx))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    for o in outs:
+        assert _rel(o, ref) < tol, _rel(o, ref)
+    assert _rel(outs[0], outs[1]) < tol

@@ -465,7 +465,7 @@ struct Plan {
 
 // tuning knobs (read once; UMAMD_IG_* environment variables for sweeps)
 struct Knobs {
-  int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles;
+  int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles, odd_bn;
   Knobs() {
     auto env = [](const char* n, int d) {
       const char* v = getenv(n);
@@ -478,6 +478,7 @@ struct Knobs {
     split_minsteps = env("UMAMD_IG_SPLIT_MINSTEPS", 8);
     halo = env("UMAMD_HALO", 1);
     halo_min_tiles = env("UMAMD_HALO_MIN_TILES", 256);
+    odd_bn = env("UMAMD_IG_ODD_BN", 1);
   }
 };
 Knobs& knobs() {
@@ -500,13 +501,23 @@ Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes) {
   p.bk = 32;
   if (NC <= 16) { p.bm = 256; p.bn = 16; p.wm = 4; p.wn = 1; }
   else if (NC <= 32) { p.bm = 256; p.bn = 32; p.wm = 4; p.wn = 1; }
+  else if (NC <= 48 && kn.odd_bn) { p.bm = 256; p.bn = 48; p.wm = 4; p.wn = 1; }
   else if (NC <= 64) { p.bm = 256; p.bn = 64; p.wm = 4; p.wn = 1; }
   else if (small_tiles(M, NC)) {
     p.bm = 64; p.bn = 64; p.wm = 2; p.wn = 2;
     if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;
   } else {
+    // 128-row tiles; the column width that pads the fewest columns.  The
+    // data gradient's NC is the conv's INPUT channel count, which after the
+    // decoder concats is 72/88/160/168/320: 96- and 160-wide tiles cut the
+    // padded MFMA work from up to 44 % to at most 12.5 % there.
     p.bm = 128; p.bn = 128; p.wm = 2; p.wn = 2;
-    if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;  // 64 KB of LDS: 2 blocks/CU
+    if (kn.odd_bn) {
+      auto padded = [&](int bn) { return (long)ceil_div(NC, bn) * bn; };
+      if (padded(96) < padded(p.bn)) p.bn = 96;
+      if (padded(160) < padded(p.bn)) p.bn = 160;
+    }
+    if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;  // 64-83 KB of LDS: 1-2 blocks/CU
   }
   p.steps = taps * ((ach + p.bk - 1) / p.bk);
   // Split only grids that leave most CUs idle: the partials cost an f32
@@ -553,6 +564,17 @@ template <typename T>
 int dispatch_tiles(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
   if (p.bn == 16) return launch<T, 32, 256, 16, 4, 1>(a, p, ws, st);
   if (p.bn == 32) return launch<T, 32, 256, 32, 4, 1>(a, p, ws, st);
+  if (p.bn == 48) return launch<T, 32, 256, 48, 4, 1>(a, p, ws, st);
+  if (p.bn == 96) {
+    if constexpr (sizeof(T) == 2)
+      if (p.bk == 64) return launch<T, 64, 128, 96, 2, 2>(a, p, ws, st);
+    return launch<T, 32, 128, 96, 2, 2>(a, p, ws, st);
+  }
+  if (p.bn == 160) {
+    if constexpr (sizeof(T) == 2)
+      if (p.bk == 64) return launch<T, 64, 128, 160, 2, 2>(a, p, ws, st);
+    return launch<T, 32, 128, 160, 2, 2>(a, p, ws, st);
+  }
   if (p.bn == 64 && p.bm == 256) return launch<T, 32, 256, 64, 4, 1>(a, p, ws, st);
   if (p.bm == 64) {
     if constexpr (sizeof(T) == 2)
@@ -599,6 +621,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "split_below")) f = &k.split_below;
   else if (!strcmp(key, "split_target")) f = &k.split_target;
   else if (!strcmp(key, "split_minsteps")) f = &k.split_minsteps;
+  else if (!strcmp(key, "odd_bn")) f = &k.odd_bn;
   if (!f) return -1;
   const int old = *f;
   *f = value;
