@@ -393,8 +393,8 @@ def test_up2_concat_adjoint(h, w, gated):
 # data gradient through the 48/96/160-wide tiles (NC = the conv's input
 # channels: the decoder-concat counts 40/88/160/168/320), against f64 torch on
 # the same bf16/f32 operands, with each shape checked under the odd-width tile
-# and under the 64/128-wide tile it replaces (UMAMD_IG_ODD_BN = 0).  M is large
-# enough that the 128-row plan (not the 64x64 deep-layer plan) is taken.
+# and under the 64/128-wide tile it replaces (UMAMD_IG_ODD_BN = 0), with the
+# 64x64 deep-layer plan switched off so the 128-row plan is taken.
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('case', [(40, 32, 3, 2, 96, 128), (88, 64, 3, 2, 128, 128),
                                   (168, 128, 3, 2, 128, 128), (160, 64, 1, 2, 128, 128),
@@ -415,12 +415,14 @@ def test_dgrad_odd_tiles(dtype, case):
     for odd in (1, 0):
         old = lib().um_set_tuning(b'odd_bn', odd)
         old_h = lib().um_set_tuning(b'halo', 0)
+        old_s = lib().um_set_tuning(b'small', 0)
         try:
             dx = U._conv_dgrad(_nhwc(dy).to(dtype), wT, (N, H, W, C), K, R, 1, pad, PAD_ZERO)
             torch.cuda.synchronize()
         finally:
             lib().um_set_tuning(b'odd_bn', old)
             lib().um_set_tuning(b'halo', old_h)
+            lib().um_set_tuning(b'small', old_s)
         outs.append(_nchw(dx))
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     for o in outs:

@@ -472,10 +472,14 @@ struct Knobs {
       return v ? atoi(v) : d;
     };
     small = env("UMAMD_IG_SMALL", 1);
-    small_tiles = env("UMAMD_IG_SMALL_TILES", 256);
-    split_below = env("UMAMD_IG_SPLIT_BELOW", 160);
-    split_target = env("UMAMD_IG_SPLIT_TARGET", 320);
-    split_minsteps = env("UMAMD_IG_SPLIT_MINSTEPS", 8);
+    // measured on MI355X (bench step, tools/sweep.sh): the deep layers' main
+    // loops are load-latency bound (one double-buffered stage in flight per
+    // block, ~1 us per k-step at 1 block per CU), so more, smaller and split
+    // tiles help: 160/320/8/256 -> 600/1024/4/1024 took 578 -> 599 pairs/s
+    small_tiles = env("UMAMD_IG_SMALL_TILES", 1024);
+    split_below = env("UMAMD_IG_SPLIT_BELOW", 600);
+    split_target = env("UMAMD_IG_SPLIT_TARGET", 1024);
+    split_minsteps = env("UMAMD_IG_SPLIT_MINSTEPS", 4);
     halo = env("UMAMD_HALO", 1);
     halo_min_tiles = env("UMAMD_HALO_MIN_TILES", 256);
     odd_bn = env("UMAMD_IG_ODD_BN", 1);
@@ -520,9 +524,10 @@ Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes) {
     if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;  // 64-83 KB of LDS: 1-2 blocks/CU
   }
   p.steps = taps * ((ach + p.bk - 1) / p.bk);
-  // Split only grids that leave most CUs idle: the partials cost an f32
-  // write + read of splits*M*NC (about 1 us per 8 MB each way), so aim at
-  // ~320 blocks, >= 8 k-steps per split and <= 32 MB of partials.
+  // Split grids that leave CUs with too few blocks to hide load latency: the
+  // partials cost an f32 write + read of splits*M*NC (about 1 us per 8 MB
+  // each way), so aim at ~1024 blocks, >= 4 k-steps per split and <= 32 MB
+  // of partials.
   const long tiles = (long)ceil_div(M, p.bm) * ceil_div(NC, p.bn);
   p.splits = 1;
   if (tiles < kn.split_below && NC % 4 == 0) {
