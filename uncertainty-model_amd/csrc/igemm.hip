@@ -509,7 +509,7 @@ Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes) {
   else if (NC <= 64) { p.bm = 256; p.bn = 64; p.wm = 4; p.wn = 1; }
   else if (small_tiles(M, NC)) {
     p.bm = 64; p.bn = 64; p.wm = 2; p.wn = 2;
-    if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;
+    if (dtype == UM_BF16 && ach % 64 == 0 && (kn.bk64 & 1)) p.bk = 64;
   } else {
     // 128-row tiles; the column width that pads the fewest columns.  The
     // data gradient's NC is the conv's INPUT channel count, which after the
@@ -521,7 +521,7 @@ Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes) {
       if (padded(96) < padded(p.bn)) p.bn = 96;
       if (padded(160) < padded(p.bn)) p.bn = 160;
     }
-    if (dtype == UM_BF16 && ach % 64 == 0) p.bk = 64;  // 64-83 KB of LDS: 1-2 blocks/CU
+    if (dtype == UM_BF16 && ach % 64 == 0 && (kn.bk64 & 2)) p.bk = 64;  // 64-83 KB of LDS: 1-2 blocks/CU
   }
   p.steps = taps * ((ach + p.bk - 1) / p.bk);
   // Split grids that leave CUs with too few blocks to hide load latency: the
