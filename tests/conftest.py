@@ -14,3 +14,11 @@ GOLDEN = os.path.join(REPO, 'tests', 'golden')
 
 def pytest_configure(config):
     config.addinivalue_line('markers', 'gpu: needs an MI355X (runs the HIP path)')
+
+
+def pytest_sessionstart(session):
+    """Build libumamd.so once per session (content-hash staleness): a compile
+    error then fails the session with hipcc's own message."""
+    from umamd import _build
+    if _build.needs_build() and _build.can_build():
+        _build.build()

@@ -465,7 +465,7 @@ struct Plan {
 
 // tuning knobs (read once; UMAMD_IG_* environment variables for sweeps)
 struct Knobs {
-  int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles, odd_bn;
+  int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles, odd_bn, bk64;
   Knobs() {
     auto env = [](const char* n, int d) {
       const char* v = getenv(n);
@@ -483,6 +483,8 @@ struct Knobs {
     halo = env("UMAMD_HALO", 1);
     halo_min_tiles = env("UMAMD_HALO_MIN_TILES", 256);
     odd_bn = env("UMAMD_IG_ODD_BN", 1);
+    // bit 0: 64-deep k-steps for the 64x64 tiles, bit 1: for the 128-row tiles
+    bk64 = env("UMAMD_IG_BK64", 3);
   }
 };
 Knobs& knobs() {
@@ -627,6 +629,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "split_target")) f = &k.split_target;
   else if (!strcmp(key, "split_minsteps")) f = &k.split_minsteps;
   else if (!strcmp(key, "odd_bn")) f = &k.odd_bn;
+  else if (!strcmp(key, "bk64")) f = &k.bk64;
   if (!f) return -1;
   const int old = *f;
   *f = value;

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -48,6 +49,33 @@ def _compile(src):
     return obj
 
 
+STAMP = LIB + '.stamp'
+
+
+def _digest() -> str:
+    """Content hash of every source and header (mtimes do not survive every
+    copy of the tree, so staleness of the library is judged on content)."""
+    h = hashlib.sha256()
+    for f in sorted(_sources() + _headers()):
+        h.update(os.path.basename(f).encode())
+        with open(f, 'rb') as fh:
+            h.update(fh.read())
+    h.update(' '.join(FLAGS).encode())
+    return h.hexdigest()
+
+
+def needs_build() -> bool:
+    """True when the library is missing or was built from other sources."""
+    if not os.path.isfile(LIB) or not os.path.isfile(STAMP):
+        return True
+    with open(STAMP) as fh:
+        return fh.read().strip() != _digest()
+
+
+def can_build() -> bool:
+    return os.path.isfile(HIPCC) and os.access(HIPCC, os.X_OK)
+
+
 def build(verbose: bool = False) -> str:
     os.makedirs(OBJDIR, exist_ok=True)
     srcs = _sources()
@@ -59,6 +87,8 @@ def build(verbose: bool = False) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f'link failed:\n{r.stderr}')
+    with open(STAMP, 'w') as fh:
+        fh.write(_digest() + '\n')
     if verbose:
         print(f'built {LIB}')
     return LIB

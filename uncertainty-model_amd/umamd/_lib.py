@@ -112,9 +112,17 @@ def lib() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.isfile(LIB_PATH):
-        raise UmamdError(f'{LIB_PATH} not found: build it with '
-                         f'`python uncertainty-model_amd/umamd/_build.py` (hipcc, gfx950)')
+    from . import _build
+    if _build.needs_build():
+        # missing or older than its sources: build now so a compile error
+        # surfaces with hipcc's own message instead of "not found"
+        if not _build.can_build():
+            raise UmamdError(f'{LIB_PATH} is missing or stale and hipcc is not available to '
+                             f'rebuild it (run `python uncertainty-model_amd/umamd/_build.py`)')
+        try:
+            _build.build()
+        except RuntimeError as e:
+            raise UmamdError(f'building {LIB_PATH} failed:\n{e}') from None
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIG.items():
         fn = getattr(L, name)
