@@ -92,13 +92,17 @@ def step(m, lf, opt, left, right, scale):
 
 
 # ------------------------------------------------------------- roofline ----
-def loss_bwd_bytes(N, H, W):
-    """Algorithmic HBM bytes of one fused loss-backward launch at an h x w
-    scale: per pixel 6 f32 image reads + 6 f32 recon reads (the SSIM stencil)
-    + 4 f32 prediction reads + 2 f32 error-map reads + 4 f32 gradient writes.
-    (SURVEY 8d prices the fused stack at 56 B/px all-f32 without the recon;
-    this kernel also reads the saved recon and error map.)"""
-    return N * H * W * 4 * (6 + 6 + 4 + 2 + 4)
+def loss_pixels(n, N, H, W):
+    """pixels summed over the n pyramid levels of one fused-loss launch"""
+    return sum(N * (H >> i) * (W >> i) for i in range(n))
+
+
+# Algorithmic HBM bytes per pixel of the fused all-scale loss launches (f32):
+# forward reads the 6 image channels + the 4 prediction channels; backward
+# also writes the 4 gradient channels.  SURVEY 8d prices the whole fused
+# stack (fwd + bwd as one pass) at 56 B/px all-f32.
+LOSS_BYTES_PER_PX = {'um_loss_fwd': 4 * (6 + 4), 'um_loss_bwd': 4 * (6 + 4 + 4)}
+LOSS_KERNELS = {'um_loss_fwd': 'loss_fwd_kernel', 'um_loss_bwd': 'loss_bwd_kernel'}
 
 
 CONV_ENTRIES = {
@@ -131,7 +135,7 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     the dominant kernel.  Conv work = algorithmic FLOPs with the real channel
     counts (2*N*P*Q*K*R*R*C per pass, attached at each call site)."""
     from umamd import _lib
-    rec = _lib.Recorder(set(CONV_ENTRIES) | {'um_loss_bwd_scale'})
+    rec = _lib.Recorder(set(CONV_ENTRIES) | set(LOSS_KERNELS))
     with rec:
         step(m, lf, opt, left, right, scale)
     torch.cuda.synchronize()
@@ -142,12 +146,13 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     table = {}
     for name, items in groups.items():
         tot_ms = sum(ms for _, ms, _ in items)
-        if name == 'um_loss_bwd_scale':
-            # args: img, rec, pred, pld, N, H, W, ...
-            work = sum(loss_bwd_bytes(a[4], a[5], a[6]) for a, _, _ in items)
+        if name in LOSS_KERNELS:
+            # args: nscales, N, H, W, ...
+            work = sum(LOSS_BYTES_PER_PX[name] * loss_pixels(a[0], a[1], a[2], a[3])
+                       for a, _, _ in items)
             ach = work / (tot_ms * 1e-3) / 1e9
-            table[name] = {'kernel': 'loss_bwd_kernel', 'bound': 'hbm', 'achieved': round(ach, 1),
-                           'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            table[name] = {'kernel': LOSS_KERNELS[name], 'bound': 'hbm',
+                           'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                            'frac': round(ach / HBM_PEAK_GBS, 4)}
         else:
             work = sum(w for _, _, w in items)
@@ -178,6 +183,18 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     out['candidates'] = {k: {kk: v[kk] for kk in ('achieved', 'unit', 'frac', 'avg_launch_ms',
                                                   'launches_per_step', 'total_ms_per_step')}
                          for k, v in table.items()}
+    if all(k in groups for k in LOSS_KERNELS):
+        # the fused loss stack (forward + backward launches) priced as SURVEY
+        # 8d does: 56 B/px all-f32 (6 image + 4 prediction reads, 4 gradient
+        # writes) over every scale
+        a0 = groups['um_loss_fwd'][0][0]
+        px = loss_pixels(a0[0], a0[1], a0[2], a0[3])
+        t = table['um_loss_fwd']['total_ms_per_step'] + table['um_loss_bwd']['total_ms_per_step']
+        ach = 56 * px / (t * 1e-3) / 1e9
+        out['loss_stack'] = {'kernels': 'loss_fwd_kernel + loss_bwd_kernel', 'bound': 'hbm',
+                             'bytes_per_px': 56, 'pixels': px, 'ms_per_step': round(t, 4),
+                             'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                             'frac': round(ach / HBM_PEAK_GBS, 4)}
     return out
 
 

@@ -250,23 +250,43 @@ int um_se_mlp_bwd(int N, int C, int R, const float* ds, const float* s, const fl
  * predictions NHWC f32 [N][H][W][pld] (d_L, d_R, sigma_L, sigma_R).
  * loss_type: 0 l1, 1 bayesian, 2 log_bayesian (train/loss.py:364-375).
  */
-int um_pyramid_level(const float* x, int NC, int H, int W, float* out, int h, int w,
-                     hipStream_t stream);
+/* image pyramid, every level in ONE launch: out[l] = [NC][H>>l][W>>l], level 0
+ * an exact copy (F.interpolate(bilinear, align_corners=True), utils.py:27-50) */
+int um_pyramid(const float* x, int NC, int H, int W, int nlevels, float* const* out,
+               hipStream_t stream);
+/* reconstruct (utils.py:65-97): out = grid_sample(img, linspace grid + sign*disp) */
 int um_warp(const float* img, int N, int C, int H, int W, const float* disp, long disp_sn,
             long disp_sp, float sign, float* out, hipStream_t stream);
-int um_loss_parts(int N, int H, int W);
-int um_loss_fwd_scale(const float* img, const float* rec, const float* pred, int pld, int N,
-                      int H, int W, float alpha, int loss_type, float esw, float ecw,
-                      float* D, float* e, float* parts, hipStream_t stream);
-int um_loss_finalize(int nscales, const float* const* parts, const int* nparts,
-                     const double* npix, float w_wssim, float w_cons, float w_smooth,
-                     float w_err, float esw, float ecw, int loss_type, float* out,
+/* its adjoint w.r.t. the disparity (the image is data): gdisp = sum_c gout_c d(warp_c)/d(disp) */
+int um_warp_bwd(const float* img, int N, int C, int H, int W, const float* disp, long disp_sn,
+                long disp_sp, float sign, const float* gout, float* gdisp, long g_sn, long g_sp,
+                hipStream_t stream);
+/* reconstruct_pyramid (utils.py:112-135), every level and both views in ONE
+ * launch: out[l] = [N][6][H>>l][W>>l]; pred[l] strided [N][4][h][w] with
+ * pred_strides[3l..3l+2] = (image, channel, pixel) strides in elements */
+int um_recon_pyramid(int nlevels, int N, int H, int W, const float* const* img,
+                     const float* const* pred, const long* pred_strides, float* const* out,
                      hipStream_t stream);
-int um_loss_bwd_scale(const float* img, const float* rec, const float* pred, int pld, int N,
-                      int H, int W, float alpha, int loss_type, float esw, float ecw,
-                      const float* e, const float* gout, float w_wssim, float w_cons,
-                      float w_smooth, float w_err, float smooth_div, float* dpred,
-                      hipStream_t stream);
+/* TukraUncertaintyLoss.forward (loss.py:512-568) over every scale in ONE launch:
+ * img[s] = pyramid level s [N][6][H>>s][W>>s], pred[s] NHWC [N][H>>s][W>>s][4].
+ * The recon is re-derived in the kernel (warp of the opposite view).
+ * ws: um_loss_ws() bytes of f64 scratch; out[6] = disp_loss, error_loss,
+ * wssim, consistency, smoothness, error term; emap_last (optional) = the last
+ * scale's error map [N][2][h][w] (WeightedSSIMLoss.previous_image_error). */
+long um_loss_ws(int nscales, int N, int H, int W);
+int um_loss_fwd(int nscales, int N, int H, int W, const float* const* img,
+                const float* const* pred, float alpha, int loss_type, float esw, float ecw,
+                float w_wssim, float w_cons, float w_smooth, float w_err, double* ws,
+                float* emap_last, float* out, hipStream_t stream);
+/* its backward in ONE launch: dpred[s] NHWC [N][h][w][4] = d(gout[0]*disp_loss +
+ * gout[1]*error_loss)/d pred[s] (gout on the device) */
+int um_loss_bwd(int nscales, int N, int H, int W, const float* const* img,
+                const float* const* pred, float alpha, int loss_type, float esw, float ecw,
+                float w_wssim, float w_cons, float w_smooth, float w_err, const float* gout,
+                float* const* dpred, hipStream_t stream);
+/* WeightedSSIMLoss.image_error (loss.py:96-131) of an explicit recon: out [N][2][H][W] */
+int um_image_error(const float* img, const float* rec, int N, int H, int W, float alpha,
+                   float* out, hipStream_t stream);
 
 /* ---------------------------------------------------------------- adam ---
  * torch.optim.Adam step, reference train/train.py:228-229.

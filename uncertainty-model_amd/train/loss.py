@@ -1,11 +1,11 @@
 """Loss functions (reference train/loss.py), HIP-backed.
 
 ``TukraUncertaintyLoss.forward`` (reference :512-568) runs the fused umamd
-loss stack: per scale a DSSIM-map kernel and a per-pixel terms kernel in the
-forward, and one backward kernel producing d(total)/d(prediction) for all
-four channels, including the WSSIM term's path through the warp, both L-R
-consistency terms (with the scatter into the warped disparity), the
-edge-aware smoothness and the reprojection-error NLL.
+loss stack: ONE forward launch over every scale (the six loss terms, reduced
+on the device) and ONE backward launch producing d(total)/d(prediction) for
+all four channels of every scale, including the WSSIM term's path through
+the warp, both L-R consistency terms (with the scatter into the warped
+disparity), the edge-aware smoothness and the reprojection-error NLL.
 
 The sub-loss modules keep the reference's names and constructor kwargs so
 configs and attribute access (``loss.wssim.previous_image_error``,
@@ -48,6 +48,14 @@ class WeightedSSIMLoss(_FusedOnly):
     def previous_image_error(self) -> Tensor:
         """Error map [B,2,h,w] of the last scale evaluated (reference :38-41)."""
         return self._previous_image_error
+
+    def image_error(self, images: Tensor, recon: Tensor) -> Tensor:
+        """Per-pixel alpha*DSSIM(upsampled) + (1-alpha)*L1, channel mean per
+        view -> [B,2,H,W] (reference :96-131); no gradient (evaluation)."""
+        if torch.is_grad_enabled() and (images.requires_grad or recon.requires_grad):
+            raise NotImplementedError('umamd WeightedSSIMLoss.image_error has no autograd '
+                                      '(training evaluates it inside TukraUncertaintyLoss)')
+        return LF.image_error(images, recon, self.alpha)
 
 
 class ConsistencyLoss(_FusedOnly):
@@ -127,17 +135,15 @@ class TukraUncertaintyLoss(nn.Module):
                 discriminator: Optional[Module] = None):
         if discriminator is not None:
             raise NotImplementedError('umamd: adversarial loss terms are not implemented yet')
-        n = len(predictions)
         for p, im, r in zip(predictions, image_pyramid, recon_pyramid):
             tag = getattr(r, '_umamd_recon', None)
             if tag is None or tag != (id(p), id(im)):
                 raise ValueError('TukraUncertaintyLoss (umamd): recon_pyramid must be '
                                  'train.utils.reconstruct_pyramid(predictions, image_pyramid) '
-                                 '(the fused backward differentiates through that warp)')
-        outs = LF.tukra_loss(self._cfg(), list(predictions), list(image_pyramid),
-                             list(recon_pyramid))
-        disp_loss, error_loss, terms = outs[0], outs[1], outs[2]
-        self.wssim._previous_image_error = outs[3 + n - 1]
-        self.last_error_maps = list(outs[3:3 + n])
+                                 '(the fused kernels re-derive that warp and differentiate '
+                                 'through it)')
+        disp_loss, error_loss, terms, emap = LF.tukra_loss(self._cfg(), list(predictions),
+                                                           list(image_pyramid))
+        self.wssim._previous_image_error = emap
         self.last_terms = terms  # [disp, error, wssim, consistency, smoothness, error-term]
         return disp_loss, error_loss

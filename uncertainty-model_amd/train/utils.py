@@ -1,9 +1,10 @@
 """Training utilities (reference train/utils.py), HIP-backed where they are on
 the hot path:
 
-  scale_pyramid        utils.py:27-50   -> um_pyramid_level
-  reconstruct(+L/R)    utils.py:65-109  -> um_warp
-  reconstruct_pyramid  utils.py:112-135 -> um_warp (tagged for the fused loss)
+  scale_pyramid        utils.py:27-50   -> um_pyramid (every level, one launch)
+  reconstruct(+L/R)    utils.py:65-109  -> um_warp / um_warp_bwd
+  reconstruct_pyramid  utils.py:112-135 -> um_recon_pyramid (one launch; tagged
+                                           for the fused loss)
   l1_loss, detach_pyramid, concatenate_pyramids, adjust_disparity,
   adjust_learning_rate, prepare_state_dict: host-side, same semantics.
 """

@@ -88,13 +88,15 @@ _SIG = {
     'um_channel_mean': (_I, [_I, _I, _L, _I, _P, _I, _P, 's']),
     'um_se_mlp_fwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, 's']),
     'um_se_mlp_bwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, 's']),
-    'um_pyramid_level': (_I, [_P, _I, _I, _I, _P, _I, _I, 's']),
+    'um_pyramid': (_I, [_P, _I, _I, _I, _I, _P, 's']),
     'um_warp': (_I, [_P, _I, _I, _I, _I, _P, _L, _L, _F, _P, 's']),
-    'um_loss_parts': (_I, [_I, _I, _I]),
-    'um_loss_fwd_scale': (_I, [_P, _P, _P, _I, _I, _I, _I, _F, _I, _F, _F, _P, _P, _P, 's']),
-    'um_loss_finalize': (_I, [_I, _P, _P, _P, _F, _F, _F, _F, _F, _F, _I, _P, 's']),
-    'um_loss_bwd_scale': (_I, [_P, _P, _P, _I, _I, _I, _I, _F, _I, _F, _F, _P, _P, _F, _F, _F,
-                               _F, _F, _P, 's']),
+    'um_warp_bwd': (_I, [_P, _I, _I, _I, _I, _P, _L, _L, _F, _P, _P, _L, _L, 's']),
+    'um_recon_pyramid': (_I, [_I, _I, _I, _I, _P, _P, _P, _P, 's']),
+    'um_loss_ws': (_L, [_I, _I, _I, _I]),
+    'um_loss_fwd': (_I, [_I, _I, _I, _I, _P, _P, _F, _I, _F, _F, _F, _F, _F, _F, _P, _P, _P,
+                         's']),
+    'um_loss_bwd': (_I, [_I, _I, _I, _I, _P, _P, _F, _I, _F, _F, _F, _F, _F, _F, _P, _P, 's']),
+    'um_image_error': (_I, [_P, _P, _I, _I, _I, _F, _P, 's']),
     'um_adam_chunk': (_I, []),
     'um_adam_step': (_I, [_P, _P, _I, _F, _F, _F, _F, _F, _I, 's']),
     'um_adam_step_dev': (_I, [_P, _P, _I, _F, _P, _F, _F, _F, _F, _P, 's']),

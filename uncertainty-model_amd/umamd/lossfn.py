@@ -1,22 +1,28 @@
 """Loss-stack autograd functions over the umamd C ABI.
 
-  * ``scale_pyramid``       reference train/utils.py:27-50
+  * ``scale_pyramid``       reference train/utils.py:27-50, every level in one launch
   * ``reconstruct``         reference train/utils.py:65-97 (+ _left/_right 100-109)
-  * ``reconstruct_pyramid`` reference train/utils.py:112-135
+  * ``reconstruct_pyramid`` reference train/utils.py:112-135, one launch
   * ``tukra_loss``          reference train/loss.py:512-568 with the sub-losses
-                            of loss.py:15-264,340-434, fused per scale into a
-                            forward kernel pair (DSSIM map + per-pixel terms)
-                            and one backward kernel that produces the gradient
-                            w.r.t. all four prediction channels, including the
-                            WSSIM term's path through the bilinear warp.
+                            of loss.py:15-264,340-434: ONE forward launch over
+                            every scale (the six terms, finished on the device)
+                            and ONE backward launch producing the gradient
+                            w.r.t. all four prediction channels of every scale,
+                            including the WSSIM term's path through the warp.
+  * ``image_error``         WeightedSSIMLoss.image_error (loss.py:96-131) of an
+                            explicit recon (evaluation)
 
 Images are NCHW f32; predictions are the model's disparity tensors (logical
-[N,4,h,w], stored channels-last).  Recon tensors are produced by
-``reconstruct_pyramid`` and tagged; the fused loss needs them to be exactly
-warp(pred, pyramid) -- which is what train/train.py passes (train.py:122-124).
+[N,4,h,w], stored channels-last).  The fused loss re-derives the recon from
+the pyramid and the predictions inside its kernels, so the recon tensors it is
+given must be exactly ``reconstruct_pyramid(predictions, pyramid)`` -- which
+is what train/train.py passes (reference train.py:122-124); they are tagged
+and checked.  The recon tensors are still real (``reconstruct_pyramid`` runs
+its own launch) and differentiable w.r.t. the disparities (adversarial terms).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List, Sequence
 
 import torch
@@ -25,6 +31,7 @@ from . import _lib as L
 from ._lib import call, ptr, query
 
 LOSS_TYPES = {'l1': 0, 'bayesian': 1, 'log_bayesian': 2}
+MAX_LEVELS = 6
 
 
 def _f32c(t: torch.Tensor) -> torch.Tensor:
@@ -34,16 +41,19 @@ def _f32c(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def _parr(ts) -> ctypes.Array:
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
 def scale_pyramid(x: torch.Tensor, scales: int) -> List[torch.Tensor]:
     L.require_device(x)
+    if not 1 <= scales <= MAX_LEVELS:
+        raise L.UmamdError(f'scale_pyramid: {scales} scales (1..{MAX_LEVELS})')
     xc = _f32c(x)
     N, C, H, W = xc.shape
-    out = []
-    for i in range(scales):
-        h, w = H // 2 ** i, W // 2 ** i
-        o = torch.empty((N, C, h, w), dtype=torch.float32, device=x.device)
-        call('um_pyramid_level', ptr(xc), N * C, H, W, ptr(o), h, w)
-        out.append(o)
+    out = [torch.empty((N, C, H >> i, W >> i), dtype=torch.float32, device=x.device)
+           for i in range(scales)]
+    call('um_pyramid', ptr(xc), N * C, H, W, scales, _parr(out))
     return out
 
 
@@ -55,50 +65,131 @@ def _pred_nhwc(p: torch.Tensor) -> torch.Tensor:
     return v
 
 
+def _disp_strides(d: torch.Tensor):
+    """(tensor, image stride, pixel stride) such that element (n, 0, y, x) of
+    the [N,1,H,W] view is at data_ptr + n*sn + (y*W + x)*sp (NCHW planes and
+    NHWC channel slices both qualify)."""
+    W = d.shape[-1]
+    sn, _, sy, sx = d.stride()
+    if sy != W * sx:
+        d = d.contiguous()
+        sn, _, sy, sx = d.stride()
+    return d, sn, sx
+
+
 class _WarpFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, disp, img, sign: float):
         L.require_device(img)
-        ctx.set_materialize_grads(False)
         imgc = _f32c(img)
         N, C, H, W = imgc.shape
         d = disp.detach()
         if d.dtype != torch.float32:
             d = d.float()
-        # element (n, 0, y, x) at d.data_ptr + n*sn + (y*W + x)*sp requires
-        # uniform pixel stride: true for NCHW planes and NHWC channel slices
-        sn, sc, sy, sx = d.stride()
-        if sy != W * sx:
-            d = d.contiguous()
-            sn, sc, sy, sx = d.stride()
+        d, sn, sp = _disp_strides(d)
         out = torch.empty((N, C, H, W), dtype=torch.float32, device=img.device)
-        call('um_warp', ptr(imgc), N, C, H, W, d.data_ptr(), sn, sx, float(sign), ptr(out))
+        call('um_warp', ptr(imgc), N, C, H, W, d.data_ptr(), sn, sp, float(sign), ptr(out))
+        ctx.sign = float(sign)
+        ctx.save_for_backward(d, imgc)
+        ctx.dshape = disp.shape
+        ctx.ddtype = disp.dtype
         return out
 
     @staticmethod
     def backward(ctx, g):
-        if g is None:
-            return None, None, None
-        raise NotImplementedError(
-            'gradient through reconstruct() is provided by TukraUncertaintyLoss directly '
-            '(fused); a standalone warp backward (adversarial path) is not implemented yet')
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError('umamd reconstruct(): gradient w.r.t. the image (a data '
+                                      'tensor in every reference call site) is not implemented')
+        d, imgc = ctx.saved_tensors
+        N, C, H, W = imgc.shape
+        gd = torch.empty((N, 1, H, W), dtype=torch.float32, device=g.device)
+        _, sn, sp = _disp_strides(d)
+        call('um_warp_bwd', ptr(imgc), N, C, H, W, d.data_ptr(), sn, sp, ctx.sign,
+             ptr(_f32c(g)), ptr(gd), H * W, 1)
+        return gd.to(ctx.ddtype).reshape(ctx.dshape), None, None
 
 
 def reconstruct(disparity: torch.Tensor, opposite_image: torch.Tensor, sign: float = 1.0):
     return _WarpFn.apply(disparity, opposite_image, sign)
 
 
+class _ReconPyramidFn(torch.autograd.Function):
+    """Every level of reconstruct_pyramid in one launch; backward = the warp
+    adjoint w.r.t. d_L (channel 0) and d_R (channel 1)."""
+
+    @staticmethod
+    def forward(ctx, n, *tensors):
+        disps, pyr = tensors[:n], [_f32c(t) for t in tensors[n:]]
+        N, _, H, W = pyr[0].shape
+        dev = pyr[0].device
+        ds, strides = [], []
+        for i, d in enumerate(disps):
+            if d.shape[0] != N or d.shape[2:] != (H >> i, W >> i) or d.shape[1] < 2:
+                raise L.UmamdError(f'reconstruct_pyramid: level {i} disparity {tuple(d.shape)} '
+                                   f'vs pyramid {tuple(pyr[i].shape)}')
+            dd = d.detach()
+            if dd.dtype != torch.float32:
+                dd = dd.float()
+            dd, sn, sp = _disp_strides(dd)
+            ds.append(dd)
+            strides += [sn, dd.stride(1), sp]
+        out = [torch.empty((N, 6, H >> i, W >> i), dtype=torch.float32, device=dev)
+               for i in range(n)]
+        sarr = (ctypes.c_long * len(strides))(*strides)
+        call('um_recon_pyramid', n, N, H, W, _parr(pyr), _parr(ds), sarr, _parr(out))
+        ctx.n = n
+        ctx.meta = [(d.shape, d.dtype) for d in disps]
+        ctx.save_for_backward(*ds, *pyr)
+        return tuple(out)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        n = ctx.n
+        sv = ctx.saved_tensors
+        ds, pyr = sv[:n], sv[n:]
+        grads = []
+        for i in range(n):
+            g = gouts[i]
+            shape, dtype = ctx.meta[i]
+            if g is None or not ctx.needs_input_grad[1 + i]:
+                grads.append(None)
+                continue
+            g = _f32c(g)
+            N, _, h, w = pyr[i].shape
+            gd = torch.zeros((N, h, w, shape[1]), dtype=torch.float32, device=g.device)
+            _, sn, sp = _disp_strides(ds[i])
+            cs = ds[i].stride(1)
+            # left recon = warp(right image, -d_L); right recon = warp(left image, +d_R)
+            for v, (img, gsl, sign) in enumerate(((pyr[i][:, 3:6], g[:, 0:3], -1.0),
+                                                  (pyr[i][:, 0:3], g[:, 3:6], 1.0))):
+                call('um_warp_bwd', ptr(img.contiguous()), N, 3, h, w,
+                     ds[i].data_ptr() + v * cs * 4, sn, sp, sign, ptr(gsl.contiguous()),
+                     gd.data_ptr() + v * 4, h * w * shape[1], shape[1])
+            grads.append(gd.permute(0, 3, 1, 2).to(dtype))
+        return (None, *grads, *([None] * n))
+
+
 def reconstruct_pyramid(disparities: Sequence[torch.Tensor],
                         pyramid: Sequence[torch.Tensor]) -> List[torch.Tensor]:
-    out = []
-    for d, im in zip(disparities, pyramid):
-        # left recon = warp(right image, -d_L); right recon = warp(left image, d_R)
-        lr = reconstruct(d[:, 0:1], im[:, 3:6], -1.0)
-        rr = reconstruct(d[:, 1:2], im[:, 0:3], 1.0)
-        r = torch.cat([lr, rr], 1)
+    n = min(len(disparities), len(pyramid))
+    if not 1 <= n <= MAX_LEVELS:
+        raise L.UmamdError(f'reconstruct_pyramid: {n} levels (1..{MAX_LEVELS})')
+    L.require_device(pyramid[0])
+    out = list(_ReconPyramidFn.apply(n, *disparities[:n], *[p.detach() for p in pyramid[:n]]))
+    for d, im, r in zip(disparities, pyramid, out):
         r._umamd_recon = (id(d), id(im))
-        out.append(r)
     return out
+
+
+def _check_levels(preds, pyr):
+    N, _, H, W = pyr[0].shape
+    for i, (p, im) in enumerate(zip(preds, pyr)):
+        want = (N, H >> i, W >> i)
+        if tuple(im.shape) != (N, 6, H >> i, W >> i) or \
+                (p.shape[0], p.shape[1], p.shape[2]) != want or p.shape[3] != 4:
+            raise L.UmamdError(f'tukra_loss: level {i}: pyramid {tuple(im.shape)}, prediction '
+                               f'(NHWC) {tuple(p.shape)}; expected [N,6,H>>i,W>>i] / [N,4,...]')
+    return N, H, W
 
 
 class TukraLossFn(torch.autograd.Function):
@@ -106,63 +197,57 @@ class TukraLossFn(torch.autograd.Function):
     def forward(ctx, cfg, n, *tensors):
         preds = [_pred_nhwc(t) for t in tensors[:n]]
         pyr = [_f32c(t) for t in tensors[n:2 * n]]
-        rec = [_f32c(t) for t in tensors[2 * n:3 * n]]
+        N, H, W = _check_levels(preds, pyr)
         dev = preds[0].device
-        parts, nparts, npix, emaps = [], [], [], []
-        for i in range(n):
-            N, H, W, pld = preds[i].shape
-            D = torch.empty((N, 2, H - 2, W - 2), dtype=torch.float32, device=dev)
-            e = torch.empty((N, 2, H, W), dtype=torch.float32, device=dev)
-            np_ = query('um_loss_parts', N, H, W)
-            pt = torch.empty((np_, 8), dtype=torch.float32, device=dev)
-            call('um_loss_fwd_scale', ptr(pyr[i]), ptr(rec[i]), ptr(preds[i]), pld, N, H, W,
-                 cfg['alpha'], cfg['loss_type'], cfg['esw'], cfg['ecw'], ptr(D), ptr(e), ptr(pt))
-            parts.append(pt)
-            nparts.append(np_)
-            npix.append(float(N * H * W))
-            emaps.append(e)
+        ws = torch.empty((max(query('um_loss_ws', n, N, H, W), 8) // 8,), dtype=torch.float64,
+                         device=dev)
+        emap = torch.empty((N, 2, H >> (n - 1), W >> (n - 1)), dtype=torch.float32, device=dev)
         out = torch.empty(6, dtype=torch.float32, device=dev)
-        import ctypes
-        parr = (ctypes.c_void_p * n)(*[p.data_ptr() for p in parts])
-        narr = (ctypes.c_int * n)(*nparts)
-        darr = (ctypes.c_double * n)(*npix)
-        call('um_loss_finalize', n, parr, narr, darr, cfg['w_wssim'], cfg['w_cons'],
-             cfg['w_smooth'], cfg['w_err'], cfg['esw'], cfg['ecw'], cfg['loss_type'], ptr(out))
+        call('um_loss_fwd', n, N, H, W, _parr(pyr), _parr(preds), cfg['alpha'],
+             cfg['loss_type'], cfg['esw'], cfg['ecw'], cfg['w_wssim'], cfg['w_cons'],
+             cfg['w_smooth'], cfg['w_err'], ptr(ws), ptr(emap), ptr(out))
         ctx.cfg = cfg
         ctx.n = n
-        ctx.save_for_backward(*preds, *pyr, *rec, *emaps)
-        ctx.shapes = [t.shape for t in tensors[:n]]
+        ctx.geom = (N, H, W)
+        ctx.save_for_backward(*preds, *pyr)
         dl = out[0].clone()
         el = out[1].clone()
-        ctx.mark_non_differentiable(out)
-        for e in emaps:
-            ctx.mark_non_differentiable(e)
-        return (dl, el, out, *emaps)
+        ctx.mark_non_differentiable(out, emap)
+        return dl, el, out, emap
 
     @staticmethod
     def backward(ctx, gd, ge, *unused):
         cfg, n = ctx.cfg, ctx.n
+        N, H, W = ctx.geom
         sv = ctx.saved_tensors
-        preds, pyr, rec, emaps = sv[:n], sv[n:2 * n], sv[2 * n:3 * n], sv[3 * n:]
+        preds, pyr = sv[:n], sv[n:2 * n]
         dev = preds[0].device
-        gout = torch.stack([gd.reshape(()).float(), ge.reshape(()).float()]).contiguous()
-        grads = []
-        for i in range(n):
-            N, H, W, pld = preds[i].shape
-            # the kernel stores channels 0-3 of every pixel; only padding needs zeros
-            dp = (torch.empty if pld == 4 else torch.zeros)((N, H, W, pld), dtype=torch.float32,
-                                                             device=dev)
-            call('um_loss_bwd_scale', ptr(pyr[i]), ptr(rec[i]), ptr(preds[i]), pld, N, H, W,
-                 cfg['alpha'], cfg['loss_type'], cfg['esw'], cfg['ecw'], ptr(emaps[i]),
-                 ptr(gout), cfg['w_wssim'], cfg['w_cons'], cfg['w_smooth'], cfg['w_err'],
-                 float(2 ** i), ptr(dp))
-            grads.append(dp.permute(0, 3, 1, 2))  # logical NCHW, NHWC memory
-        return (None, None, *grads, *([None] * (2 * n)))
+        zero = torch.zeros((), dtype=torch.float32, device=dev)
+        gout = torch.stack([(gd if gd is not None else zero).reshape(()).float(),
+                            (ge if ge is not None else zero).reshape(()).float()]).contiguous()
+        grads = [torch.empty((N, H >> i, W >> i, 4), dtype=torch.float32, device=dev)
+                 for i in range(n)]
+        call('um_loss_bwd', n, N, H, W, _parr(pyr), _parr(preds), cfg['alpha'],
+             cfg['loss_type'], cfg['esw'], cfg['ecw'], cfg['w_wssim'], cfg['w_cons'],
+             cfg['w_smooth'], cfg['w_err'], ptr(gout), _parr(grads))
+        return (None, None, *[g.permute(0, 3, 1, 2) for g in grads], *([None] * n))
 
 
-def tukra_loss(cfg: dict, preds, pyramid, recon):
-    """The fused backward differentiates through the warp itself, so the
-    recon tensors enter as plain (detached) data."""
+def tukra_loss(cfg: dict, preds, pyramid):
+    """Returns (disp_loss, error_loss, terms[6], last-scale error map).  The
+    backward differentiates through the warp itself (the recon is re-derived)."""
     n = len(preds)
-    return TukraLossFn.apply(cfg, n, *preds, *[p.detach() for p in pyramid],
-                             *[r.detach() for r in recon])
+    if not 1 <= n <= MAX_LEVELS:
+        raise L.UmamdError(f'tukra_loss: {n} scales (1..{MAX_LEVELS})')
+    return TukraLossFn.apply(cfg, n, *preds, *[p.detach() for p in pyramid])
+
+
+def image_error(images: torch.Tensor, recon: torch.Tensor, alpha: float) -> torch.Tensor:
+    L.require_device(images)
+    img, rec = _f32c(images), _f32c(recon)
+    N, C, H, W = img.shape
+    if C != 6 or rec.shape != img.shape:
+        raise L.UmamdError(f'image_error: images {tuple(img.shape)} / recon {tuple(rec.shape)}')
+    out = torch.empty((N, 2, H, W), dtype=torch.float32, device=img.device)
+    call('um_image_error', ptr(img), ptr(rec), N, H, W, float(alpha), ptr(out))
+    return out
