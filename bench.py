@@ -85,7 +85,10 @@ def step(m, lf, opt, left, right, scale):
     pyr = u.scale_pyramid(images, 4)
     opt.zero_grad(set_to_none=True)
     d = m(left, scale)
-    dl, el = lf(pyr, d, u.reconstruct_pyramid(d, pyr), 0, None)
+    from umamd import lossfn as LF
+    with LF.deferred_recon():  # as train.train.train_step: the loss forward writes the recon
+        recon = u.reconstruct_pyramid(d, pyr)
+    dl, el = lf(pyr, d, recon, 0, None)
     (dl + el).backward()
     opt.step()
     return dl, el

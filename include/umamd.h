@@ -272,12 +272,14 @@ int um_recon_pyramid(int nlevels, int N, int H, int W, const float* const* img,
  * The recon is re-derived in the kernel (warp of the opposite view).
  * ws: um_loss_ws() bytes of f64 scratch; out[6] = disp_loss, error_loss,
  * wssim, consistency, smoothness, error term; emap_last (optional) = the last
- * scale's error map [N][2][h][w] (WeightedSSIMLoss.previous_image_error). */
+ * scale's error map [N][2][h][w] (WeightedSSIMLoss.previous_image_error);
+ * recon_out (optional, per scale) receives the reconstruction [N][6][h][w]
+ * the kernel derives (reconstruct_pyramid's result, as a side output). */
 long um_loss_ws(int nscales, int N, int H, int W);
 int um_loss_fwd(int nscales, int N, int H, int W, const float* const* img,
                 const float* const* pred, float alpha, int loss_type, float esw, float ecw,
                 float w_wssim, float w_cons, float w_smooth, float w_err, double* ws,
-                float* emap_last, float* out, hipStream_t stream);
+                float* emap_last, float* const* recon_out, float* out, hipStream_t stream);
 /* its backward in ONE launch: dpred[s] NHWC [N][h][w][4] = d(gout[0]*disp_loss +
  * gout[1]*error_loss)/d pred[s] (gout on the device) */
 int um_loss_bwd(int nscales, int N, int H, int W, const float* const* img,

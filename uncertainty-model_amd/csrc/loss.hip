@@ -335,6 +335,7 @@ struct LArgs {
   float w_wssim, w_cons, w_smooth, w_err;
   double* parts;      // fwd: [nblocks][8] f64 partial terms
   float* emap;        // fwd: error map of the last scale [N][2][h][w] (or null)
+  float* rec[MAXS];   // fwd (optional): the reconstruction [N][6][h][w] as a side output
   float* out;         // fwd: [6] disp_loss, error_loss, wssim, consistency, smoothness, error
   const float* gout;  // bwd: [2] d total / d disp_loss, d total / d error_loss
 };
@@ -425,15 +426,15 @@ __device__ __forceinline__ void init_tabs(Tabs<TY, TX>& tb, int H, int W, int ty
 }
 
 // predictions of the staged region, float4 per pixel (d_L, d_R, s_L, s_R)
-template <int TY, int TX>
+template <int TY, int TX, int NT = 256>
 __device__ __forceinline__ void stage_pred(const float* pp, int H, int W, int ty0, int tx0,
                                            float4 (*sP)[Tile<TY, TX>::RX]) {
   using T = Tile<TY, TX>;
-  constexpr int K = (T::NP + 255) / 256;
+  constexpr int K = (T::NP + NT - 1) / NT;
   float4 v[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const int i = min((int)threadIdx.x + k * 256, T::NP - 1);
+    const int i = min((int)threadIdx.x + k * NT, T::NP - 1);
     const int r = i / T::RX, q = i - (i / T::RX) * T::RX;
     const int y = ty0 - 2 + r, x = tx0 - 2 + q;
     const bool in = x >= 0 && x < W && y >= 0 && y < H;
@@ -443,7 +444,7 @@ __device__ __forceinline__ void stage_pred(const float* pp, int H, int W, int ty
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const int i = threadIdx.x + k * 256;
+    const int i = threadIdx.x + k * NT;
     if (i < T::NP) sP[i / T::RX][i % T::RX] = v[k];
   }
 }
@@ -454,7 +455,7 @@ __device__ __forceinline__ float comp(const float4& v, int c) {
 
 // image of view v and its reconstruction (warp of the opposite view by
 // sign * d_v); with DIX also d(recon_c)/d(ix) at the TY x TX pixels
-template <int TY, int TX, bool DIX>
+template <int TY, int TX, bool DIX, int NT = 256>
 __device__ __forceinline__ void stage_view(const float* Iv, const float* Io, int H, int W, int HW,
                                            int ty0, int tx0, int v, const Tabs<TY, TX>& tb,
                                            const float4 (*sP)[Tile<TY, TX>::RX],
@@ -462,7 +463,7 @@ __device__ __forceinline__ void stage_view(const float* Iv, const float* Io, int
                                            float (*sR)[Tile<TY, TX>::RY][Tile<TY, TX>::RX],
                                            float (*sX)[TY][TX]) {
   using T = Tile<TY, TX>;
-  constexpr int K = (T::NP + 255) / 256;
+  constexpr int K = (T::NP + NT - 1) / NT;
   constexpr int G = 2;
   const float sign = v == 0 ? -1.f : 1.f;
   const float Wh = (float)W * 0.5f;
@@ -474,7 +475,7 @@ __device__ __forceinline__ void stage_view(const float* Iv, const float* Io, int
     int own[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const int i = min((int)threadIdx.x + (k0 + g) * 256, T::NP - 1);
+      const int i = min((int)threadIdx.x + (k0 + g) * NT, T::NP - 1);
       r[g] = i / T::RX;
       q[g] = i - r[g] * T::RX;
       const int y = ty0 - 2 + r[g], x = tx0 - 2 + q[g];
@@ -496,7 +497,7 @@ __device__ __forceinline__ void stage_view(const float* Iv, const float* Io, int
       }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const int i = threadIdx.x + (k0 + g) * 256;
+      const int i = threadIdx.x + (k0 + g) * NT;
       if (k0 + g >= K || i >= T::NP) continue;
       const Samp& u = t[g];
 #pragma unroll
@@ -546,17 +547,17 @@ __device__ __forceinline__ float dssim_up(const float (*sD)[GX], const UpTap& uy
 }
 
 // ------------------------------------------------------------ forward ------
-constexpr int FTY = 8, FTX = 64;
+constexpr int FTY = 16, FTX = 64, FNT = 512;
 using FT = Tile<FTY, FTX>;
 
 __device__ __forceinline__ float fdiv(float a, float b) { return __fdividef(a, b); }
 
-__global__ void __launch_bounds__(256, 4) loss_fwd_kernel(LArgs a) {
+__global__ void __launch_bounds__(FNT, 2) loss_fwd_kernel(LArgs a) {
   __shared__ float4 sP[FT::RY][FT::RX];
   __shared__ float sI[3][FT::RY][FT::RX], sR[3][FT::RY][FT::RX];
   __shared__ float sD[FT::GY][FT::GX];
   __shared__ Tabs<FTY, FTX> tb;
-  __shared__ double red[6][4];
+  __shared__ double red[6][FNT / 64];
   __shared__ int last;
   const int tid = threadIdx.x;
   const int s = scale_of(a, blockIdx.x);
@@ -571,19 +572,20 @@ __global__ void __launch_bounds__(256, 4) loss_fwd_kernel(LArgs a) {
   const float* img = S.img + (long)n * 6 * HW;
   const int gh = H - 2, gw = W - 2;
   const float Wh = (float)W * 0.5f;
-  constexpr int KP = FTY * FTX / 256;  // pixels per thread and view
+  float* const recp = pick(a.rec, s);
+  constexpr int KP = FTY * FTX / FNT;  // pixels per thread and view
   float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
-  stage_pred<FTY, FTX>(pp, H, W, ty0, tx0, sP);
+  stage_pred<FTY, FTX, FNT>(pp, H, W, ty0, tx0, sP);
   init_tabs<FTY, FTX>(tb, H, W, ty0, tx0);
   __syncthreads();
   for (int v = 0; v < 2; ++v) {
     const float sign = v == 0 ? -1.f : 1.f;
-    stage_view<FTY, FTX, false>(img + v * 3 * HW, img + (1 - v) * 3 * HW, H, W, HW, ty0, tx0,
+    stage_view<FTY, FTX, false, FNT>(img + v * 3 * HW, img + (1 - v) * 3 * HW, H, W, HW, ty0, tx0,
                                 v, tb, sP, sI, sR, nullptr);
     __syncthreads();
     // DSSIM on the valid grid: mean_c clamp((1 - SSIM_c)/2, 0, 1)
-    for (int i = tid; i < FT::GY * FT::GX; i += 256) {
+    for (int i = tid; i < FT::GY * FT::GX; i += FNT) {
       const int r = i / FT::GX, q = i - (i / FT::GX) * FT::GX;
       const int gy = ty0 - 2 + r, gx = tx0 - 2 + q;
       float dv = 0.f;
@@ -605,7 +607,7 @@ __global__ void __launch_bounds__(256, 4) loss_fwd_kernel(LArgs a) {
     float dvv[KP], sgv[KP];
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
-      const int i = tid + k * 256;
+      const int i = tid + k * FNT;
       ly[k] = i / FTX;
       lx[k] = i - (i / FTX) * FTX;
       const float4 p = sP[ly[k] + 2][lx[k] + 2];
@@ -636,6 +638,9 @@ __global__ void __launch_bounds__(256, 4) loss_fwd_kernel(LArgs a) {
       const float ev = a.alpha * up + (1.f - a.alpha) * (l1 * (1.f / 3.f));
       if (a.emap != nullptr && s == a.nscales - 1)
         a.emap[(n * 2 + v) * HW + y * W + x] = ev;
+      if (recp != nullptr)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) recp[(n * 6 + v * 3 + c) * HW + y * W + x] = sR[c][rr][qq];
       acc[0] += ev;
       const float wxs = __expf(-gxi * (1.f / 3.f)), wys = __expf(-gyi * (1.f / 3.f));
       const float4 p0 = sP[rr][qq], px1 = sP[rr][qq + 1], py1 = sP[rr + 1][qq];
@@ -670,7 +675,10 @@ __global__ void __launch_bounds__(256, 4) loss_fwd_kernel(LArgs a) {
     const double np = (double)a.N * HW;
     double r[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) r[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+    for (int k = 0; k < 6; ++k) {
+      r[k] = 0.0;
+      for (int w = 0; w < FNT / 64; ++w) r[k] += red[k][w];
+    }
     double* o = a.parts + (long)blockIdx.x * 8;
     o[0] = r[0] / np;
     o[1] = r[1] / np;
@@ -697,7 +705,7 @@ __global__ void __launch_bounds__(256, 4) loss_fwd_kernel(LArgs a) {
   __syncthreads();
   if (!last) return;
   double q[6] = {0, 0, 0, 0, 0, 0};
-  for (int b = tid; b < a.nblocks; b += 256)
+  for (int b = tid; b < a.nblocks; b += FNT)
 #pragma unroll
     for (int k = 0; k < 6; ++k) q[k] += a.parts[(long)b * 8 + k];
 #pragma unroll
@@ -713,7 +721,10 @@ __global__ void __launch_bounds__(256, 4) loss_fwd_kernel(LArgs a) {
   if (tid == 0) {
     double f[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) f[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+    for (int k = 0; k < 6; ++k) {
+      f[k] = 0.0;
+      for (int w = 0; w < FNT / 64; ++w) f[k] += red[k][w];
+    }
     const double ws = f[0], cs = f[1], sm = f[2];
     const double er = f[3] + (double)a.esw * f[5] + (double)a.ecw * f[4];
     a.out[0] = (float)(ws * a.w_wssim + cs * a.w_cons + sm * a.w_smooth);
@@ -814,10 +825,10 @@ __global__ void __launch_bounds__(SCT) loss_scatter_kernel(LArgs a) {
 }
 
 // (2) every other gradient, per TY x TX tile (both views), plus the scatter sums
-constexpr int BTY = 8, BTX = 32;
+constexpr int BTY = 16, BTX = 32, BNT = 512;
 using BT = Tile<BTY, BTX>;
 
-__global__ void __launch_bounds__(256, 3) loss_grad_kernel(LArgs a) {
+__global__ void __launch_bounds__(BNT, 2) loss_grad_kernel(LArgs a) {
   __shared__ float4 sP[BT::RY][BT::RX];
   __shared__ float sI[3][BT::RY][BT::RX], sR[3][BT::RY][BT::RX];
   __shared__ float sX[3][BTY][BTX];           // d recon_c / d ix at the pixels
@@ -854,7 +865,7 @@ __global__ void __launch_bounds__(256, 3) loss_grad_kernel(LArgs a) {
   float* dslot = S.dpred + ((long)n * HW + (long)min(y, H - 1) * W + min(x, W - 1)) * 4;
   const float2 sav = *reinterpret_cast<const float2*>(dslot);
 
-  stage_pred<BTY, BTX>(pp, H, W, ty0, tx0, sP);
+  stage_pred<BTY, BTX, BNT>(pp, H, W, ty0, tx0, sP);
   init_tabs<BTY, BTX>(tb, H, W, ty0, tx0);
   if (tid < BT::GY) {
     const int gy = ty0 - 2 + tid;
@@ -867,12 +878,12 @@ __global__ void __launch_bounds__(256, 3) loss_grad_kernel(LArgs a) {
   float4 outv = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int v = 0; v < 2; ++v) {
     const float sign = v == 0 ? -1.f : 1.f;
-    stage_view<BTY, BTX, true>(img + v * 3 * HW, img + (1 - v) * 3 * HW, H, W, HW, ty0, tx0, v,
+    stage_view<BTY, BTX, true, BNT>(img + v * 3 * HW, img + (1 - v) * 3 * HW, H, W, HW, ty0, tx0, v,
                                tb, sP, sI, sR, sX);
     __syncthreads();
     // per grid point: DSSIM (for the NLL's error map) and the SSIM
     // gradient coefficients
-    for (int i = tid; i < BT::GY * BT::GX; i += 256) {
+    for (int i = tid; i < BT::GY * BT::GX; i += BNT) {
       const int r = i / BT::GX, q = i - (i / BT::GX) * BT::GX;
       const int gy = ty0 - 2 + r, gx = tx0 - 2 + q;
       float dsum = 0.f;
@@ -1160,7 +1171,7 @@ long um_loss_ws(int nscales, int N, int H, int W) {
 int um_loss_fwd(int nscales, int N, int H, int W, const float* const* img,
                 const float* const* pred, float alpha, int loss_type, float esw, float ecw,
                 float w_wssim, float w_cons, float w_smooth, float w_err, double* ws,
-                float* emap_last, float* out, hipStream_t st) {
+                float* emap_last, float* const* recon_out, float* out, hipStream_t st) {
   UM_CHECK_ARG(nscales >= 1 && nscales <= MAXS, "um_loss_fwd: %d scales (1..%d)", nscales, MAXS);
   UM_CHECK_ARG((H >> (nscales - 1)) >= 3 && (W >> (nscales - 1)) >= 3,
                "um_loss_fwd: image %dx%d too small for %d scales", H, W, nscales);
@@ -1170,8 +1181,9 @@ int um_loss_fwd(int nscales, int N, int H, int W, const float* const* img,
   a.w_wssim = w_wssim; a.w_cons = w_cons; a.w_smooth = w_smooth; a.w_err = w_err;
   a.parts = ws;
   a.emap = emap_last;
+  for (int l = 0; l < nscales; ++l) a.rec[l] = recon_out ? recon_out[l] : nullptr;
   a.out = out;
-  hipLaunchKernelGGL(loss_fwd_kernel, dim3(blocks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(loss_fwd_kernel, dim3(blocks), dim3(FNT), 0, st, a);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -1199,7 +1211,7 @@ int um_loss_bwd(int nscales, int N, int H, int W, const float* const* img,
   int blocks = loss_setup(a, nscales, N, H, W, img, pred, dpred, STR, 0);
   hipLaunchKernelGGL(loss_scatter_kernel, dim3(blocks), dim3(SCT), lds, st, a);
   blocks = loss_setup(a, nscales, N, H, W, img, pred, dpred, BTY, BTX);
-  hipLaunchKernelGGL(loss_grad_kernel, dim3(blocks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(loss_grad_kernel, dim3(blocks), dim3(BNT), 0, st, a);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

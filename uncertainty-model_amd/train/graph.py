@@ -24,6 +24,7 @@ import os
 
 import torch
 
+from umamd import lossfn as LF
 from umamd import overlap
 
 from . import utils as u
@@ -69,7 +70,8 @@ class CapturedTrainStep:
         images = torch.cat([self.left, self.right], dim=1)
         pyramid = u.scale_pyramid(images, self.scales)
         disparities = self.model(self.left, self.scale)
-        recon = u.reconstruct_pyramid(disparities, pyramid)
+        with LF.deferred_recon():  # the loss forward writes the recon
+            recon = u.reconstruct_pyramid(disparities, pyramid)
         disp_loss, error_loss = self.loss_function(pyramid, disparities, recon, 0, None)
         if self.overlap is None:
             (disp_loss + error_loss).backward()

@@ -142,8 +142,12 @@ class TukraUncertaintyLoss(nn.Module):
                                  'train.utils.reconstruct_pyramid(predictions, image_pyramid) '
                                  '(the fused kernels re-derive that warp and differentiate '
                                  'through it)')
-        disp_loss, error_loss, terms, emap = LF.tukra_loss(self._cfg(), list(predictions),
-                                                           list(image_pyramid))
+        pending = [r for r in recon_pyramid if getattr(r, '_umamd_pending', False)]
+        if pending and len(pending) != len(recon_pyramid):
+            raise ValueError('TukraUncertaintyLoss (umamd): partly deferred recon_pyramid')
+        disp_loss, error_loss, terms, emap = LF.tukra_loss(
+            self._cfg(), list(predictions), list(image_pyramid),
+            list(recon_pyramid) if pending else None)
         self.wssim._previous_image_error = emap
         self.last_terms = terms  # [disp, error, wssim, consistency, smoothness, error-term]
         return disp_loss, error_loss

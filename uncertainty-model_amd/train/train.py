@@ -16,6 +16,7 @@ from torch.nn import Module
 from torch.optim import Optimizer
 from torch.utils.data import DataLoader
 
+from umamd import lossfn as LF
 from umamd.optim import Adam
 
 from . import utils as u
@@ -47,7 +48,8 @@ def train_step(model: Module, left, right, loss_function: Module, optimiser: Opt
     image_pyramid = u.scale_pyramid(images, scales)
     optimiser.zero_grad()
     disparities = model(left, scale)
-    recon_pyramid = u.reconstruct_pyramid(disparities, image_pyramid)
+    with LF.deferred_recon():  # the fused loss forward writes the recon
+        recon_pyramid = u.reconstruct_pyramid(disparities, image_pyramid)
     disp_loss, error_loss = loss_function(image_pyramid, disparities, recon_pyramid,
                                           batch_index, None)
     (disp_loss + error_loss).backward()

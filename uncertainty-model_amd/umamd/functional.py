@@ -274,8 +274,8 @@ class ConvBNELUFn(torch.autograd.Function):
             call('um_channel_mean', _dt(a), N, P * Q, K, ptr(a), K, ptr(pooled))
             z1 = torch.empty((N, R1), dtype=torch.float32, device=dev)
             s = torch.empty((N, K), dtype=torch.float32, device=dev)
-            call('um_se_mlp_fwd', N, K, R1, ptr(pooled), ptr(w1.detach().float().contiguous()),
-                 ptr(w2.detach().float().contiguous()), ptr(z1), ptr(s))
+            w1c, w2c = w1.detach().float().contiguous(), w2.detach().float().contiguous()
+            call('um_se_mlp_fwd', N, K, R1, ptr(pooled), ptr(w1c), ptr(w2c), ptr(z1), ptr(s))
             se = (pooled, z1, s)
             outs.append(s)
         ctx.spec = spec
@@ -306,10 +306,10 @@ class ConvBNELUFn(torch.autograd.Function):
             dw2 = torch.zeros(w2.shape, dtype=torch.float32, device=dev)
             add_nc = torch.empty((N, K), dtype=torch.float32, device=dev)
             dz = torch.empty((N, R1), dtype=torch.float32, device=dev)
-            call('um_se_mlp_bwd', N, K, R1, ptr(ds.float().contiguous()), ptr(s), ptr(z1),
-                 ptr(pooled), ptr(w1.detach().float().contiguous()),
-                 ptr(w2.detach().float().contiguous()), ptr(dw1), ptr(dw2), ptr(add_nc),
-                 ptr(dz), 1.0 / (P * Q))
+            dsc = ds.float().contiguous()
+            w1c, w2c = w1.detach().float().contiguous(), w2.detach().float().contiguous()
+            call('um_se_mlp_bwd', N, K, R1, ptr(dsc), ptr(s), ptr(z1), ptr(pooled), ptr(w1c),
+                 ptr(w2c), ptr(dw1), ptr(dw2), ptr(add_nc), ptr(dz), 1.0 / (P * Q))
         dgamma = dbeta = None
         k1 = torch.empty(K, dtype=torch.float32, device=dev)
         k2 = torch.empty_like(k1)

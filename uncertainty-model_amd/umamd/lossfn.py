@@ -18,10 +18,12 @@ the pyramid and the predictions inside its kernels, so the recon tensors it is
 given must be exactly ``reconstruct_pyramid(predictions, pyramid)`` -- which
 is what train/train.py passes (reference train.py:122-124); they are tagged
 and checked.  The recon tensors are still real (``reconstruct_pyramid`` runs
-its own launch) and differentiable w.r.t. the disparities (adversarial terms).
+its own launch, or -- under ``deferred_recon`` -- the loss forward writes them)
+and differentiable w.r.t. the disparities (adversarial terms).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import List, Sequence
 
@@ -32,6 +34,24 @@ from ._lib import call, ptr, query
 
 LOSS_TYPES = {'l1': 0, 'bayesian': 1, 'log_bayesian': 2}
 MAX_LEVELS = 6
+
+_defer = [False]
+
+
+@contextlib.contextmanager
+def deferred_recon():
+    """Inside this context ``reconstruct_pyramid`` only allocates its outputs
+    and marks them pending; the fused loss forward that follows fills them
+    as a side output of the kernel that derives the reconstruction anyway
+    (saving the separate recon launch).  Only for step bodies where the loss
+    directly consumes the recon (train.train.train_step, the captured step):
+    a pending recon holds no values until that loss forward has run."""
+    old = _defer[0]
+    _defer[0] = True
+    try:
+        yield
+    finally:
+        _defer[0] = old
 
 
 def _f32c(t: torch.Tensor) -> torch.Tensor:
@@ -104,8 +124,9 @@ class _WarpFn(torch.autograd.Function):
         N, C, H, W = imgc.shape
         gd = torch.empty((N, 1, H, W), dtype=torch.float32, device=g.device)
         _, sn, sp = _disp_strides(d)
+        gc = _f32c(g)  # keep alive until the launch is queued (no temporaries by pointer)
         call('um_warp_bwd', ptr(imgc), N, C, H, W, d.data_ptr(), sn, sp, ctx.sign,
-             ptr(_f32c(g)), ptr(gd), H * W, 1)
+             ptr(gc), ptr(gd), H * W, 1)
         return gd.to(ctx.ddtype).reshape(ctx.dshape), None, None
 
 
@@ -118,7 +139,7 @@ class _ReconPyramidFn(torch.autograd.Function):
     adjoint w.r.t. d_L (channel 0) and d_R (channel 1)."""
 
     @staticmethod
-    def forward(ctx, n, *tensors):
+    def forward(ctx, n, defer, *tensors):
         disps, pyr = tensors[:n], [_f32c(t) for t in tensors[n:]]
         N, _, H, W = pyr[0].shape
         dev = pyr[0].device
@@ -135,8 +156,9 @@ class _ReconPyramidFn(torch.autograd.Function):
             strides += [sn, dd.stride(1), sp]
         out = [torch.empty((N, 6, H >> i, W >> i), dtype=torch.float32, device=dev)
                for i in range(n)]
-        sarr = (ctypes.c_long * len(strides))(*strides)
-        call('um_recon_pyramid', n, N, H, W, _parr(pyr), _parr(ds), sarr, _parr(out))
+        if not defer:
+            sarr = (ctypes.c_long * len(strides))(*strides)
+            call('um_recon_pyramid', n, N, H, W, _parr(pyr), _parr(ds), sarr, _parr(out))
         ctx.n = n
         ctx.meta = [(d.shape, d.dtype) for d in disps]
         ctx.save_for_backward(*ds, *pyr)
@@ -151,7 +173,7 @@ class _ReconPyramidFn(torch.autograd.Function):
         for i in range(n):
             g = gouts[i]
             shape, dtype = ctx.meta[i]
-            if g is None or not ctx.needs_input_grad[1 + i]:
+            if g is None or not ctx.needs_input_grad[2 + i]:
                 grads.append(None)
                 continue
             g = _f32c(g)
@@ -162,11 +184,14 @@ class _ReconPyramidFn(torch.autograd.Function):
             # left recon = warp(right image, -d_L); right recon = warp(left image, +d_R)
             for v, (img, gsl, sign) in enumerate(((pyr[i][:, 3:6], g[:, 0:3], -1.0),
                                                   (pyr[i][:, 0:3], g[:, 3:6], 1.0))):
-                call('um_warp_bwd', ptr(img.contiguous()), N, 3, h, w,
-                     ds[i].data_ptr() + v * cs * 4, sn, sp, sign, ptr(gsl.contiguous()),
+                # bind the contiguous copies: a temporary passed only by pointer
+                # could be freed (and its memory reused) before the launch runs
+                imgc, gc = img.contiguous(), gsl.contiguous()
+                call('um_warp_bwd', ptr(imgc), N, 3, h, w,
+                     ds[i].data_ptr() + v * cs * 4, sn, sp, sign, ptr(gc),
                      gd.data_ptr() + v * 4, h * w * shape[1], shape[1])
             grads.append(gd.permute(0, 3, 1, 2).to(dtype))
-        return (None, *grads, *([None] * n))
+        return (None, None, *grads, *([None] * n))
 
 
 def reconstruct_pyramid(disparities: Sequence[torch.Tensor],
@@ -175,9 +200,12 @@ def reconstruct_pyramid(disparities: Sequence[torch.Tensor],
     if not 1 <= n <= MAX_LEVELS:
         raise L.UmamdError(f'reconstruct_pyramid: {n} levels (1..{MAX_LEVELS})')
     L.require_device(pyramid[0])
-    out = list(_ReconPyramidFn.apply(n, *disparities[:n], *[p.detach() for p in pyramid[:n]]))
+    defer = _defer[0]
+    out = list(_ReconPyramidFn.apply(n, defer, *disparities[:n],
+                                     *[p.detach() for p in pyramid[:n]]))
     for d, im, r in zip(disparities, pyramid, out):
         r._umamd_recon = (id(d), id(im))
+        r._umamd_pending = defer
     return out
 
 
@@ -194,10 +222,17 @@ def _check_levels(preds, pyr):
 
 class TukraLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cfg, n, *tensors):
+    def forward(ctx, cfg, n, recon_out, *tensors):
         preds = [_pred_nhwc(t) for t in tensors[:n]]
         pyr = [_f32c(t) for t in tensors[n:2 * n]]
         N, H, W = _check_levels(preds, pyr)
+        rarr = None
+        if recon_out is not None:
+            for i, r in enumerate(recon_out):
+                if r.shape != pyr[i].shape or r.dtype != torch.float32 or not r.is_contiguous():
+                    raise L.UmamdError('tukra_loss: recon_out must be the [N,6,h,w] f32 '
+                                       'contiguous reconstruct_pyramid outputs')
+            rarr = _parr(recon_out)
         dev = preds[0].device
         ws = torch.empty((max(query('um_loss_ws', n, N, H, W), 8) // 8,), dtype=torch.float64,
                          device=dev)
@@ -205,7 +240,7 @@ class TukraLossFn(torch.autograd.Function):
         out = torch.empty(6, dtype=torch.float32, device=dev)
         call('um_loss_fwd', n, N, H, W, _parr(pyr), _parr(preds), cfg['alpha'],
              cfg['loss_type'], cfg['esw'], cfg['ecw'], cfg['w_wssim'], cfg['w_cons'],
-             cfg['w_smooth'], cfg['w_err'], ptr(ws), ptr(emap), ptr(out))
+             cfg['w_smooth'], cfg['w_err'], ptr(ws), ptr(emap), rarr, ptr(out))
         ctx.cfg = cfg
         ctx.n = n
         ctx.geom = (N, H, W)
@@ -230,16 +265,21 @@ class TukraLossFn(torch.autograd.Function):
         call('um_loss_bwd', n, N, H, W, _parr(pyr), _parr(preds), cfg['alpha'],
              cfg['loss_type'], cfg['esw'], cfg['ecw'], cfg['w_wssim'], cfg['w_cons'],
              cfg['w_smooth'], cfg['w_err'], ptr(gout), _parr(grads))
-        return (None, None, *[g.permute(0, 3, 1, 2) for g in grads], *([None] * n))
+        return (None, None, None, *[g.permute(0, 3, 1, 2) for g in grads], *([None] * n))
 
 
-def tukra_loss(cfg: dict, preds, pyramid):
+def tukra_loss(cfg: dict, preds, pyramid, recon_out=None):
     """Returns (disp_loss, error_loss, terms[6], last-scale error map).  The
-    backward differentiates through the warp itself (the recon is re-derived)."""
+    backward differentiates through the warp itself (the recon is re-derived).
+    ``recon_out``: pending reconstruct_pyramid outputs to fill (deferred_recon)."""
     n = len(preds)
     if not 1 <= n <= MAX_LEVELS:
         raise L.UmamdError(f'tukra_loss: {n} scales (1..{MAX_LEVELS})')
-    return TukraLossFn.apply(cfg, n, *preds, *[p.detach() for p in pyramid])
+    out = TukraLossFn.apply(cfg, n, recon_out, *preds, *[p.detach() for p in pyramid])
+    if recon_out is not None:
+        for r in recon_out:
+            r._umamd_pending = False
+    return out
 
 
 def image_error(images: torch.Tensor, recon: torch.Tensor, alpha: float) -> torch.Tensor:
