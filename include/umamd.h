@@ -290,6 +290,26 @@ int um_loss_bwd(int nscales, int N, int H, int W, const float* const* img,
 int um_image_error(const float* img, const float* rec, int N, int H, int W, float alpha,
                    float* out, hipStream_t stream);
 
+/* ---------------------------------------------------------- evaluation ---
+ * evaluate_model / sparsification (reference train/evaluate.py:66-196,
+ * train/sparsification.py:8-61).  Off the training hot path.
+ */
+/* torchmetrics structural_similarity_index_measure (gaussian window, sigma ->
+ * 11 taps, k1 0.01, k2 0.03) per image: out[n] = mean SSIM over the C x
+ * (H-10) x (W-10) full windows; ws: um_ssim_ws() bytes */
+long um_ssim_ws(int N, int H, int W);
+int um_ssim_gauss(const float* x, const float* y, int N, int C, int H, int W, float data_range,
+                  float sigma, double* ws, float* out, hipStream_t stream);
+/* nn.AvgPool2d(k, stride=1): out [NC][H-k+1][W-k+1] */
+int um_avgpool_valid(const float* x, int NC, int H, int W, int k, float* out, hipStream_t stream);
+/* argsort(keys, descending) + gather(vals) per segment of L (nseg segments) */
+long um_spars_sort_ws(int nseg, int L);
+int um_spars_sort(const float* keys, const float* vals, int nseg, int L, float* keys_out,
+                  float* vals_out, void* ws, long ws_bytes, hipStream_t stream);
+/* curve[k] = mean_seg( mean(sorted[int(k/steps*L):]) / mean(sorted) ); ws: nseg*steps f64 */
+int um_spars_curve(const float* sorted_vals, int nseg, int L, int steps, double* ws,
+                   float* curve, hipStream_t stream);
+
 /* ---------------------------------------------------------------- adam ---
  * torch.optim.Adam step, reference train/train.py:228-229.
  */

@@ -260,7 +260,8 @@ def gen_model(ref_model, cfg):
     save('model_fwd.npz', **arrays)
 
 
-def gen_step(ref_model, ref_loss, ref_utils, cfg, loss_type, steps=3, tag=None):
+def gen_step(ref_model, ref_loss, ref_utils, cfg, loss_type, steps=3, tag=None, b=2, h=64,
+             w=128, disp_levels=(0, 1, 2, 3)):
     sd, specs = _formula_weights(cfg)
     m = _ref_model(ref_model, cfg)
     m.load_state_dict(sd)
@@ -269,7 +270,6 @@ def gen_step(ref_model, ref_loss, ref_utils, cfg, loss_type, steps=3, tag=None):
     lcfg['error_loss_config']['loss_type'] = loss_type
     lf = ref_loss.TukraUncertaintyLoss(**lcfg)
     opt = torch.optim.Adam(m.parameters(), 1e-4)
-    b, h, w = 2, 64, 128
     left, right, _ = stereo_pair(b, h, w, seed=555)
     arrays = {'left': left, 'right': right}
     scale = float(ref_utils.adjust_disparity(0))
@@ -286,7 +286,10 @@ def gen_step(ref_model, ref_loss, ref_utils, cfg, loss_type, steps=3, tag=None):
             for k, p in m.named_parameters():
                 arrays[f'gradnorm/{k}'] = p.grad.double().norm()
             for i, d in enumerate(disps):
-                arrays[f'step0_disp{i}'] = d.detach()
+                if i in disp_levels:
+                    arrays[f'step0_disp{i}'] = d.detach()
+                arrays[f'step0_disp{i}_sum'] = d.detach().double().sum()
+                arrays[f'step0_disp{i}_abssum'] = d.detach().double().abs().sum()
         opt.step()
         arrays[f'disp_loss_{step}'] = dl.detach()
         arrays[f'error_loss_{step}'] = el.detach()
@@ -313,6 +316,45 @@ def gen_nodes10(ref_model, cfg10):
          schema=np.array(json.dumps([[s[0], list(s[1])] for s in specs])))
 
 
+def gen_transforms():
+    """The reference's RandomFlip / RandomAugment decision and arithmetic
+    logic (train/transforms.py:44-129) on seeded numpy RNG draws.  torchvision
+    is absent: RandomHorizontalFlip(1) is stubbed by a tensor flip, which is
+    torchvision's tensor semantics."""
+    tv = sys.modules['torchvision.transforms']
+    tv.RandomHorizontalFlip = lambda p: (lambda x: x.flip(-1))
+    import importlib
+    import train.transforms as ref_t  # noqa: E402
+    importlib.reload(ref_t)
+    g = torch.Generator().manual_seed(99)
+    left = torch.rand(3, 24, 40, generator=g)
+    right = torch.rand(3, 24, 40, generator=g)
+    flip = ref_t.RandomFlip(0.5)
+    aug = ref_t.RandomAugment(0.5, gamma=(0.8, 1.2), brightness=(0.5, 2.0), colour=(0.8, 1.2))
+    np.random.seed(2024)
+    arrays = {'left': left, 'right': right}
+    for i in range(12):
+        out = aug(flip({'left': left.clone(), 'right': right.clone()}))
+        arrays[f'left{i}'] = out['left']
+        arrays[f'right{i}'] = out['right']
+    save('transforms.npz', **arrays)
+
+
+def gen_sparsification():
+    """train/sparsification.py curves on synthetic error / uncertainty maps
+    (the deterministic parts: the oracle and predicted curves, AUSE; the
+    random curve is recorded for its seed only)."""
+    import train.sparsification as ref_s  # noqa: E402
+    g = torch.Generator().manual_seed(7)
+    b, h, w = 2, 40, 72
+    err = torch.rand(b, 2, h, w, generator=g) ** 2
+    unc = (err + 0.3 * torch.rand(b, 2, h, w, generator=g)).clamp_min(0)
+    oracle = ref_s.curve(err, err)
+    pred = ref_s.curve(err, unc)
+    save('sparsification.npz', err=err, unc=unc, oracle_curve=oracle, pred_curve=pred,
+         ause=ref_s.ause(oracle, pred))
+
+
 def main():
     ref_model, ref_loss, ref_utils = import_reference()
     torch.set_num_threads(8)
@@ -320,7 +362,8 @@ def main():
         cfg = yaml.safe_load(f)
     with open(os.path.join(REPO, 'config_nodes10.yml')) as f:
         cfg10 = yaml.safe_load(f)
-    which = sys.argv[1:] or ['warp', 'loss', 'model', 'step', 'nodes10']
+    which = sys.argv[1:] or ['warp', 'loss', 'model', 'step', 'nodes10', 'c1', 'transforms',
+                             'sparsification']
     if 'warp' in which:
         gen_warp(ref_utils)
     if 'loss' in which:
@@ -333,6 +376,13 @@ def main():
         gen_step(ref_model, ref_loss, ref_utils, cfg, 'l1', steps=1)
     if 'nodes10' in which:
         gen_nodes10(ref_model, cfg10)
+    if 'c1' in which:  # BASELINE config 1: 128x256, batch 2, l1 error loss, one step
+        gen_step(ref_model, ref_loss, ref_utils, cfg, 'l1', steps=1, tag='c1_l1', b=2, h=128,
+                 w=256, disp_levels=(2, 3))
+    if 'transforms' in which:
+        gen_transforms()
+    if 'sparsification' in which:
+        gen_sparsification()
 
 
 if __name__ == '__main__':

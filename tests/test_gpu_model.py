@@ -298,3 +298,115 @@ def test_batched_weight_pack_matches_per_site_pack(dtype):
                 assert torch.equal(t, t2), key
             checked += 1
         assert checked >= 40
+
+
+def test_train_step_config1_l1():
+    """BASELINE config 1 shape (B=2, 128x256, l1 error loss), one fp32 step
+    against the reference-generated golden (make_goldens.py c1)."""
+    import train.utils as u
+    from train.loss import TukraUncertaintyLoss
+    from umamd.optim import Adam
+    z = _z('step_c1_l1.npz')
+    cfg = _cfg()
+    cfg['loss']['error_loss_config']['loss_type'] = 'l1'
+    m = _model(cfg).train()
+    lf = TukraUncertaintyLoss(**cfg['loss'])
+    opt = Adam(m.parameters(), 1e-4)
+    left = torch.from_numpy(z['left']).to(DEV)
+    right = torch.from_numpy(z['right']).to(DEV)
+    scale = float(u.adjust_disparity(0))
+    pyr = u.scale_pyramid(torch.cat([left, right], 1), 4)
+    opt.zero_grad()
+    d = m(left, scale)
+    for i in (2, 3):
+        assert _rel(d[i], z[f'step0_disp{i}']) < 1e-3
+    for i in range(4):
+        assert abs(float(d[i].double().sum()) / float(z[f'step0_disp{i}_sum']) - 1) < 1e-4
+    dl, el = lf(pyr, d, u.reconstruct_pyramid(d, pyr), 0, None)
+    assert abs(float(dl) / float(z['disp_loss_0']) - 1) < 1e-3
+    assert abs(float(el) / float(z['error_loss_0']) - 1) < 1e-3
+    (dl + el).backward()
+    bad = []
+    for k, p in m.named_parameters():
+        if _pre_bn_bias(k):
+            continue
+        ref, got = float(z[f'gradnorm/{k}']), float(p.grad.double().norm())
+        rtol = 0.1 if ('excite' in k or k.endswith('mean_weight')) else 2e-2  # l1: see above
+        if abs(got - ref) > rtol * ref + 1e-6:
+            bad.append((k, got, ref))
+    assert not bad, bad[:8]
+    opt.step()
+    sd = m.state_dict()
+    for k in z.files:
+        if k.startswith('bn/'):
+            assert _rel(sd[k[3:]], z[k]) < 1e-3, k
+
+
+def test_train_step_config2_bf16_properties():
+    """BASELINE config 2 shape (B=8, 256x512, bayesian, bf16): the captured
+    step's losses and gradients are finite, and the bf16 loss scalars agree
+    with an fp32 step from the same weights within the bf16 bar (SURVEY F8:
+    <= 1e-2 disp, 3e-2 error relative)."""
+    import train.utils as u
+    from train.loss import TukraUncertaintyLoss
+    from train.train import train_step
+    from umamd.optim import Adam
+    cfg = _cfg()
+    cfg['loss']['error_loss_config']['loss_type'] = 'bayesian'
+    torch.manual_seed(0)
+    m16 = _model(cfg, 'bf16').train()
+    m32 = _model(cfg, 'fp32').train()
+    m32.load_state_dict(m16.state_dict())
+    lf = TukraUncertaintyLoss(**cfg['loss'])
+    left, right = _uniform_pair(8, 256, 512, seed=99)
+    left, right = left.to(DEV), right.to(DEV)
+    losses = []
+    for m in (m16, m32):
+        opt = Adam(m.parameters(), 1e-4)
+        dl, el = train_step(m, left, right, lf, opt, 0.3)
+        torch.cuda.synchronize()
+        assert torch.isfinite(dl) and torch.isfinite(el)
+        for k, p in m.named_parameters():
+            assert p.grad is not None and torch.isfinite(p.grad).all(), k
+        losses.append((float(dl), float(el)))
+    (d16, e16), (d32, e32) = losses
+    assert abs(d16 / d32 - 1) < 1e-2 and abs(e16 / e32 - 1) < 3e-2, losses
+
+
+def test_nodes10_train_step_matches_oracle():
+    """BASELINE config 5's graphs (nodes=10, several output nodes per stage):
+    the reference cannot train them (in-place output sum breaks
+    autograd), so the oracle's out-of-place restatement is the reference for
+    one fp32 training step at 64x128 (losses and per-parameter grad norms)."""
+    import train.utils as u
+    from oracle import loss as OL, model as OM, step as OS
+    from train.loss import TukraUncertaintyLoss
+    cfg = _cfg('config_nodes10.yml')
+    cfg['loss']['error_loss_config']['loss_type'] = 'bayesian'
+    graphs = OM.load_stage_graphs(cfg['model']['encoder'])
+    sd = OS.formula_state_dict(OS.param_specs(cfg['model'], graphs))
+    m = _model(cfg).train()
+    m.load_state_dict(sd)
+    left, right = _uniform_pair(2, 64, 128, seed=5)
+    lf = TukraUncertaintyLoss(**cfg['loss'])
+    pyr = u.scale_pyramid(torch.cat([left, right], 1).to(DEV), 4)
+    d = m(left.to(DEV), 0.3)
+    dl, el = lf(pyr, d, u.reconstruct_pyramid(d, pyr), 0, None)
+    (dl + el).backward()
+    P = {k: v.clone().requires_grad_(v.is_floating_point() and 'running' not in k)
+         for k, v in sd.items()}
+    pyr_c = OL.scale_pyramid(torch.cat([left, right], 1), 4)
+    dc = OM.model_forward(left, P, cfg['model'], graphs, 0.3)
+    dlc, elc, _ = OL.total_loss(pyr_c, dc, OL.reconstruct_pyramid(dc, pyr_c), cfg['loss'])
+    (dlc + elc).backward()
+    assert abs(float(dl) / float(dlc) - 1) < 1e-3
+    assert abs(float(el) / float(elc) - 1) < 1e-3
+    bad = []
+    for k, p in m.named_parameters():
+        if _pre_bn_bias(k) or P[k].grad is None:
+            continue
+        ref, got = float(P[k].grad.double().norm()), float(p.grad.double().norm())
+        atol = 3e-5 if k.endswith('mean_weight') else 1e-6
+        if abs(got - ref) > 2e-2 * ref + atol:
+            bad.append((k, got, ref))
+    assert not bad, bad[:8]

@@ -8,7 +8,7 @@ the hot path:
   l1_loss, detach_pyramid, concatenate_pyramids, adjust_disparity,
   adjust_learning_rate, prepare_state_dict: host-side, same semantics.
 """
-from typing import Callable, List, OrderedDict, Union
+from typing import Callable, List, Optional, OrderedDict, Union
 
 import numpy as np
 import torch
@@ -87,6 +87,86 @@ def adjust_learning_rate(optimiser: Optimizer, epoch: int, lr: float,
         group['lr'] = target
 
 
-def run_discriminator(*args, **kwargs):
-    raise NotImplementedError('umamd: adversarial training (run_discriminator, reference '
-                              'train/utils.py:248-273) is not implemented yet')
+# ------------------------------------------------ visualisation (host) ----
+# reference train/utils.py:177-245,276-325 and the torchvision.utils
+# make_grid / save_image they rely on (torchvision is not in this image)
+def to_heatmap(x: Tensor, device: Device = 'cpu', inverse: bool = False,
+               colour_map: str = 'inferno') -> Tensor:
+    """Single-channel image -> RGB heatmap (reference :177-199)."""
+    import matplotlib.pyplot as plt
+    image = x.squeeze(0).detach().float().cpu().numpy()
+    image = 1 - image if inverse else image
+    heatmap = plt.get_cmap(colour_map)(image)[:, :, :3]
+    return torch.from_numpy(heatmap).to(device).permute(2, 0, 1)
+
+
+def combine_disparity(left: Tensor, right: Tensor, device: Device = 'cpu',
+                      alpha: float = 20, beta: float = 0.05) -> Tensor:
+    """Monodepth2-style blind-spot blend of the two views (reference :202-245)."""
+    left_disp = left.detach().cpu().numpy()
+    right_disp = right.detach().cpu().numpy()
+    mean_disp = (left_disp + right_disp) / 2
+    _, height, width = mean_disp.shape
+    xv, _ = np.meshgrid(np.linspace(0, 1, width), np.linspace(0, 1, height))
+    left_mask = 1 - np.clip(alpha * (xv - beta), 0, 1)
+    right_mask = np.fliplr(left_mask)
+    mean_mask = 1 - (left_mask + right_mask)
+    combined = (right_mask * left_disp) + (left_mask * right_disp) + (mean_mask * mean_disp)
+    return torch.from_numpy(combined).to(device)
+
+
+def make_grid(tensor: Tensor, nrow: int = 8, padding: int = 2, pad_value: float = 0.0) -> Tensor:
+    """torchvision.utils.make_grid (no normalisation) for a [B,C,H,W] batch."""
+    t = tensor.detach()
+    if t.dim() == 3:
+        t = t.unsqueeze(0)
+    if t.shape[1] == 1:
+        t = t.repeat(1, 3, 1, 1)
+    nmaps = t.shape[0]
+    xmaps = min(nrow, nmaps)
+    ymaps = (nmaps + xmaps - 1) // xmaps
+    height, width = t.shape[2] + padding, t.shape[3] + padding
+    grid = t.new_full((t.shape[1], height * ymaps + padding, width * xmaps + padding), pad_value)
+    k = 0
+    for y in range(ymaps):
+        for x in range(xmaps):
+            if k >= nmaps:
+                break
+            grid[:, y * height + padding:(y + 1) * height, x * width + padding:(x + 1) * width] = t[k]
+            k += 1
+    return grid
+
+
+def save_image(tensor: Tensor, fp: str) -> None:
+    """torchvision.utils.save_image of a [C,H,W] image in [0, 1]."""
+    from PIL import Image
+    grid = make_grid(tensor) if tensor.dim() == 4 else tensor.detach()
+    arr = grid.float().mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to('cpu', torch.uint8)
+    Image.fromarray(arr.numpy()).save(fp)
+
+
+def get_comparison(image: Tensor, prediction: Tensor, extra: Optional[Tensor],
+                   add_scaled: bool = False, device: Device = 'cpu') -> Tensor:
+    """Grid of the stereo images, disparity heatmaps and an extra pair (reference :276-325)."""
+    image, prediction = image.detach().float().cpu(), prediction.detach().float().cpu()
+    left_image, right_image = torch.split(image, [3, 3], dim=0)
+    left_pred, right_pred = torch.split(prediction, [1, 1], dim=0)
+    min_pred, max_pred = prediction.min(), prediction.max()
+    scaled_left_pred = (left_pred - min_pred) / (max_pred - min_pred)
+    scaled_right_pred = (right_pred - min_pred) / (max_pred - min_pred)
+    left_pred = to_heatmap(left_pred).float()
+    right_pred = to_heatmap(right_pred).float()
+    if extra is not None:
+        extra = extra.detach().float().cpu()
+        extra_split = [3, 3] if extra.size(0) == 6 else [1, 1]
+        left_extra, right_extra = torch.split(extra, extra_split, dim=0)
+        if extra.size(0) == 2:
+            left_extra = to_heatmap(left_extra).float()
+            right_extra = to_heatmap(right_extra).float()
+    images = torch.stack((left_image, right_image, left_pred, right_pred))
+    if add_scaled:
+        images = torch.cat((images, to_heatmap(scaled_left_pred).float().unsqueeze(0),
+                            to_heatmap(scaled_right_pred).float().unsqueeze(0)))
+    if extra is not None:
+        images = torch.cat((images, left_extra.unsqueeze(0), right_extra.unsqueeze(0)))
+    return make_grid(images, nrow=2).to(device)

@@ -97,6 +97,12 @@ _SIG = {
                          _P, 's']),
     'um_loss_bwd': (_I, [_I, _I, _I, _I, _P, _P, _F, _I, _F, _F, _F, _F, _F, _F, _P, _P, 's']),
     'um_image_error': (_I, [_P, _P, _I, _I, _I, _F, _P, 's']),
+    'um_ssim_ws': (_L, [_I, _I, _I]),
+    'um_ssim_gauss': (_I, [_P, _P, _I, _I, _I, _I, _F, _F, _P, _P, 's']),
+    'um_avgpool_valid': (_I, [_P, _I, _I, _I, _I, _P, 's']),
+    'um_spars_sort_ws': (_L, [_I, _I]),
+    'um_spars_sort': (_I, [_P, _P, _I, _I, _P, _P, _P, _L, 's']),
+    'um_spars_curve': (_I, [_P, _I, _I, _I, _P, _P, 's']),
     'um_adam_chunk': (_I, []),
     'um_adam_step': (_I, [_P, _P, _I, _F, _F, _F, _F, _F, _I, 's']),
     'um_adam_step_dev': (_I, [_P, _P, _I, _F, _P, _F, _F, _F, _F, _P, 's']),
