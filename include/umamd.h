@@ -159,6 +159,8 @@ int um_bn_stats_coeffs(const float* parts, int nparts, int C, double* ws, double
 int um_bn_bwd_stats_coeffs(const float* parts, int nparts, int C, double* ws, double count,
                            const float* gamma, const float* invstd, float* dgamma,
                            float* dbeta, float* k1, float* k2, float* k3, hipStream_t stream);
+/* count <= 0: read the element count from stats[2C] (SyncBN: the per-rank
+ * counts are all-reduced with the statistics) -- also for um_bn_bwd_coeffs */
 int um_bn_coeffs(const double* stats, double count, int C, const float* gamma,
                  const float* beta, float eps, float momentum, float* running_mean,
                  float* running_var, long long* num_batches_tracked, float* mean,

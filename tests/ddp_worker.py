@@ -7,6 +7,7 @@ mode 'cpu'    : gloo, CPU only -- host logic of the DP wrapper: SyncBN
 mode 'single' : one process, full batch on cuda:0, one train step.
 mode 'ddp'    : gloo ranks sharing cuda:0, each on its batch shard, one
                 DDP+SyncBN train step (SURVEY 8c golden (v): SyncBN identity).
+mode 'ddp_uneven': the same with shards of 1 and 3 images (per-rank counts).
 Writes results to <out>/<mode>_<rank>.pt (torch.save of tensors only).
 """
 import os
@@ -79,12 +80,15 @@ def run_step(mode, rank, world, out):
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     m = model_with_formula_weights(c).to(dev).train()
-    if mode == 'ddp':
+    if mode in ('ddp', 'ddp_uneven'):
         m = data_parallel(m, 0)
     left, right = batch()
-    per = left.shape[0] // world
-    left = left[rank * per:(rank + 1) * per].to(dev)
-    right = right[rank * per:(rank + 1) * per].to(dev)
+    if mode == 'ddp_uneven':  # rank 0: image 0, rank 1: images 1-3
+        sl = slice(0, 1) if rank == 0 else slice(1, 4)
+    else:
+        per = left.shape[0] // world
+        sl = slice(rank * per, (rank + 1) * per)
+    left, right = left[sl].to(dev), right[sl].to(dev)
     lf = TukraUncertaintyLoss(**c['loss'])
     opt = Adam(m.parameters(), 1e-4)
     dl, el = train_step(m, left, right, lf, opt, 0.3)
@@ -101,7 +105,7 @@ def main():
     mode, out = sys.argv[1], sys.argv[2]
     rank = int(os.environ.get('RANK', '0'))
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    if mode in ('cpu', 'ddp'):
+    if mode in ('cpu', 'ddp', 'ddp_uneven'):
         dist.init_process_group('gloo', init_method='env://', rank=rank, world_size=world)
     if mode == 'cpu':
         run_cpu(rank, world, out)

@@ -45,3 +45,22 @@ def test_syncbn_ddp_matches_single_process(tmp_path):
             # first Adam step moves each weight by ~lr * sign(grad)
             assert torch.equal(a, b), k
             assert float((a - v).abs().max()) <= 2.5e-4, k
+
+
+def test_syncbn_uneven_rank_batches(tmp_path):
+    """Shards of 1 and 3 images: SyncBN must weight each rank by its own
+    element count (torch SyncBatchNorm all-gathers the counts), so the BN
+    running statistics equal those of one process on all 4 images.  (The
+    gradients differ by design: DDP averages per-rank means equally.)"""
+    launch('single', 1, str(tmp_path))
+    launch('ddp_uneven', 2, str(tmp_path))
+    s = torch.load(tmp_path / 'single_0.pt', weights_only=True)
+    r = [torch.load(tmp_path / f'ddp_uneven_{i}.pt', weights_only=True) for i in range(2)]
+    n = 0
+    for k, v in s['state'].items():
+        if 'running' in k:
+            a, b = r[0]['state'][k], r[1]['state'][k]
+            assert torch.equal(a, b), k
+            assert float((a - v).abs().max()) <= 1e-3 * (float(v.abs().max()) + 1e-3), k
+            n += 1
+    assert n == 80

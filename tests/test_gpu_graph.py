@@ -56,7 +56,8 @@ def test_captured_step_matches_eager(dtype):
     # same parameters in: the losses agree to summation order
     for a, b in ((float(dl_e), float(dl_g)), (float(el_e), float(el_g))):
         assert abs(a - b) <= 1e-5 * abs(a) + 1e-7, (a, b)
-    assert int(opt_g._dev[0]['step']) == int(opt_e._dev[0]['step']) == 5
+    # warm-up updates are undone at capture (restore_state): 3 replays
+    assert int(opt_g._dev[0]['step']) == int(opt_e._dev[0]['step']) == 3
     se, sg = m_e.state_dict(), m_g.state_dict()
     pnames = {k for k, _ in m_e.named_parameters()}
     for k in se:
@@ -70,6 +71,36 @@ def test_captured_step_matches_eager(dtype):
             assert d <= 1e-4 * (float(se[k].abs().max()) + 1.0), (k, d)
         else:
             assert torch.equal(se[k], sg[k]), k
+
+
+def test_capture_restores_pre_warmup_state():
+    """CapturedTrainStep's eager warm-up steps are undone after capture: the
+    weights, BN buffers and Adam state equal the initial ones, and the first
+    replay matches one eager step from that initial state."""
+    from train.graph import CapturedTrainStep
+    from train.loss import TukraUncertaintyLoss
+    from train.train import train_step
+    from umamd.optim import Adam
+    cfg = _cfg()
+    cfg['loss']['error_loss_config']['loss_type'] = 'l1'
+    left, right = _uniform_pair(2, 64, 128)
+    left, right = left.to(DEV), right.to(DEV)
+    lf = TukraUncertaintyLoss(**cfg['loss'])
+    m_g = _model(cfg).train()
+    init = {k: v.clone() for k, v in m_g.state_dict().items()}
+    opt_g = Adam(m_g.parameters(), 1e-4)
+    cap = CapturedTrainStep(m_g, lf, opt_g, left, right, 0.3, warmup=2)
+    for k, v in m_g.state_dict().items():
+        assert torch.equal(v, init[k]), k
+    assert int(opt_g._dev[0]['step']) == 0
+    assert all(float(st['exp_avg'].abs().max()) == 0 for st in opt_g.state.values())
+    dl_g, el_g = cap()
+    m_e = _model(cfg).train()
+    opt_e = Adam(m_e.parameters(), 1e-4)
+    dl_e, el_e = train_step(m_e, left, right, lf, opt_e, 0.3)
+    torch.cuda.synchronize()
+    for a, b in ((float(dl_e), float(dl_g)), (float(el_e), float(el_g))):
+        assert abs(a - b) <= 1e-5 * abs(a) + 1e-7, (a, b)
 
 
 def test_set_lr_reaches_graph():

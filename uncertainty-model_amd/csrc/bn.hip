@@ -28,6 +28,9 @@ __global__ void coeffs_kernel(const double* __restrict__ st, double count, int C
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && nbt != nullptr) *nbt += 1;
   if (c >= C) return;
+  // count <= 0: the element count rides in the all-reduced buffer after the
+  // C channel pairs (SyncBN with per-rank batch sizes, no host sync)
+  if (count <= 0) count = st[2 * C];
   const double mean = st[2 * c] / count;
   double var = st[2 * c + 1] / count - mean * mean;
   if (var < 0) var = 0;
@@ -130,6 +133,7 @@ __global__ void bwd_coeffs_kernel(const double* __restrict__ st, double count, i
                                   float* __restrict__ k2, float* __restrict__ k3) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  if (count <= 0) count = st[2 * C];  // all-reduced element count (see coeffs_kernel)
   const double sdz = st[2 * c], sdzx = st[2 * c + 1];
   const float g = gamma ? gamma[c] : 1.f;
   // dx = g*invstd*(dz - sdz/n - xhat*sdzx/n)

@@ -11,6 +11,11 @@ replays it:
   graph 2: fused Adam over those gradients (pointer table uploaded once,
            step counter and lr read from device memory by the kernel)
 
+Construction runs ``warmup`` eager steps (allocator warm-up, optimiser state
+creation) and then captures; by default (``restore_state=True``) the
+parameters, BN buffers and Adam moments / step counters are put back to their
+values from before the warm-up, so the first replay is the first update.
+
 Inputs are copied into static device buffers before each replay.  Host-side
 state that the eager loop would change between steps must not change under
 a captured step: the disparity ``scale`` is fixed at capture (recapture when
@@ -32,9 +37,10 @@ from . import utils as u
 
 class CapturedTrainStep:
     def __init__(self, model, loss_function, optimiser, left, right, scale: float,
-                 scales: int = 4, warmup: int = 3):
+                 scales: int = 4, warmup: int = 3, restore_state: bool = True):
         if not hasattr(optimiser, 'prepare'):
             raise TypeError('CapturedTrainStep needs umamd.optim.Adam (graph-replayable)')
+        snap = self._snapshot(model, optimiser) if restore_state else None
         self.model, self.loss_function, self.optimiser = model, loss_function, optimiser
         self.scale, self.scales = float(scale), scales
         # weight gradients on a side stream beside the dgrad chain (umamd.overlap);
@@ -65,6 +71,39 @@ class CapturedTrainStep:
         self.g_opt = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool(), stream=side):
             optimiser.step()
+        if snap is not None:
+            self._restore(model, optimiser, snap)
+
+    @staticmethod
+    @torch.no_grad()
+    def _snapshot(model, opt):
+        params = [p.detach().clone() for p in model.parameters()]
+        bufs = [b.detach().clone() for b in model.buffers()]
+        moments = {id(p): {k: v.clone() for k, v in opt.state[p].items() if torch.is_tensor(v)}
+                   for g in opt.param_groups for p in g['params'] if p in opt.state}
+        dev = {gi: st['step'].clone() for gi, st in opt._dev.items()}
+        return params, bufs, moments, dev
+
+    @staticmethod
+    @torch.no_grad()
+    def _restore(model, opt, snap):
+        """Undo the warm-up updates in place (the captured graphs keep the
+        same tensors)."""
+        params, bufs, moments, dev = snap
+        for p, v in zip(model.parameters(), params):
+            p.copy_(v)
+        for b, v in zip(model.buffers(), bufs):
+            b.copy_(v)
+        for g in opt.param_groups:
+            for p in g['params']:
+                for k, v in opt.state.get(p, {}).items():
+                    if torch.is_tensor(v):
+                        old = moments.get(id(p), {}).get(k)
+                        v.copy_(old) if old is not None else v.zero_()
+        for gi, st in opt._dev.items():
+            old = dev.get(gi)
+            st['step'].copy_(old) if old is not None else st['step'].zero_()
+        torch.cuda.synchronize()
 
     def _fwd_bwd(self):
         images = torch.cat([self.left, self.right], dim=1)

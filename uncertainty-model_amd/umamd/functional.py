@@ -202,10 +202,14 @@ def _bn_forward_coeffs(parts, nparts, K, count, bn, sync: BNSync, training: bool
                  ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs, ptr(mean),
                  ptr(invstd), ptr(scale), ptr(shift))
         else:
-            st = torch.empty((K, 2), dtype=torch.float64, device=device)
+            # (K + 1) x 2 f64: the channel sums, then this rank's element
+            # count, all-reduced together (per-rank batches may differ, as in
+            # torch SyncBatchNorm's count all-gather) -- no host sync
+            st = torch.empty((K + 1, 2), dtype=torch.float64, device=device)
+            st[K].fill_(float(count))
             call('um_bn_stats_reduce', ptr(parts), nparts, K, ptr(st), ptr(ws))
             sync.all_reduce(st)
-            call('um_bn_coeffs', ptr(st), float(count * sync.world), K, ptr(gamma), ptr(beta),
+            call('um_bn_coeffs', ptr(st), -1.0, K, ptr(gamma), ptr(beta),
                  float(bn.eps), float(bn.momentum or 0.0), *rs,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift))
     else:
@@ -328,11 +332,12 @@ class ConvBNELUFn(torch.autograd.Function):
                 call('um_bn_bwd_stats_coeffs', ptr(parts), nb, K, ptr(ws), float(M), ptr(gamma),
                      ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(k1), ptr(k2), ptr(k3))
             else:
-                st = torch.empty((K, 2), dtype=torch.float64, device=dev)
+                st = torch.empty((K + 1, 2), dtype=torch.float64, device=dev)
+                st[K].fill_(float(M))  # this rank's count, summed by the all-reduce
                 call('um_bn_stats_reduce', ptr(parts), nb, K, ptr(st), ptr(ws))
                 st_local = st.clone()
                 ctx.sync.all_reduce(st)
-                call('um_bn_bwd_coeffs', ptr(st), float(M * world), K, ptr(gamma), ptr(invstd),
+                call('um_bn_bwd_coeffs', ptr(st), -1.0, K, ptr(gamma), ptr(invstd),
                      ptr(st_local), ptr(dgamma), ptr(dbeta), 0, ptr(k1), ptr(k2), ptr(k3))
         else:
             # no batch statistics (no BN, or BN in eval mode): dy = dz * scale
