@@ -292,6 +292,26 @@ int um_loss_bwd(int nscales, int N, int H, int W, const float* const* img,
 int um_image_error(const float* img, const float* rec, int N, int H, int W, float alpha,
                    float* out, hipStream_t stream);
 
+/* ------------------------------------------------------- adversarial ---
+ * RandomDiscriminator pieces around its EncoderStages (reference
+ * model/discriminator.py:53-86, train/loss.py:267-337).
+ */
+/* adjoint of um_image_to_nhwc: NHWC [N][H][W][ld] (dtype) -> NCHW f32 [N][C][H][W] */
+int um_nhwc_to_image(int dtype, const void* x, int N, int C, int H, int W, int ld, float* out,
+                     hipStream_t stream);
+/* prob[n] = sigmoid(b + sum w[c*HW + p] x[n][p][c]): Linear over the NCHW flatten + sigmoid */
+int um_disc_head_fwd(int dtype, const void* x, int N, int HW, int C, const float* w,
+                     const float* bias, float* prob, hipStream_t stream);
+int um_disc_head_bwd(int dtype, const void* x, int N, int HW, int C, const float* w,
+                     const float* prob, const float* dprob, void* dx, float* dw, float* db,
+                     hipStream_t stream);
+/* out[0] = mean |a - b| over n elements (ws: um_l1_mean_ws() bytes) and its backward */
+long um_l1_mean_ws(void);
+int um_l1_mean(int dtype, const void* a, const void* b, long n, double* ws, float* out,
+               hipStream_t stream);
+int um_l1_mean_bwd(int dtype, const void* a, const void* b, long n, const float* g, void* da,
+                   void* db, hipStream_t stream);
+
 /* ---------------------------------------------------------- evaluation ---
  * evaluate_model / sparsification (reference train/evaluate.py:66-196,
  * train/sparsification.py:8-61).  Off the training hot path.

@@ -75,6 +75,31 @@ def param_specs(model_cfg, graphs) -> List[Tuple[str, tuple, str]]:
     return specs
 
 
+def disc_param_specs(disc_cfg, graphs) -> List[Tuple[str, tuple, str]]:
+    """state_dict schema of reference model/discriminator.py:33-51 (the
+    encoder-stage layout of param_specs under ``layers.{s}`` and ``conv``,
+    then ``linear``).  ``graphs`` holds one graph per stage incl. the final
+    one (stage len(layers) + 1)."""
+    specs: List[Tuple[str, tuple, str]] = []
+    stages = list(disc_cfg['layers']) + [disc_cfg['final_conv']]
+    for s, lay in enumerate(stages):
+        base = f'layers.{s}.' if s < len(disc_cfg['layers']) else 'conv.'
+        nodes, _, _ = og.graph_info(graphs[s])
+        cin, cout, k = lay['in_channels'], lay['out_channels'], lay['kernel_size']
+        for node in nodes:
+            pre = f'{base}layers.0.node_blocks.{node.id}.'
+            if len(node.inputs) > 1:
+                specs.append((pre + 'mean_weight', (len(node.inputs),), 'mean_weight'))
+            ci = cin if node.node_type == 'input' else cout
+            _conv(specs, pre + 'convolution.layers.0.', ci, cout, k)
+            _bn(specs, pre + 'convolution.layers.1.', cout)
+        for nm in ('keys', 'queries', 'values', 'reprojection'):
+            _conv(specs, f'{base}layers.1.{nm}.', cout, cout, 1)
+    specs.append(('linear.weight', (1, disc_cfg['linear_in_features']), 'fc'))
+    specs.append(('linear.bias', (1,), 'conv_bias'))
+    return specs
+
+
 def _formula(name: str, n: int, lo: float, hi: float) -> torch.Tensor:
     """Deterministic values in [lo, hi] from (name, index): a low-discrepancy
     sine sequence keyed by crc32(name)."""

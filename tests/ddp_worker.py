@@ -91,7 +91,7 @@ def run_step(mode, rank, world, out):
     left, right = left[sl].to(dev), right[sl].to(dev)
     lf = TukraUncertaintyLoss(**c['loss'])
     opt = Adam(m.parameters(), 1e-4)
-    dl, el = train_step(m, left, right, lf, opt, 0.3)
+    dl, el, _ = train_step(m, left, right, lf, opt, 0.3)
     torch.cuda.synchronize()
     # Adam reads .grad but does not modify it; under DDP these are the
     # all-reduced (averaged) bucket views

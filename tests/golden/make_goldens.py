@@ -355,6 +355,106 @@ def gen_sparsification():
          ause=ref_s.ause(oracle, pred))
 
 
+def disc_setup(cfg, h, w):
+    """discriminator config for an h x w input (linear_in_features follows
+    the final map: C * h/32 * w/32) and its formula weights"""
+    sys.path.insert(0, REPO)
+    from oracle import graph as og  # noqa: E402
+    from oracle import step as OS  # noqa: E402
+    dcfg = json.loads(json.dumps(cfg['discriminator']))
+    dcfg['linear_in_features'] = dcfg['final_conv']['out_channels'] * (h // 32) * (w // 32)
+    nstages = len(dcfg['layers']) + 1
+    graphs = [og.load_json(os.path.join(REPO, 'graphs', 'nodes_5_seed_42', f'stage_{s}.json'))
+              for s in range(1, nstages + 1)]
+    return dcfg, OS.formula_state_dict(OS.disc_param_specs(dcfg, graphs))
+
+
+def gen_adversarial(ref_model, ref_loss, ref_utils, cfg):
+    """RandomDiscriminator forward/features, GeneratorLoss, PerceptualLoss,
+    run_discriminator (model/discriminator.py, train/loss.py:267-337,
+    train/utils.py:248-273) and two adversarial training steps
+    (train/train.py:112-152) at B=2, 64x128 with formula weights."""
+    b, h, w = 2, 64, 128
+    dcfg, dsd = disc_setup(cfg, h, w)
+    rcfg = json.loads(json.dumps(dcfg))
+    rcfg['load_graph'] = os.path.join(REF, 'graphs', 'nodes_5_seed_42')
+    disc = ref_model.RandomDiscriminator(**rcfg)
+    assert list(disc.state_dict().keys()) == list(dsd.keys()), 'disc schema'
+    disc.load_state_dict(dsd)
+    disc.train()
+    left, right, _ = stereo_pair(b, h, w, seed=808)
+    pyr = ref_utils.scale_pyramid(torch.cat([left, right], 1), 4)
+    preds = [p.requires_grad_(True) for p in pred_pyramid(b, h, w, seed=909)]
+    recon = ref_utils.reconstruct_pyramid(preds, pyr)
+    arrays = {'left': left, 'right': right, 'disc_cfg': np.array(json.dumps(dcfg))}
+    for i, p in enumerate(preds):
+        arrays[f'pred{i}'] = p.detach()
+    with torch.no_grad():
+        d2 = ref_model.RandomDiscriminator(**rcfg)
+        d2.load_state_dict(dsd)
+        d2.train()
+        arrays['prob_images'] = d2(pyr)
+        for i, f in enumerate(d2.features(pyr)):
+            arrays[f'feat{i}_sum'] = f.double().sum()
+            arrays[f'feat{i}_abssum'] = f.double().abs().sum()
+    gen = ref_loss.GeneratorLoss('mse')(recon, disc)
+    per = ref_loss.PerceptualLoss()(pyr, recon, disc)
+    arrays['generator_loss'] = gen.detach()
+    arrays['perceptual_loss'] = per.detach()
+    g = torch.autograd.grad(gen * 0.85 + per * 0.05, preds)
+    for i, gi in enumerate(g):
+        arrays[f'adv_grad{i}'] = gi
+    d3 = ref_model.RandomDiscriminator(**rcfg)
+    d3.load_state_dict(dsd)
+    d3.train()
+    dl = ref_utils.run_discriminator(pyr, recon, d3, torch.nn.BCELoss(), b)
+    dl.backward()
+    arrays['disc_loss'] = dl.detach()
+    for k, p in d3.named_parameters():
+        arrays[f'disc_gradnorm/{k}'] = p.grad.double().norm()
+    # two adversarial training steps (reference train_one_epoch body)
+    from copy import deepcopy
+    sd, _ = _formula_weights(cfg)
+    m = _ref_model(ref_model, cfg)
+    m.load_state_dict(sd)
+    m.train()
+    lcfg = json.loads(json.dumps(cfg['loss']))
+    lcfg['error_loss_config']['loss_type'] = 'bayesian'
+    lcfg['perceptual_start'] = 1  # the perceptual term from batch 1 on
+    lf = ref_loss.TukraUncertaintyLoss(**lcfg)
+    d4 = ref_model.RandomDiscriminator(**rcfg)
+    d4.load_state_dict(dsd)
+    d4.train()
+    opt = torch.optim.Adam(m.parameters(), 1e-4)
+    dopt = torch.optim.Adam(d4.parameters(), 1e-4)
+    clone = deepcopy(d4)
+    for i in range(2):
+        images = torch.cat([left, right], 1)
+        pyr = ref_utils.scale_pyramid(images, 4)
+        opt.zero_grad()
+        disps = m(left, 0.3)
+        rec = ref_utils.reconstruct_pyramid(disps, pyr)
+        dl_, el_ = lf(pyr, disps, rec, i, clone)
+        (dl_ + el_).backward()
+        opt.step()
+        dopt.zero_grad()
+        dsl = ref_utils.run_discriminator(pyr, rec, d4, torch.nn.BCELoss(), b)
+        dsl.backward()
+        dopt.step()
+        if i % 10 == 0:
+            clone.load_state_dict(d4.state_dict())
+        arrays[f'step_disp_{i}'] = dl_.detach()
+        arrays[f'step_err_{i}'] = el_.detach()
+        arrays[f'step_disc_{i}'] = dsl.detach()
+        if i == 0:  # parameters after the first model and discriminator updates
+            for pre, mod in (('model', m), ('disc', d4)):
+                for k, v in mod.state_dict().items():
+                    if v.is_floating_point():
+                        arrays[f'{pre}_sum/{k}'] = v.double().sum()
+                        arrays[f'{pre}_abs/{k}'] = v.double().abs().sum()
+    save('adversarial.npz', **arrays)
+
+
 def main():
     ref_model, ref_loss, ref_utils = import_reference()
     torch.set_num_threads(8)
@@ -363,7 +463,7 @@ def main():
     with open(os.path.join(REPO, 'config_nodes10.yml')) as f:
         cfg10 = yaml.safe_load(f)
     which = sys.argv[1:] or ['warp', 'loss', 'model', 'step', 'nodes10', 'c1', 'transforms',
-                             'sparsification']
+                             'sparsification', 'adversarial']
     if 'warp' in which:
         gen_warp(ref_utils)
     if 'loss' in which:
@@ -383,6 +483,8 @@ def main():
         gen_transforms()
     if 'sparsification' in which:
         gen_sparsification()
+    if 'adversarial' in which:
+        gen_adversarial(ref_model, ref_loss, ref_utils, cfg)
 
 
 if __name__ == '__main__':

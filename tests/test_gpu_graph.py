@@ -50,7 +50,7 @@ def test_captured_step_matches_eager(dtype):
     m_e = _model(cfg, dtype).train()
     m_e.load_state_dict(m_g.state_dict())
     opt_e = _adam_clone(opt_g, m_g, m_e)
-    dl_e, el_e = train_step(m_e, left, right, lf, opt_e, 0.3)
+    dl_e, el_e, _ = train_step(m_e, left, right, lf, opt_e, 0.3)
     dl_g, el_g = cap()
     torch.cuda.synchronize()
     # same parameters in: the losses agree to summation order
@@ -97,7 +97,7 @@ def test_capture_restores_pre_warmup_state():
     dl_g, el_g = cap()
     m_e = _model(cfg).train()
     opt_e = Adam(m_e.parameters(), 1e-4)
-    dl_e, el_e = train_step(m_e, left, right, lf, opt_e, 0.3)
+    dl_e, el_e, _ = train_step(m_e, left, right, lf, opt_e, 0.3)
     torch.cuda.synchronize()
     for a, b in ((float(dl_e), float(dl_g)), (float(el_e), float(el_g))):
         assert abs(a - b) <= 1e-5 * abs(a) + 1e-7, (a, b)

@@ -220,7 +220,7 @@ def test_train_step_fp32(lt):
             assert not bad, bad[:8]
             opt.step()
         else:
-            dl, el = train_step(m, left, right, lf, opt, scale, 4, step)
+            dl, el, _ = train_step(m, left, right, lf, opt, scale, 4, step)
         rel = 1e-3 if step == 0 else 5e-3
         assert abs(float(dl) / float(z[f'disp_loss_{step}']) - 1) < rel, step
         assert abs(float(el) / float(z[f'error_loss_{step}']) - 1) < rel, step
@@ -363,7 +363,7 @@ def test_train_step_config2_bf16_properties():
     losses = []
     for m in (m16, m32):
         opt = Adam(m.parameters(), 1e-4)
-        dl, el = train_step(m, left, right, lf, opt, 0.3)
+        dl, el, _ = train_step(m, left, right, lf, opt, 0.3)
         torch.cuda.synchronize()
         assert torch.isfinite(dl) and torch.isfinite(el)
         for k, p in m.named_parameters():

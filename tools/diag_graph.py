@@ -13,7 +13,7 @@ lf = TukraUncertaintyLoss(**cfg['loss'])
 def eager(n):
     m = _model(cfg).train(); o = Adam(m.parameters(), 1e-4); out = []
     for _ in range(n):
-        dl, el = train_step(m, left, right, lf, o, 0.3); out.append((float(dl), float(el)))
+        dl, el, _ = train_step(m, left, right, lf, o, 0.3); out.append((float(dl), float(el)))
     return m, out
 m1, e1 = eager(8); m2, e2 = eager(8)
 print('eager1', e1); print('eager2', e2)

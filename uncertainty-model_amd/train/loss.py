@@ -18,8 +18,11 @@ import torch
 import torch.nn as nn
 from torch import Tensor
 from torch.nn import Module
+from torch.nn.parallel import DistributedDataParallel
 
+from umamd import discfn as DF
 from umamd import lossfn as LF
+from umamd import packer as P
 
 from .utils import ImagePyramid
 
@@ -66,16 +69,41 @@ class SmoothnessLoss(_FusedOnly):
     """Edge-aware smoothness (reference :191-264)."""
 
 
-class PerceptualLoss(_FusedOnly):
-    """Discriminator feature L1 (reference :267-305); adversarial path, not implemented."""
+def _disc_module(disc: Module) -> Module:
+    # discriminator methods are reached through .module under DDP (reference :294-299)
+    return disc.module if isinstance(disc, DistributedDataParallel) else disc
 
 
-class GeneratorLoss(_FusedOnly):
-    """GAN generator loss (reference :308-337); adversarial path, not implemented."""
+class PerceptualLoss(nn.Module):
+    """Discriminator feature reconstruction L1 (reference :267-305): sum over
+    the discriminator stages of mean |features(image) - features(recon)|,
+    on the NHWC feature maps (one fused L1 launch per stage)."""
+
+    def forward(self, image_pyramid: ImagePyramid, recon_pyramid: ImagePyramid,
+                disc: Module) -> Tensor:
+        d = _disc_module(disc)
+        with P.scope(d._packer):
+            image_maps = d._features(image_pyramid)
+            recon_maps = d._features(recon_pyramid)
+        perceptual_loss = 0
+        for image_map, recon_map in zip(image_maps, recon_maps):
+            perceptual_loss = perceptual_loss + DF.l1_mean(image_map, recon_map)
+        return perceptual_loss
+
+
+class GeneratorLoss(nn.Module):
+    """Loss of failing to convince the discriminator (reference :308-337):
+    ``self.adversarial`` (MSE or BCE) of the discriminator's predictions on
+    the reconstructions against ones."""
 
     def __init__(self, loss: str = 'mse') -> None:
         super().__init__()
         self.adversarial = nn.MSELoss() if loss == 'mse' else nn.BCELoss()
+
+    def forward(self, recon_pyramid: ImagePyramid, discriminator: Module) -> Tensor:
+        predictions = discriminator(recon_pyramid)
+        labels = torch.ones_like(predictions)
+        return self.adversarial(predictions, labels)
 
 
 class ReprojectionErrorLoss(_FusedOnly):
@@ -133,8 +161,6 @@ class TukraUncertaintyLoss(nn.Module):
     def forward(self, image_pyramid: ImagePyramid, predictions: ImagePyramid,
                 recon_pyramid: ImagePyramid, epoch: Optional[int] = None,
                 discriminator: Optional[Module] = None):
-        if discriminator is not None:
-            raise NotImplementedError('umamd: adversarial loss terms are not implemented yet')
         for p, im, r in zip(predictions, image_pyramid, recon_pyramid):
             tag = getattr(r, '_umamd_recon', None)
             if tag is None or tag != (id(p), id(im)):
@@ -150,4 +176,12 @@ class TukraUncertaintyLoss(nn.Module):
             list(recon_pyramid) if pending else None)
         self.wssim._previous_image_error = emap
         self.last_terms = terms  # [disp, error, wssim, consistency, smoothness, error-term]
+        if discriminator is not None:
+            # adversarial terms (reference :552-564); the recon pyramid carries
+            # the gradient back to the disparities through the warp adjoint
+            adversarial_loss = self.adversarial(recon_pyramid, discriminator)
+            disp_loss = disp_loss + adversarial_loss * self.adversarial_weight
+            if epoch is not None and epoch >= self.perceptual_start:
+                perceptual_loss = self.perceptual(image_pyramid, recon_pyramid, discriminator)
+                disp_loss = disp_loss + perceptual_loss * self.perceptual_weight
         return disp_loss, error_loss

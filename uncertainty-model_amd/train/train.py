@@ -41,9 +41,12 @@ def save_model(model: Module, save_model_to: str, disc: Optional[Module] = None,
 
 
 def train_step(model: Module, left, right, loss_function: Module, optimiser: Optimizer,
-               scale: float, scales: int = 4, batch_index: int = 0):
-    """One step of the reference loop body (train.py:116-129) without logging;
-    returns the (disp_loss, error_loss) device tensors."""
+               scale: float, scales: int = 4, batch_index: int = 0,
+               disc: Optional[Module] = None, disc_clone: Optional[Module] = None,
+               disc_optimiser: Optional[Optimizer] = None,
+               disc_loss_function: Optional[Module] = None):
+    """One step of the reference loop body (train.py:114-149) without
+    logging; returns (disp_loss, error_loss, disc_loss or None) device tensors."""
     images = torch.cat([left, right], dim=1)
     image_pyramid = u.scale_pyramid(images, scales)
     optimiser.zero_grad()
@@ -51,10 +54,17 @@ def train_step(model: Module, left, right, loss_function: Module, optimiser: Opt
     with LF.deferred_recon():  # the fused loss forward writes the recon
         recon_pyramid = u.reconstruct_pyramid(disparities, image_pyramid)
     disp_loss, error_loss = loss_function(image_pyramid, disparities, recon_pyramid,
-                                          batch_index, None)
+                                          batch_index, disc_clone)
     (disp_loss + error_loss).backward()
     optimiser.step()
-    return disp_loss, error_loss
+    disc_loss = None
+    if disc is not None:
+        disc_optimiser.zero_grad()
+        disc_loss = u.run_discriminator(image_pyramid, recon_pyramid, disc, disc_loss_function,
+                                        left.shape[0])
+        disc_loss.backward()
+        disc_optimiser.step()
+    return disp_loss, error_loss, disc_loss
 
 
 def train_one_epoch(model: Module, loader: DataLoader, loss_function: Module,
@@ -65,35 +75,45 @@ def train_one_epoch(model: Module, loader: DataLoader, loss_function: Module,
                     epoch_number: Optional[int] = None, scales: int = 4,
                     perceptual_update_freq: int = 10, device: Device = 'cpu',
                     no_pbar: bool = False, rank: int = 0) -> Tuple[float, float]:
-    if disc is not None:
-        raise NotImplementedError('umamd: adversarial training is not implemented yet')
+    """Reference train/train.py:51-170."""
     model.train()
-    running_disp_loss = running_error_loss = 0.0
-    disp_loss_per_image = unc_loss_per_image = None
+    if disc is not None:
+        disc.train()
+    running_disp_loss = running_error_loss = running_disc_loss = 0.0
+    disp_loss_per_image = unc_loss_per_image = disc_loss_per_image = None
     batch_size = loader.batch_size if loader.batch_size is not None else len(loader)
     description = f'Epoch #{epoch_number}' if epoch_number is not None else 'Epoch'
+    disc_clone = deepcopy(disc) if disc is not None else None
     it = tqdm.tqdm(loader, description, unit='batch', disable=(no_pbar or rank > 0)) \
         if tqdm is not None else loader
     for i, image_pair in enumerate(it):
         left = image_pair['left'].to(device)
         right = image_pair['right'].to(device)
-        disp_loss, error_loss = train_step(model, left, right, loss_function,
-                                           model_optimiser, scale, scales, i)
+        disp_loss, error_loss, disc_loss = train_step(
+            model, left, right, loss_function, model_optimiser, scale, scales, i, disc,
+            disc_clone, disc_optimiser, disc_loss_function)
         if rank == 0:
             running_disp_loss += disp_loss.item()
             running_error_loss += error_loss.item()
             disp_loss_per_image = running_disp_loss / ((i + 1) * batch_size)
             unc_loss_per_image = running_error_loss / ((i + 1) * batch_size)
-            if tqdm is not None and hasattr(it, 'set_postfix'):
-                it.set_postfix(disp=disp_loss_per_image, unc=unc_loss_per_image,
-                               disc=None, scale=scale)
+            if disc_loss is not None:
+                running_disc_loss += disc_loss.item()
+                disc_loss_per_image = running_disc_loss / ((i + 1) * batch_size)
+        if disc is not None and i % perceptual_update_freq == 0:
+            disc_clone.load_state_dict(disc.state_dict())
+        if rank == 0 and tqdm is not None and hasattr(it, 'set_postfix'):
+            it.set_postfix(disp=disp_loss_per_image, unc=unc_loss_per_image,
+                           disc=disc_loss_per_image, scale=scale)
     if no_pbar and rank == 0:
+        disc_loss_string = f'{disc_loss_per_image:.2e}' \
+            if disc_loss_per_image is not None else None
         print(f'{description}:'
               f'\n\tdisparity loss: {disp_loss_per_image:.2e}'
               f'\n\tuncertainty loss: {unc_loss_per_image:.2e}'
-              f'\n\tdiscriminator loss: None'
+              f'\n\tdiscriminator loss: {disc_loss_string}'
               f'\n\tdisparity scale: {scale:.2f}')
-    return disp_loss_per_image, unc_loss_per_image, None
+    return disp_loss_per_image, unc_loss_per_image, disc_loss_per_image
 
 
 def train_model(model: Module, loader: DataLoader, loss_function: Module,
@@ -113,12 +133,13 @@ def train_model(model: Module, loader: DataLoader, loss_function: Module,
     """Epoch loop with the reference's LR / disparity-scale schedules (:173-267)."""
     from .evaluate import evaluate_model
     model_optimiser = Adam(model.parameters(), learning_rate)
+    disc_optimiser = Adam(disc.parameters(), learning_rate) if disc is not None else None
     training_losses, validation_metrics = [], []
     for i in range(epochs):
         adjust_learning_rate(model_optimiser, i, learning_rate)
         scale = 1 if finetune else adjust_disparity(i)
         loss = train_one_epoch(model, loader, loss_function, model_optimiser, scale, disc,
-                               None, disc_loss_function, epoch_number=(i + 1),
+                               disc_optimiser, disc_loss_function, epoch_number=(i + 1),
                                perceptual_update_freq=perceptual_update_freq, device=device,
                                no_pbar=no_pbar, rank=rank)
         if rank == 0:

@@ -87,6 +87,18 @@ def adjust_learning_rate(optimiser: Optimizer, epoch: int, lr: float,
         group['lr'] = target
 
 
+def run_discriminator(image_pyramid: ImagePyramid, recon_pyramid: ImagePyramid,
+                      discriminator, disc_loss_function, batch_size: int) -> Tensor:
+    """Discriminator predictions on real (label 1) and detached reconstructed
+    (label 0) pyramids and its loss / 2 (reference :248-273)."""
+    recon_pyramid = detach_pyramid(recon_pyramid)
+    pyramid = concatenate_pyramids(image_pyramid, recon_pyramid)
+    predictions = discriminator(pyramid)
+    labels = torch.zeros_like(predictions)
+    labels[:batch_size] = 1
+    return disc_loss_function(predictions, labels) / 2
+
+
 # ------------------------------------------------ visualisation (host) ----
 # reference train/utils.py:177-245,276-325 and the torchvision.utils
 # make_grid / save_image they rely on (torchvision is not in this image)

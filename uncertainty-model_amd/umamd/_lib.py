@@ -97,6 +97,12 @@ _SIG = {
                          _P, 's']),
     'um_loss_bwd': (_I, [_I, _I, _I, _I, _P, _P, _F, _I, _F, _F, _F, _F, _F, _F, _P, _P, 's']),
     'um_image_error': (_I, [_P, _P, _I, _I, _I, _F, _P, 's']),
+    'um_nhwc_to_image': (_I, [_I, _P, _I, _I, _I, _I, _I, _P, 's']),
+    'um_disc_head_fwd': (_I, [_I, _P, _I, _I, _I, _P, _P, _P, 's']),
+    'um_disc_head_bwd': (_I, [_I, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, 's']),
+    'um_l1_mean_ws': (_L, []),
+    'um_l1_mean': (_I, [_I, _P, _P, _L, _P, _P, 's']),
+    'um_l1_mean_bwd': (_I, [_I, _P, _P, _L, _P, _P, _P, 's']),
     'um_ssim_ws': (_L, [_I, _I, _I]),
     'um_ssim_gauss': (_I, [_P, _P, _I, _I, _I, _I, _F, _F, _P, _P, 's']),
     'um_avgpool_valid': (_I, [_P, _I, _I, _I, _I, _P, 's']),
