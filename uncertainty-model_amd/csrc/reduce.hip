@@ -16,6 +16,8 @@
 // per BN layer and per direction.  The ticket counters are static device
 // words reset by the last workgroup, so launches of one entry must be
 // stream-ordered (one stream per process, as everywhere in umamd).
+#include <cstdlib>
+
 #include "common.h"
 #include "reduce.h"
 
@@ -210,12 +212,18 @@ namespace umamd {
 // agent-scope release/acquire pair costs about as much as a kernel boundary,
 // MI355X_MICROARCH.md price list).  Larger: 256-thread workgroups of >= 16K
 // values each and the last-arriver finish.
-constexpr long COLRED_SINGLE = 128 * 1024;
+// (UMAMD_COLRED_SINGLE / UMAMD_COLRED_PER override the two sizes for sweeps)
+static long env_long(const char* n, long d) {
+  const char* v = getenv(n);
+  return v ? atol(v) : d;
+}
 
 int colred_blocks(int nparts, int C, int NV) {
+  static const long single = env_long("UMAMD_COLRED_SINGLE", 128 * 1024);
+  static const long per = env_long("UMAMD_COLRED_PER", 16384);
   const long work = (long)nparts * C * NV;
-  if (work <= COLRED_SINGLE) return 1;
-  long b = (work + 16383) / 16384;  // >= 16K values per workgroup
+  if (work <= single) return 1;
+  long b = (work + per - 1) / per;  // >= `per` values per workgroup
   if (b > 128) b = 128;
   if (b > nparts) b = nparts;
   if (b < 1) b = 1;
