@@ -49,7 +49,9 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--no-graph', action='store_true',
-                    help='eager launches instead of the captured HIP graph (N=1)')
+                    help='eager launches instead of the captured HIP graph')
+    ap.add_argument('--eager-steps', type=int, default=3,
+                    help='N=1: also time this many eagerly launched steps (reported beside)')
     ap.add_argument('--cpu-sample-batch', type=int, default=2)
     ap.add_argument('--cpu-sample-steps', type=int, default=2)
     return ap.parse_args()
@@ -65,13 +67,15 @@ def load_cfg(path, loss_type):
     return cfg
 
 
-def build(cfg, dtype, device, world):
+def build(cfg, dtype, device, world, dp=None):
     import model as M
     from train.loss import TukraUncertaintyLoss
     from umamd.optim import Adam
     torch.manual_seed(0)
     m = M.RandomlyConnectedModel(**cfg['model'], dtype=dtype).to(device).train()
-    if world > 1:
+    if dp is None:
+        dp = world > 1
+    if dp:
         from train.parallel import data_parallel
         m = data_parallel(m, device.index)
     lf = TukraUncertaintyLoss(**cfg['loss'])
@@ -92,6 +96,20 @@ def step(m, lf, opt, left, right, scale):
     (dl + el).backward()
     opt.step()
     return dl, el
+
+
+def time_eager(m, lf, opt, left, right, scale, batch, steps):
+    """The same step launched eagerly from Python, for comparison with the
+    captured graph (after the timed region; the graphs are not replayed
+    again)."""
+    step(m, lf, opt, left, right, scale)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        step(m, lf, opt, left, right, scale)
+    torch.cuda.synchronize()
+    te = (time.perf_counter() - t1) / steps
+    return {'value': round(batch / te, 2), 'ms_per_step': round(te * 1e3, 3), 'steps': steps}
 
 
 # ------------------------------------------------------------- roofline ----
@@ -241,7 +259,10 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
+    # UMAMD_DIST=1 (under torchrun) runs the data-parallel path even with one
+    # rank: the DDP wrapper and the captured RCCL all-reduce on a 1-GPU box
+    dp = world > 1 or os.environ.get('UMAMD_DIST') == '1'
+    if dp:
         # 'nccl' is RCCL; UMAMD_DIST_BACKEND=gloo rehearses the N>1 path with
         # several ranks on one GPU (RCCL needs a GPU per rank)
         dist.init_process_group(os.environ.get('UMAMD_DIST_BACKEND', 'nccl'),
@@ -250,17 +271,24 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device('cuda', local)
     cfg = load_cfg(a.config, a.loss_type)
-    m, lf, opt = build(cfg, a.dtype, device, world)
+    use_graph = not a.no_graph
+    # the graph is captured on this stream; DDP is constructed under it (it
+    # keeps the parameters' AccumulateGrad nodes, which remember their stream)
+    cap_stream = torch.cuda.Stream() if use_graph else torch.cuda.current_stream()
+    with torch.cuda.stream(cap_stream):
+        m, lf, opt = build(cfg, a.dtype, device, world, dp)
+    torch.cuda.current_stream().wait_stream(cap_stream)
     g = torch.Generator(device='cpu').manual_seed(1234 + rank)
     left = torch.rand(a.batch, 3, a.height, a.width, generator=g).to(device)
     right = torch.rand(a.batch, 3, a.height, a.width, generator=g).to(device)
     scale = 0.3  # adjust_disparity(0)
 
-    use_graph = world == 1 and not a.no_graph
     if use_graph:
         from train.graph import CapturedTrainStep
         # the capture's own eager warm-up steps count toward W; one replay warms the graph
-        cap = CapturedTrainStep(m, lf, opt, left, right, scale, warmup=max(1, a.warmup - 1))
+        # (N>1: SyncBN and the gradient all-reduce are RCCL nodes inside the graph)
+        cap = CapturedTrainStep(m, lf, opt, left, right, scale, warmup=max(1, a.warmup - 1),
+                                stream=cap_stream)
         run = cap
         run()
     else:
@@ -286,9 +314,16 @@ def main():
         elapsed = float(t)
     losses = (float(dl), float(el))
 
-    roof = None
-    if not a.no_roofline:
-        roof = measure_roofline(m, lf, opt, left, right, scale, a.dtype)
+    # the eager comparison and the roofline pass launch on the stream the
+    # model (and DDP) was built under
+    with torch.cuda.stream(cap_stream):
+        eager = None
+        if use_graph and world == 1 and a.eager_steps > 0:
+            eager = time_eager(m, lf, opt, left, right, scale, a.batch, a.eager_steps)
+        roof = None
+        if not a.no_roofline:
+            roof = measure_roofline(m, lf, opt, left, right, scale, a.dtype)
+        torch.cuda.synchronize()
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(cfg, a.height, a.width, a.cpu_sample_batch, a.cpu_sample_steps)
@@ -308,15 +343,16 @@ def main():
                                    f'{"2" if world == 1 else "4"}): fwd+4-scale loss+bwd+Adam',
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch,
                        'height': a.height, 'width': a.width, 'loss': a.loss_type,
-                       'parallelism': f'dp{world}' + ('+syncbn' if world > 1 else ''),
+                       'parallelism': f'dp{world}' + ('+syncbn' if dp else ''),
                        'launch': 'hip-graph' if use_graph else 'eager',
                        'graph': 'config.yml (nodes=5, K5 stage graphs)'},
+            'eager_launch': eager,
             'final_losses': {'disp': round(losses[0], 5), 'error': round(losses[1], 5)},
             'roofline': roof,
             'cpu_baseline': cpu,
         }
         print(json.dumps(out))
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 

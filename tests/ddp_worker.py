@@ -63,7 +63,22 @@ def run_cpu(rank, world, out):
     x = torch.ones(3, 8) * (rank + 1)
     dp(x).sum().backward()
     nparams = sum(p.numel() for p in model_with_formula_weights(c).parameters())
-    torch.save({'n_sync_bn': torch.tensor(count_sync_bn(sm)),
+    # the captured step's own gradient exchange (train/graph.py _reduce_grads:
+    # pack -> one all-reduce -> .grad views), host logic on the same module;
+    # the third Linear is unused and keeps .grad None
+    from train.graph import CapturedTrainStep
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Linear(16, 4),
+                              torch.nn.Linear(4, 4))
+    net[1](net[0](x)).sum().backward()
+    cs = CapturedTrainStep.__new__(CapturedTrainStep)
+    cs.model, cs.group, cs.world = net, dist.group.WORLD, world
+    cs._flat = cs._layout = cs._raw = None
+    cs._reduce_grads()
+    flat_grads = [p.grad.clone() for p in list(net.parameters())[:4]]
+    assert all(p.grad is None for p in net[2].parameters())
+    assert all(p.grad.data_ptr() >= cs._flat.data_ptr() for p in list(net.parameters())[:4])
+    torch.save({'flat_grads': flat_grads,'n_sync_bn': torch.tensor(count_sync_bn(sm)),
                 'world_seen': torch.tensor(BNSync(bns[0]).world),
                 'stats': st,
                 'grads': [p.grad.clone() for p in dp.parameters()],

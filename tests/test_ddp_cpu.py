@@ -57,3 +57,6 @@ def test_dp_wrapper_gloo_world2(tmp_path):
     for x in r:
         for a, b in zip(x['grads'], g):
             assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)
+        # CapturedTrainStep's packed all-reduce gives DDP's average
+        for a, b in zip(x['flat_grads'], g):
+            assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)

@@ -162,3 +162,60 @@ def test_wgrad_side_stream_matches_single_stream(dtype):
     with pytest.raises(RuntimeError):
         with ov:
             pass
+
+
+def test_captured_ddp_step_one_rank():
+    """The data-parallel captured step (DDP wrapper, SyncBN statistics and
+    the packed gradient all-reduce recorded in the graph as RCCL nodes) on a
+    one-rank 'nccl' group -- the only RCCL group a 1-GPU box can form: it
+    captures, replays, leaves .grad as views of the reduced buffer and tracks
+    the single-process eager step (at world 1 the average is the identity)."""
+    import socket
+    import torch.distributed as dist
+    from train.graph import CapturedTrainStep
+    from train.loss import TukraUncertaintyLoss
+    from train.parallel import data_parallel, unwrap
+    from train.train import train_step
+    from umamd.functional import BNSync
+    from umamd.optim import Adam
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{port}', rank=0,
+                            world_size=1)
+    BNSync.force = True
+    try:
+        cfg = _cfg()
+        cfg['loss']['error_loss_config']['loss_type'] = 'l1'
+        left, right = _uniform_pair(2, 64, 128)
+        left, right = left.to(DEV), right.to(DEV)
+        lf = TukraUncertaintyLoss(**cfg['loss'])
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):  # DDP under the capture stream
+            m_g = data_parallel(_model(cfg).train(), 0)
+        torch.cuda.current_stream().wait_stream(st)
+        opt_g = Adam(m_g.parameters(), 1e-4)
+        cap = CapturedTrainStep(m_g, lf, opt_g, left, right, 0.3, warmup=2, stream=st)
+        assert cap.group is not None and cap.world == 1
+        for _ in range(2):
+            cap()
+        torch.cuda.synchronize()
+        lo = cap._flat.data_ptr()
+        hi = lo + cap._flat.numel() * 4
+        for p in unwrap(m_g).parameters():
+            assert lo <= p.grad.data_ptr() < hi
+        m_e = _model(cfg).train()
+        m_e.load_state_dict(unwrap(m_g).state_dict())
+        opt_e = _adam_clone(opt_g, unwrap(m_g), m_e)
+        dl_e, el_e, _ = train_step(m_e, left, right, lf, opt_e, 0.3)
+        dl_g, el_g = cap()
+        torch.cuda.synchronize()
+        for a, b in ((float(dl_e), float(dl_g)), (float(el_e), float(el_g))):
+            assert abs(a - b) <= 1e-5 * abs(a) + 1e-7, (a, b)
+        ge = {k: p.grad for k, p in m_e.named_parameters()}
+        for k, p in unwrap(m_g).named_parameters():
+            d = float((p.grad - ge[k]).norm())
+            assert d <= 1e-3 * float(ge[k].norm()) + 1e-5, (k, d)
+    finally:
+        BNSync.force = False
+        dist.destroy_process_group()

@@ -20,14 +20,27 @@ Inputs are copied into static device buffers before each replay.  Host-side
 state that the eager loop would change between steps must not change under
 a captured step: the disparity ``scale`` is fixed at capture (recapture when
 ``adjust_disparity`` moves it) and the learning rate goes through
-``umamd.optim.Adam.set_lr``.  Single-process only: the DDP gradient
-all-reduce runs eagerly.
+``umamd.optim.Adam.set_lr``.
+
+Data parallel (one process per GPU, model wrapped by train.parallel): the
+captured forward runs the wrapped module directly, so DDP's autograd hooks
+stay idle, and graph 1 ends with the gradient exchange itself -- the
+gradients are packed into one flat f32 buffer and averaged with a single
+RCCL all-reduce recorded in the graph (SyncBN's statistic all-reduces are
+recorded the same way).  ``.grad`` of each parameter is then a view of the
+reduced buffer, which is what the fused Adam's pointer table holds.  DDP
+construction still broadcasts rank 0's parameters, and its module keeps the
+reference's ``module.`` checkpoint keys; construct it under the capture
+stream (``stream=``).
 """
 from __future__ import annotations
 
 import os
+import time
 
 import torch
+from torch import distributed as dist
+from torch.nn.parallel import DistributedDataParallel
 
 from umamd import lossfn as LF
 from umamd import overlap
@@ -37,9 +50,25 @@ from . import utils as u
 
 class CapturedTrainStep:
     def __init__(self, model, loss_function, optimiser, left, right, scale: float,
-                 scales: int = 4, warmup: int = 3, restore_state: bool = True):
+                 scales: int = 4, warmup: int = 3, restore_state: bool = True,
+                 stream=None):
+        """``stream``: the stream to warm up and capture on (default: a new
+        one).  A DistributedDataParallel model must have been constructed
+        while that stream was current: DDP keeps the parameters'
+        AccumulateGrad nodes alive, and a node created on another stream
+        makes the backward synchronise with that stream, which breaks the
+        capture."""
         if not hasattr(optimiser, 'prepare'):
             raise TypeError('CapturedTrainStep needs umamd.optim.Adam (graph-replayable)')
+        self.group, self.world = None, 1
+        if isinstance(model, DistributedDataParallel):
+            self.group = model.process_group
+            model = model.module  # DDP's reducer stays idle; see _reduce_grads
+        elif dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            self.group = dist.group.WORLD
+        if self.group is not None:
+            self.world = dist.get_world_size(self.group)
+        self._flat, self._layout, self._raw = None, None, None
         snap = self._snapshot(model, optimiser) if restore_state else None
         self.model, self.loss_function, self.optimiser = model, loss_function, optimiser
         self.scale, self.scales = float(scale), scales
@@ -51,8 +80,9 @@ class CapturedTrainStep:
         self.left = left.detach().clone().contiguous()
         self.right = right.detach().clone().contiguous()
         cur = torch.cuda.current_stream()
-        side = torch.cuda.Stream()
-        side.wait_stream(cur)
+        side = stream if stream is not None else torch.cuda.Stream()
+        if side != cur:
+            side.wait_stream(cur)
         with torch.cuda.stream(side):
             for _ in range(warmup):  # eager steps: allocator warm-up, optimiser state
                 optimiser.zero_grad(set_to_none=True)
@@ -60,19 +90,34 @@ class CapturedTrainStep:
                 optimiser.step()
         cur.wait_stream(side)
         torch.cuda.synchronize()
+        self._drain_watchdog()
         optimiser.zero_grad(set_to_none=True)
         # capture on the warm-up stream so autograd's cached AccumulateGrad
         # nodes see the stream they were created on
+        # the backward (autograd's device thread) launches into the capture
+        # too; the process group's watchdog is drained first (_drain_watchdog)
+        mode = os.environ.get('UMAMD_CAPTURE_MODE', 'global')
         self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb, stream=side):
+        with torch.cuda.graph(self.g_fb, stream=side, capture_error_mode=mode):
             self.disp_loss, self.error_loss = self._fwd_bwd()
         optimiser.prepare()  # tables for the graph-pool gradients, outside capture
         torch.cuda.synchronize()
         self.g_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool(), stream=side):
+        with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool(), stream=side,
+                              capture_error_mode=mode):
             optimiser.step()
         if snap is not None:
             self._restore(model, optimiser, snap)
+
+    def _drain_watchdog(self):
+        """Let the process group's watchdog retire the warm-up collectives
+        before capturing: it polls the end events of outstanding work, and
+        HIP refuses (and invalidates the capture on) a query of an event
+        whose stream is capturing -- the RCCL stream joins the capture at
+        the first recorded collective.  Measured on MI355X: 0.5 s suffices;
+        without it the capture fails at random."""
+        if self.group is not None:
+            time.sleep(float(os.environ.get('UMAMD_CAPTURE_DRAIN_S', '1.0')))
 
     @staticmethod
     @torch.no_grad()
@@ -117,7 +162,38 @@ class CapturedTrainStep:
         else:
             with self.overlap:
                 (disp_loss + error_loss).backward()
+        if self.group is not None:
+            self._reduce_grads()
         return disp_loss, error_loss
+
+    def _reduce_grads(self):
+        """Average the gradients over the group: pack -> one all-reduce ->
+        ``.grad`` = views of the reduced buffer (DDP's result, one
+        collective instead of its buckets)."""
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        have = tuple(p.grad is not None for p in params)
+        if self._layout is None:
+            total = sum(p.numel() for p, h in zip(params, have) if h)
+            self._flat = torch.empty(total, dtype=torch.float32, device=params[0].device)
+            self._layout = have
+        elif have != self._layout:
+            raise RuntimeError('CapturedTrainStep: the set of parameters with gradients changed')
+        used = [p for p, h in zip(params, have) if h]
+        grads = [p.grad for p in used]
+        if any(g.dtype != torch.float32 for g in grads):
+            raise TypeError('CapturedTrainStep: float32 gradients expected')
+        torch.cat([g.reshape(-1) for g in grads], out=self._flat)
+        self._raw = grads  # the backward's own gradient tensors stay allocated
+        if dist.get_backend(self.group) == 'nccl':
+            dist.all_reduce(self._flat, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(self._flat, group=self.group)
+            self._flat.mul_(1.0 / self.world)
+        off = 0
+        for p in used:
+            n = p.numel()
+            p.grad = self._flat[off:off + n].view_as(p)
+            off += n
 
     def __call__(self, left=None, right=None):
         if left is not None:

@@ -21,6 +21,7 @@ Granularity (one autograd node each):
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -166,7 +167,11 @@ def _colsum(y, C):
 
 
 class BNSync:
-    """How a BN layer exchanges statistics (SyncBatchNorm semantics)."""
+    """How a BN layer exchanges statistics (SyncBatchNorm semantics).
+    UMAMD_DIST=1 keeps the all-reduce with a single rank (rehearsal of the
+    data-parallel path on one GPU)."""
+
+    force = os.environ.get('UMAMD_DIST') == '1'
 
     def __init__(self, bn: torch.nn.Module):
         self.bn = bn
@@ -178,7 +183,7 @@ class BNSync:
             self.world = dist.get_world_size(self.group)
 
     def all_reduce(self, t: torch.Tensor):
-        if self.world > 1:
+        if self.group is not None and (self.world > 1 or self.force):
             dist.all_reduce(t, group=self.group)
 
 

@@ -18,8 +18,9 @@ the caching allocator does not hand their memory to the launch stream while
 the side stream still reads it (during capture it defers those frees to the
 end of capture).
 
-Single-process only (``train.graph.CapturedTrainStep``): DDP's reducer reads
-gradients from its hooks during backward and is left on the launch stream.
+Used by ``train.graph.CapturedTrainStep``, whose data-parallel gradient
+all-reduce runs after the join (DDP's per-bucket hooks would read gradients
+before the side stream wrote them, so the eager DDP step does not use it).
 """
 from __future__ import annotations
 
