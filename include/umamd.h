@@ -155,10 +155,15 @@ int um_bn_stats_coeffs(const float* parts, int nparts, int C, double* ws, double
                        float* mean, float* invstd, float* scale, float* shift,
                        hipStream_t stream);
 /* single-process BN backward: reduce the bwd partials and compute k1..k3,
- * dgamma, dbeta in one launch (um_bn_stats_reduce + um_bn_bwd_coeffs) */
+ * dgamma, dbeta in one launch (um_bn_stats_reduce + um_bn_bwd_coeffs).
+ * dbias (optional): the gradient of the bias of the conv feeding this BN,
+ * sum_m dy = k1 (sum dz - n k2 - k3 sum xhat) with sum xhat = 0 by
+ * construction of the batch mean -- evaluated in closed form from the
+ * reduced sums instead of a reduction of dy over the pixels */
 int um_bn_bwd_stats_coeffs(const float* parts, int nparts, int C, double* ws, double count,
                            const float* gamma, const float* invstd, float* dgamma,
-                           float* dbeta, float* k1, float* k2, float* k3, hipStream_t stream);
+                           float* dbeta, float* dbias, float* k1, float* k2, float* k3,
+                           hipStream_t stream);
 /* count <= 0: read the element count from stats[2C] (SyncBN: the per-rank
  * counts are all-reduced with the statistics) -- also for um_bn_bwd_coeffs */
 int um_bn_coeffs(const double* stats, double count, int C, const float* gamma,
@@ -172,12 +177,16 @@ int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int 
                          const void* y, int ldy, const float* mean, const float* invstd,
                          const float* scale, const float* shift, const float* add_nc,
                          int apply_elu, float* parts, hipStream_t stream);
+/* dbias as in um_bn_bwd_stats_coeffs from the all-reduced sums, times
+ * dbias_scale (SyncBN: 1/world, so that the data-parallel gradient average
+ * over ranks gives the global sum's average, as the reference's DDP does) */
 int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamma,
                      const float* invstd, const double* stats_local, float* dgamma,
-                     float* dbeta, int accumulate, float* k1, float* k2, float* k3,
-                     hipStream_t stream);
+                     float* dbeta, float* dbias, float dbias_scale, int accumulate, float* k1,
+                     float* k2, float* k3, hipStream_t stream);
 /* sum_parts (optional): per-block partial sums of dy, [um_bn_bwd_parts(M)][C]
- * (the conv-bias gradient, reduced by um_reduce_rows) */
+ * (the conv-bias gradient, reduced by um_reduce_rows; only needed when no
+ * coefficient kernel supplies it) */
 int um_bn_elu_bwd_apply(int dtype, long M, int C, long HW, const void* da, int ldda,
                         const void* y, int ldy, const float* mean, const float* invstd,
                         const float* scale, const float* shift, const float* add_nc,

@@ -5,7 +5,7 @@
 //             -> um_bn_coeffs (mean/invstd/scale/shift + running-stat update)
 //             -> um_bn_elu_fwd (a = ELU(y*scale + shift)), or fused consumers
 //   backward: um_bn_elu_bwd_reduce (sum dz, sum dz*xhat) -> um_bn_stats_reduce
-//             -> [all-reduce] -> um_bn_bwd_coeffs (dgamma/dbeta + dx coeffs)
+//             -> [all-reduce] -> um_bn_bwd_coeffs (dgamma/dbeta/conv dbias + dx coeffs)
 //             -> um_bn_elu_bwd_apply (dy)
 // The pre-BN conv output y is always f32 (also in bf16 mode): BN subtracts a
 // batch mean that can be much larger than the batch std, so a bf16 y would
@@ -129,17 +129,22 @@ __global__ void bwd_coeffs_kernel(const double* __restrict__ st, double count, i
                                   const float* __restrict__ gamma,
                                   const float* __restrict__ invstd,
                                   const double* __restrict__ st_local, float* dgamma,
-                                  float* dbeta, int accumulate, float* __restrict__ k1,
-                                  float* __restrict__ k2, float* __restrict__ k3) {
+                                  float* dbeta, float* dbias, float dbias_scale, int accumulate,
+                                  float* __restrict__ k1, float* __restrict__ k2,
+                                  float* __restrict__ k3) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   if (count <= 0) count = st[2 * C];  // all-reduced element count (see coeffs_kernel)
   const double sdz = st[2 * c], sdzx = st[2 * c + 1];
   const float g = gamma ? gamma[c] : 1.f;
   // dx = g*invstd*(dz - sdz/n - xhat*sdzx/n)
-  k1[c] = g * invstd[c];
-  k2[c] = (float)(sdz / count);
+  const float a1 = g * invstd[c], a2 = (float)(sdz / count);
+  k1[c] = a1;
+  k2[c] = a2;
   k3[c] = (float)(sdzx / count);
+  // conv-bias gradient: sum_m dy = k1 (sdz - n k2 - k3 sum xhat), sum xhat = 0
+  // (global sums; dbias_scale spreads it over the ranks' gradient average)
+  if (dbias) dbias[c] = dbias_scale * a1 * (float)(sdz - count * (double)a2);
   // parameter grads use the local (per-rank) sums, like torch SyncBatchNorm
   const double* sl = st_local ? st_local : st;
   if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)sl[2 * c + 1];
@@ -275,9 +280,11 @@ int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int 
 
 int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamma,
                      const float* invstd, const double* stats_local, float* dgamma, float* dbeta,
-                     int accumulate, float* k1, float* k2, float* k3, hipStream_t st) {
+                     float* dbias, float dbias_scale, int accumulate, float* k1, float* k2,
+                     float* k3, hipStream_t st) {
   hipLaunchKernelGGL(bwd_coeffs_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, stats, count, C,
-                     gamma, invstd, stats_local, dgamma, dbeta, accumulate, k1, k2, k3);
+                     gamma, invstd, stats_local, dgamma, dbeta, dbias, dbias_scale, accumulate, k1,
+                     k2, k3);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -19,6 +19,7 @@
 // f32 : 8 x v_mfma_f32_16x16x4_f32 per BK step with the k-permutation
 //       "lane group g, element e -> k = 8g+e" on both operands (exact f32).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "igemm.h"
@@ -662,7 +663,12 @@ static int generic_wgrad_splits(int M, int K, int RRC, bool tr) {
   // tiles of the bf16 kernels (the f32 kernel uses 64x64 tiles; same split count)
   const int bm = tr ? umamd::wgrad_tr_bm(K) : wgrad_bm(K);
   const long tiles = (long)ceil_div(K, bm) * ceil_div(RRC, 128);
-  long splits = (768 + tiles - 1) / tiles;
+  // target workgroups over the chip (UMAMD_WSPLIT_BLOCKS overrides for sweeps)
+  static const long target = [] {
+    const char* e = getenv("UMAMD_WSPLIT_BLOCKS");
+    return e ? atol(e) : 768l;
+  }();
+  long splits = (target + tiles - 1) / tiles;
   const long max_by_m = (M + 255) / 256;  // >= 256 pixels per split
   if (splits > max_by_m) splits = max_by_m;
   const long max_by_bytes = (32l << 20) / ((long)K * RRC * 4);  // <= 32 MB of slabs

@@ -24,7 +24,7 @@ struct ColRed {
   long long* nbt;
   float *mean, *invstd, *scale, *shift;
   const float* invstd_in;
-  float *dgamma, *dbeta, *k1, *k2, *k3;
+  float *dgamma, *dbeta, *dbias, *k1, *k2, *k3;
   // COLRED_ROWS
   float* out;
   int accumulate;

@@ -51,11 +51,14 @@ __device__ __forceinline__ void finish(const umamd::ColRed& a, int c, double s0,
     case umamd::COLRED_BN_BWD: {
       // dx = g*invstd*(dz - sdz/n - xhat*sdzx/n); dgamma = sum dz*xhat, dbeta = sum dz
       const float g = a.gamma ? a.gamma[c] : 1.f;
-      a.k1[c] = g * a.invstd_in[c];
-      a.k2[c] = (float)(s0 / a.count);
+      const float k1 = g * a.invstd_in[c], k2 = (float)(s0 / a.count);
+      a.k1[c] = k1;
+      a.k2[c] = k2;
       a.k3[c] = (float)(s1 / a.count);
       if (a.dgamma) a.dgamma[c] = (float)s1;
       if (a.dbeta) a.dbeta[c] = (float)s0;
+      // conv-bias gradient sum_m dy = k1 (s0 - n k2 - k3 sum xhat), sum xhat = 0
+      if (a.dbias) a.dbias[c] = k1 * (float)(s0 - a.count * (double)k2);
       break;
     }
     default:  // COLRED_ROWS
@@ -279,13 +282,13 @@ int um_bn_stats_coeffs(const float* parts, int nparts, int C, double* ws, double
 
 int um_bn_bwd_stats_coeffs(const float* parts, int nparts, int C, double* ws, double count,
                            const float* gamma, const float* invstd, float* dgamma, float* dbeta,
-                           float* k1, float* k2, float* k3, hipStream_t st) {
+                           float* dbias, float* k1, float* k2, float* k3, hipStream_t st) {
   UM_CHECK_ARG(ws != nullptr && count > 0, "um_bn_bwd_stats_coeffs: ws / count");
   umamd::ColRed a{};
   a.parts = parts; a.nparts = nparts; a.C = C; a.rowstride = (long)C * 2; a.ws = ws;
   a.mode = umamd::COLRED_BN_BWD;
   a.count = count; a.gamma = gamma; a.invstd_in = invstd; a.dgamma = dgamma; a.dbeta = dbeta;
-  a.k1 = k1; a.k2 = k2; a.k3 = k3;
+  a.dbias = dbias; a.k1 = k1; a.k2 = k2; a.k3 = k3;
   return umamd::colred_run(a, 2, st);
 }
 

@@ -16,6 +16,7 @@
 // sums them.  Used for the bf16 convs the halo kernel does not cover (deep
 // layers with many channels or small maps).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "wgrad_tr.h"
@@ -24,7 +25,6 @@ namespace {
 
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
 
-constexpr int TBK = 32;  // pixels per k-step
 constexpr int TBN = 128;  // (r,s,c) columns per block
 
 struct TrArgs {
@@ -78,13 +78,18 @@ __device__ __forceinline__ void pix_adv(Pix& x, int step, int P, int Q, long m, 
   x.ok = m < mend;
 }
 
-template <int BM>
+// TBK pixels per k-step (a multiple of the MFMA's 32): the loads of step
+// s+1 are in flight during the MFMAs of step s, so a larger step hides more
+// of the global-load latency per barrier (these GEMMs are latency-bound at
+// one or two blocks per CU).
+template <int BM, int TBK>
 __global__ void __launch_bounds__(256) wgrad_tr_kernel(TrArgs a) {
   constexpr int NCA = BM / 16, NCB = TBN / 16;  // 16-channel chunks per image row
   constexpr int TM = BM / 32, TN = 4;           // 2x2 waves, 16x16 tiles
   constexpr int A_PER = TBK * BM / 8 / 256;     // 8-channel chunks per thread per step
   constexpr int B_PER = TBK * TBN / 8 / 256;
-  static_assert(A_PER >= 1 && B_PER == 2, "tiles");
+  constexpr int KS = TBK / 32;                  // MFMA k-substeps per step
+  static_assert(A_PER >= 1 && B_PER >= 2 && TBK % 32 == 0, "tiles");
   __shared__ __attribute__((aligned(16))) bf16_t sA[2][TBK * BM];
   __shared__ __attribute__((aligned(16))) bf16_t sB[2][TBK * TBN];
 
@@ -198,22 +203,29 @@ __global__ void __launch_bounds__(256) wgrad_tr_kernel(TrArgs a) {
   for (long m0 = m_begin; m0 < m_end; m0 += TBK) {
     const bool more = m0 + TBK < m_end;
     if (more) load();
-    bf16x8_t fa[TM], fb[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const bf16x4_t lo = tr_read(&sA[cur][oa[i][0]]), hi = tr_read(&sA[cur][oa[i][1]]);
-      fa[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int ks = 0; ks < KS; ++ks) {
+      // 32 more pixel rows: row bits 0..3 (the swizzle's) are unchanged
+      const int da = ks * 32 * NCA * 16, db = ks * 32 * NCB * 16;
+      bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bf16x4_t lo = tr_read(&sA[cur][oa[i][0] + da]);
+        const bf16x4_t hi = tr_read(&sA[cur][oa[i][1] + da]);
+        fa[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const bf16x4_t lo = tr_read(&sB[cur][ob[j][0] + db]);
+        const bf16x4_t hi = tr_read(&sB[cur][ob[j][1] + db]);
+        fb[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const bf16x4_t lo = tr_read(&sB[cur][ob[j][0]]), hi = tr_read(&sB[cur][ob[j][1]]);
-      fb[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     if (more) {
       store(cur ^ 1);
       advance(m0 + 2 * TBK);
@@ -242,6 +254,16 @@ namespace umamd {
 
 int wgrad_tr_bm(int K) { return K <= 64 ? 64 : 128; }
 
+// pixels per k-step (UMAMD_WTR_TBK overrides: 32, 64 or 128)
+int wgrad_tr_tbk() {
+  static const int v = [] {
+    const char* e = getenv("UMAMD_WTR_TBK");
+    const int t = e ? atoi(e) : 32;
+    return (t == 64 || t == 128) ? t : 32;
+  }();
+  return v;
+}
+
 int wgrad_tr_run(const void* x, int N, int H, int W, int C, int ldx, int K, int R, int stride,
                  int pad, int reflect, int P, int Q, const void* dy, int ldy, float* slabs,
                  int splits, hipStream_t st) {
@@ -253,15 +275,21 @@ int wgrad_tr_run(const void* x, int N, int H, int W, int C, int ldx, int K, int 
   a.pad = pad; a.reflect = reflect; a.P = P; a.Q = Q; a.ldy = ldy;
   a.M = N * P * Q;
   a.RRC = R * R * C;
-  a.m_per_split = ceil_div(ceil_div(a.M, splits), TBK) * TBK;
+  const int tbk = wgrad_tr_tbk();
+  a.m_per_split = ceil_div(ceil_div(a.M, splits), tbk) * tbk;
   const int bm = wgrad_tr_bm(K);
   dim3 grid(ceil_div(K, bm), ceil_div(a.RRC, TBN), splits);
-  if (bm == 64)
-    hipLaunchKernelGGL(wgrad_tr_kernel<64>, grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL(wgrad_tr_kernel<128>, grid, dim3(256), 0, st, a);
-  UM_LAUNCH_CHECK();
-  return UM_OK;
+#define UM_WTR(BM_, TBK_)                                                                 \
+  if (bm == BM_ && tbk == TBK_) {                                                         \
+    hipLaunchKernelGGL((wgrad_tr_kernel<BM_, TBK_>), grid, dim3(256), 0, st, a);          \
+    UM_LAUNCH_CHECK();                                                                    \
+    return UM_OK;                                                                         \
+  }
+  UM_WTR(64, 32) UM_WTR(64, 64) UM_WTR(64, 128)
+  UM_WTR(128, 32) UM_WTR(128, 64) UM_WTR(128, 128)
+#undef UM_WTR
+  umamd::set_error("wgrad_tr: no kernel for bm %d tbk %d", bm, tbk);
+  return UM_ERR_ARG;
 }
 
 }  // namespace umamd

@@ -60,13 +60,13 @@ _SIG = {
     'um_bn_stats_reduce': (_I, [_P, _I, _I, _P, _P, 's']),
     'um_bn_stats_coeffs': (_I, [_P, _I, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P,
                                 's']),
-    'um_bn_bwd_stats_coeffs': (_I, [_P, _I, _I, _P, _D, _P, _P, _P, _P, _P, _P, _P, 's']),
+    'um_bn_bwd_stats_coeffs': (_I, [_P, _I, _I, _P, _D, _P, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_coeffs': (_I, [_P, _D, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, 's']),
     'um_bn_bwd_parts': (_I, [_L]),
     'um_bn_elu_bwd_reduce': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P,
                                   's']),
-    'um_bn_bwd_coeffs': (_I, [_P, _D, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, 's']),
+    'um_bn_bwd_coeffs': (_I, [_P, _D, _I, _P, _P, _P, _P, _P, _P, _F, _I, _P, _P, _P, 's']),
     'um_bn_elu_bwd_apply': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P,
                                  _P, _P, _P, _I, _P, 's']),
     'um_merge_fwd': (_I, [_I, _I, _P, _P, _P, _P, _L, _P, 's']),

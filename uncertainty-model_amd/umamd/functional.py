@@ -319,11 +319,16 @@ class ConvBNELUFn(torch.autograd.Function):
             w1c, w2c = w1.detach().float().contiguous(), w2.detach().float().contiguous()
             call('um_se_mlp_bwd', N, K, R1, ptr(dsc), ptr(s), ptr(z1), ptr(pooled), ptr(w1c),
                  ptr(w2c), ptr(dw1), ptr(dw2), ptr(add_nc), ptr(dz), 1.0 / (P * Q))
-        dgamma = dbeta = None
+        dgamma = dbeta = dbias = None
+        need_b = ctx.needs_input_grad[2]
         k1 = torch.empty(K, dtype=torch.float32, device=dev)
         k2 = torch.empty_like(k1)
         k3 = torch.empty_like(k1)
         if ctx.has_bn:
+            # the conv bias feeds a training-mode BN: its gradient comes out of
+            # the coefficient kernel in closed form (no reduction of dy)
+            if need_b:
+                dbias = torch.empty(K, dtype=torch.float32, device=dev)
             nb = query('um_bn_bwd_parts', M)
             parts = torch.empty((nb, K, 2), dtype=torch.float32, device=dev)
             call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
@@ -335,7 +340,7 @@ class ConvBNELUFn(torch.autograd.Function):
             ws = _colred_ws(nb, K, 2, dev)
             if world == 1:
                 call('um_bn_bwd_stats_coeffs', ptr(parts), nb, K, ptr(ws), float(M), ptr(gamma),
-                     ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(k1), ptr(k2), ptr(k3))
+                     ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(k1), ptr(k2), ptr(k3))
             else:
                 st = torch.empty((K + 1, 2), dtype=torch.float64, device=dev)
                 st[K].fill_(float(M))  # this rank's count, summed by the all-reduce
@@ -343,7 +348,8 @@ class ConvBNELUFn(torch.autograd.Function):
                 st_local = st.clone()
                 ctx.sync.all_reduce(st)
                 call('um_bn_bwd_coeffs', ptr(st), -1.0, K, ptr(gamma), ptr(invstd),
-                     ptr(st_local), ptr(dgamma), ptr(dbeta), 0, ptr(k1), ptr(k2), ptr(k3))
+                     ptr(st_local), ptr(dgamma), ptr(dbeta), ptr(dbias), 1.0 / world, 0,
+                     ptr(k1), ptr(k2), ptr(k3))
         else:
             # no batch statistics (no BN, or BN in eval mode): dy = dz * scale
             k1.copy_(scale)
@@ -352,16 +358,15 @@ class ConvBNELUFn(torch.autograd.Function):
             if gamma is not None and spec.bn is not None:
                 raise NotImplementedError('backward through an eval-mode BatchNorm')
         dy = torch.empty(y.shape, dtype=adt, device=dev)
-        need_b = ctx.needs_input_grad[2]
         nbp = query('um_bn_bwd_parts', M)
-        bparts = torch.empty((nbp, K), dtype=torch.float32, device=dev) if need_b else None
+        reduce_b = need_b and dbias is None
+        bparts = torch.empty((nbp, K), dtype=torch.float32, device=dev) if reduce_b else None
         call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
              ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1), ptr(k2),
              ptr(k3), ptr(dy), K, ptr(bparts))
         dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode,
                          segs=spec.segs)
-        dbias = None
-        if need_b:
+        if reduce_b:
             dbias = torch.empty(K, dtype=torch.float32, device=dev)
             _reduce_rows(bparts, nbp, K, dbias)
         dx = None
