@@ -47,26 +47,43 @@ __global__ void coeffs_kernel(const double* __restrict__ st, double count, int C
   }
 }
 
+// RowMap layout (as the backward kernels): a thread owns 8 channels, keeps
+// their scale/shift in registers and walks rows of its block's row chunk.
 template <typename T>
-__global__ void bn_elu_fwd_kernel(const float* __restrict__ y, int ldy, long M, int C,
-                                  const float* __restrict__ scale, const float* __restrict__ shift,
-                                  T* __restrict__ a, int lda, int apply_elu) {
-  // 8 channels per thread (C % 8 == 0)
+__global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
+    const float* __restrict__ y, int ldy, long M, int C, const float* __restrict__ scale,
+    const float* __restrict__ shift, T* __restrict__ a, int lda, int apply_elu,
+    int rows_per_block) {
   const int cg = C / 8;
-  const long total = M * cg;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const long m = i / cg;
-    const int c = (int)(i - m * cg) * 8;
-    float v[8];
-    load8(y + m * ldy + c, v);
+  const RowMap rm(cg);
+  const long m0 = (long)blockIdx.x * rows_per_block;
+  const long m1 = min(M, m0 + rows_per_block);
+  for (int g0 = 0; g0 < cg; g0 += rm.G) {
+    const int g = g0 + rm.g;
+    if (!rm.active() || g >= cg) continue;
+    const int c = g * 8;
+    float sc[8], sh[8];
+    load8(scale + c, sc);
+    load8(shift + c, sh);
+#pragma unroll 4
+    for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+      float v[8];
+      load8(y + m * ldy + c, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float z = v[e] * scale[c + e] + shift[c + e];
-      v[e] = apply_elu ? eluf_(z) : z;
+      for (int e = 0; e < 8; ++e) {
+        const float z = v[e] * sc[e] + sh[e];
+        v[e] = apply_elu ? eluf_(z) : z;
+      }
+      store8(a + m * lda + c, v);
     }
-    store8(a + m * lda + c, v);
   }
+}
+
+// rows per forward block: ~2048 blocks over the chip, >= 16 rows each
+inline int fwd_rows(long M) {
+  long r = (M + 2047) / 2048;
+  if (r < 16) r = 16;
+  return (int)r;
 }
 
 // Backward reduce: dz = (da + add[n][c]) * ELU'(z), z = y*scale + shift,
@@ -220,13 +237,6 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
   }
 }
 
-inline int grid_for(long n) {
-  long b = (n + 255) / 256;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  return (int)b;
-}
-
 }  // namespace
 
 extern "C" {
@@ -245,13 +255,14 @@ int um_bn_coeffs(const double* stats, double count, int C, const float* gamma, c
 int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
                   const float* shift, void* a, int lda, int apply_elu, hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0 && ldy % 8 == 0 && lda % 8 == 0, "um_bn_elu_fwd: C/ld not multiple of 8");
-  const int g = grid_for(M * C / 8);
+  const int rows = fwd_rows(M);
+  const int g = ceil_div(M, rows);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const float*)y,
-                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu);
+                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu, rows);
   else
     hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)y, ldy,
-                       M, C, scale, shift, (float*)a, lda, apply_elu);
+                       M, C, scale, shift, (float*)a, lda, apply_elu, rows);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

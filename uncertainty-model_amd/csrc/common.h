@@ -144,9 +144,28 @@ struct RowMap {
   __device__ bool active() const { return lane < lanes; }
 };
 
-// reduce red[lanes][G][NV] over lanes into thread (lane==0) registers
+// reduce red[lanes][G][NV] over lanes into thread (lane==0) registers.
+// G | 64 (C = 32..256 channels): the lanes of one channel group inside a
+// wave are combined with a butterfly of cross-lane shuffles (offsets G..32)
+// and only the four wave sums meet in LDS -- no serial 64-lane LDS walk.
 template <int NV>
 __device__ __forceinline__ void lane_reduce(float* red, const RowMap& rm, float* v) {
+  if (rm.G < 64 && (64 % rm.G) == 0) {
+    for (int o = rm.G; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < NV; ++e) v[e] += __shfl_xor(v[e], o, 64);
+    const int wave = threadIdx.x >> 6, wl = threadIdx.x & 63;
+    if (wl < rm.G)
+#pragma unroll
+      for (int e = 0; e < NV; ++e) red[(wave * rm.G + wl) * NV + e] = v[e];
+    __syncthreads();
+    if (rm.lane == 0)  // wave 0, wl == g
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+#pragma unroll
+        for (int e = 0; e < NV; ++e) v[e] += red[(w * rm.G + rm.g) * NV + e];
+    __syncthreads();
+    return;
+  }
   if (rm.active())
 #pragma unroll
     for (int e = 0; e < NV; ++e) red[(rm.lane * rm.G + rm.g) * NV + e] = v[e];

@@ -166,6 +166,20 @@ def _colsum(y, C):
     return _reduce_rows(parts, parts_n, C, out)
 
 
+_CONSTS = {}
+
+
+def _const_vec(value: float, n: int, device) -> torch.Tensor:
+    """A read-only f32 vector of ``value`` (first n entries of a cached
+    buffer): identity BN coefficients without a fill launch per conv."""
+    key = (str(device), float(value))
+    buf = _CONSTS.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.full((max(n, 512),), float(value), dtype=torch.float32, device=device)
+        _CONSTS[key] = buf
+    return buf[:n]
+
+
 class BNSync:
     """How a BN layer exchanges statistics (SyncBatchNorm semantics).
     UMAMD_DIST=1 keeps the all-reduce with a single rank (rehearsal of the
@@ -268,10 +282,8 @@ class ConvBNELUFn(torch.autograd.Function):
             training = False
             y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
                           out_dtype=torch.float32, creal=Creal)
-            mean = torch.zeros(K, dtype=torch.float32, device=dev)
-            shift = mean
-            invstd = torch.ones(K, dtype=torch.float32, device=dev)
-            scale = invstd
+            mean = shift = _const_vec(0.0, K, dev)
+            invstd = scale = _const_vec(1.0, K, dev)
         a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y is f32 (pre-BN)
         call('um_bn_elu_fwd', _dt(a), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
              int(spec.elu))
@@ -321,10 +333,10 @@ class ConvBNELUFn(torch.autograd.Function):
                  ptr(w2c), ptr(dw1), ptr(dw2), ptr(add_nc), ptr(dz), 1.0 / (P * Q))
         dgamma = dbeta = dbias = None
         need_b = ctx.needs_input_grad[2]
-        k1 = torch.empty(K, dtype=torch.float32, device=dev)
-        k2 = torch.empty_like(k1)
-        k3 = torch.empty_like(k1)
         if ctx.has_bn:
+            k1 = torch.empty(K, dtype=torch.float32, device=dev)
+            k2 = torch.empty_like(k1)
+            k3 = torch.empty_like(k1)
             # the conv bias feeds a training-mode BN: its gradient comes out of
             # the coefficient kernel in closed form (no reduction of dy)
             if need_b:
@@ -352,9 +364,8 @@ class ConvBNELUFn(torch.autograd.Function):
                      ptr(k1), ptr(k2), ptr(k3))
         else:
             # no batch statistics (no BN, or BN in eval mode): dy = dz * scale
-            k1.copy_(scale)
-            k2.zero_()
-            k3.zero_()
+            k1 = scale
+            k2 = k3 = _const_vec(0.0, K, dev)
             if gamma is not None and spec.bn is not None:
                 raise NotImplementedError('backward through an eval-mode BatchNorm')
         dy = torch.empty(y.shape, dtype=adt, device=dev)
