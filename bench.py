@@ -52,8 +52,10 @@ def parse():
                     help='eager launches instead of the captured HIP graph')
     ap.add_argument('--eager-steps', type=int, default=3,
                     help='N=1: also time this many eagerly launched steps (reported beside)')
-    ap.add_argument('--cpu-sample-batch', type=int, default=2)
-    ap.add_argument('--cpu-sample-steps', type=int, default=2)
+    ap.add_argument('--cpu-steps', type=int, default=5,
+                    help='CPU baseline: best of this many timed steps per shape (BASELINE.md)')
+    ap.add_argument('--fp32-steps', type=int, default=5,
+                    help='N=1: also time the fp32 (parity-mode) captured step, reported beside')
     return ap.parse_args()
 
 
@@ -150,6 +152,33 @@ def conv_min_bytes(name, a):
     return None
 
 
+def conv1x1_report(groups, peak):
+    """Every 1x1 conv launch (forward and data gradient) against its own
+    attainable rate min(P, AI * BW), AI = algorithmic FLOPs / compulsory
+    HBM bytes (the 1x1 convs are HBM-bound at these shapes)."""
+    rows = []
+    for name in ('um_conv2d_fwd', 'um_conv2d_dgrad'):
+        for a, ms, work in groups.get(name, []):
+            if a[10] != 1:
+                continue
+            b = conv_min_bytes(name, a)
+            ai = work / b
+            att = min(peak, ai * HBM_PEAK_GBS / 1e3)  # TFLOP/s
+            ach = work / (ms * 1e-3) / 1e12
+            rows.append({'entry': name, 'N': a[1], 'H': a[2], 'W': a[3], 'C': a[4], 'K': a[9],
+                         'ms': round(ms, 4), 'tflops': round(ach, 2), 'ai_flop_per_byte': round(ai, 1),
+                         'attainable_tflops': round(att, 1), 'frac': round(ach / att, 4)})
+    if not rows:
+        return None
+    tot_ms = sum(r['ms'] for r in rows)
+    # time-weighted fraction of attainable = sum(work / attainable) / sum(time)
+    ideal_ms = sum(r['ms'] * r['frac'] for r in rows)
+    rows.sort(key=lambda r: -r['ms'])
+    return {'launches_per_step': len(rows), 'total_ms_per_step': round(tot_ms, 4),
+            'frac_of_attainable': round(ideal_ms / tot_ms, 4), 'peak_tflops': peak,
+            'hbm_gbs': HBM_PEAK_GBS, 'layers': rows}
+
+
 def measure_roofline(m, lf, opt, left, right, scale, dtype):
     """Time every launch of the candidate kernels with HIP events on the
     launch stream (one eager step); the entry with the largest total time is
@@ -204,6 +233,7 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     out['candidates'] = {k: {kk: v[kk] for kk in ('achieved', 'unit', 'frac', 'avg_launch_ms',
                                                   'launches_per_step', 'total_ms_per_step')}
                          for k, v in table.items()}
+    out['conv1x1'] = conv1x1_report(groups, peak)
     if all(k in groups for k in LOSS_KERNELS):
         # the fused loss stack (forward + backward launches) priced as SURVEY
         # 8d does: 56 B/px all-f32 (6 image + 4 prediction reads, 4 gradient
@@ -220,16 +250,12 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
 
 
 # --------------------------------------------------------- CPU baseline ----
-def cpu_baseline(cfg, H, W, batch, steps):
-    """Oracle (plain-PyTorch CPU restatement, pinned to reference goldens)
-    train step on the host cores; bounded sample."""
+def _cpu_step_rate(cfg, H, W, batch, steps, seed=1234):
+    """best-of-``steps`` oracle train steps (1 warm-up) -> (pairs/s, s/step)"""
     from oracle import model as OM, step as OS
-    threads = os.cpu_count() or 1
-    threads = min(threads, 64)
-    torch.set_num_threads(threads)
     graphs = OM.load_stage_graphs(cfg['model']['encoder'])
     P = OS.formula_state_dict(OS.param_specs(cfg['model'], graphs))
-    g = torch.Generator().manual_seed(1234)
+    g = torch.Generator().manual_seed(seed)
     left = torch.rand(batch, 3, H, W, generator=g)
     right = torch.rand(batch, 3, H, W, generator=g)
     st = {}
@@ -239,6 +265,18 @@ def cpu_baseline(cfg, H, W, batch, steps):
         t0 = time.perf_counter()
         OS.train_step(P, left, right, 0.3, cfg['model'], cfg['loss'], graphs, st)
         best = min(best, time.perf_counter() - t0)
+    return batch / best, best
+
+
+def cpu_baseline(config, steps):
+    """The oracle's CPU train step (plain-PyTorch restatement of the
+    reference, pinned to its goldens) on the host cores, BASELINE.md
+    protocol: C2 (B=8 256x512 bayesian, the GPU workload's shape; ``value``)
+    and C1 (B=2 128x256 l1), 1 warm-up + best of ``steps`` each."""
+    threads = min(os.cpu_count() or 1, 64)
+    torch.set_num_threads(threads)
+    c2, t2 = _cpu_step_rate(load_cfg(config, 'bayesian'), 256, 512, 8, steps)
+    c1, t1 = _cpu_step_rate(load_cfg(config, 'l1'), 128, 256, 2, steps)
     cpu = ''
     try:
         with open('/proc/cpuinfo') as f:
@@ -248,10 +286,31 @@ def cpu_baseline(cfg, H, W, batch, steps):
                     break
     except OSError:
         pass
-    return {'value': round(batch / best, 3), 'unit': 'stereo-pairs/sec', 'cores': threads,
-            'kind': 'port',
-            'sample': f'oracle train step (fp32, {cfg["loss"]["error_loss_config"]["loss_type"]}) '
-                      f'B={batch} {H}x{W}, 1 warm-up + best of {steps}; {cpu}'}
+    return {'value': round(c2, 3), 'unit': 'stereo-pairs/sec', 'cores': threads, 'kind': 'port',
+            'sample': f'oracle fp32 train step, C2 B=8 256x512 bayesian, 1 warm-up + best of '
+                      f'{steps} ({t2:.2f} s/step); {cpu}',
+            'c1': {'value': round(c1, 3), 'unit': 'stereo-pairs/sec',
+                   'sample': f'C1 B=2 128x256 l1, best of {steps} ({t1:.3f} s/step)'}}
+
+
+def time_fp32(cfg, device, left, right, scale, batch, warmup, steps):
+    """The fp32 (parity-mode, INTEGRATION.md default) captured step on the
+    same inputs: reported beside the bf16 headline."""
+    from train.graph import CapturedTrainStep
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        m, lf, opt = build(cfg, 'fp32', device, 1, False)
+    torch.cuda.current_stream().wait_stream(st)
+    cap = CapturedTrainStep(m, lf, opt, left, right, scale, warmup=max(1, warmup), stream=st)
+    cap()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        cap()
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / steps
+    return {'value': round(batch / t, 2), 'ms_per_step': round(t * 1e3, 3), 'steps': steps,
+            'dtype': 'fp32'}
 
 
 def main():
@@ -312,11 +371,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
-    losses = (float(dl), float(el))
+    losses = (float(dl.detach()), float(el.detach()))
 
-    # the eager comparison and the roofline pass launch on the stream the
-    # model (and DDP) was built under
-    with torch.cuda.stream(cap_stream):
+    # the eager comparison and the roofline pass: N>1 launches on the stream
+    # DDP was built under (it keeps AccumulateGrad nodes bound to it)
+    with torch.cuda.stream(cap_stream if dp else torch.cuda.current_stream()):
         eager = None
         if use_graph and world == 1 and a.eager_steps > 0:
             eager = time_eager(m, lf, opt, left, right, scale, a.batch, a.eager_steps)
@@ -324,9 +383,12 @@ def main():
         if not a.no_roofline:
             roof = measure_roofline(m, lf, opt, left, right, scale, a.dtype)
         torch.cuda.synchronize()
+    fp32 = None
+    if world == 1 and a.dtype == 'bf16' and a.fp32_steps > 0:
+        fp32 = time_fp32(cfg, device, left, right, scale, a.batch, 2, a.fp32_steps)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, a.height, a.width, a.cpu_sample_batch, a.cpu_sample_steps)
+        cpu = cpu_baseline(a.config, a.cpu_steps)
 
     if rank == 0:
         total = a.batch * world * a.steps
@@ -347,6 +409,7 @@ def main():
                        'launch': 'hip-graph' if use_graph else 'eager',
                        'graph': 'config.yml (nodes=5, K5 stage graphs)'},
             'eager_launch': eager,
+            'fp32_line': fp32,
             'final_losses': {'disp': round(losses[0], 5), 'error': round(losses[1], 5)},
             'roofline': roof,
             'cpu_baseline': cpu,

@@ -10,5 +10,5 @@ cd $GRAFT_REPO_ROOT
 trace=$(find gpurun_out/$OUT/prof -name '*kernel_trace.csv' | head -1)
 stats=$(find gpurun_out/$OUT/prof -name '*kernel_stats.csv' | head -1)
 cp $stats gpurun_out/$OUT/kernel_stats.csv
-python3 tools/step_stats.py $trace 45 > gpurun_out/$OUT/step_kernels.txt
+python3 tools/step_stats.py $trace 200 > gpurun_out/$OUT/step_kernels.txt
 rm -f $trace
