@@ -170,8 +170,12 @@ int um_bn_coeffs(const double* stats, double count, int C, const float* gamma,
                  const float* beta, float eps, float momentum, float* running_mean,
                  float* running_var, long long* num_batches_tracked, float* mean,
                  float* invstd, float* scale, float* shift, hipStream_t stream);
+/* pool_parts (optional, SE squeeze of decoder.py:124-136 fused in): per-block
+ * channel sums of a, [um_bn_fwd_pool_parts(M, HW)][C], HW = pixels per image */
+int um_bn_fwd_pool_parts(long M, long HW);
 int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
-                  const float* shift, void* a, int lda, int apply_elu, hipStream_t stream);
+                  const float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
+                  hipStream_t stream);
 int um_bn_bwd_parts(long M);
 int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int ldda,
                          const void* y, int ldy, const float* mean, const float* invstd,
@@ -180,6 +184,17 @@ int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int 
 /* dbias as in um_bn_bwd_stats_coeffs from the all-reduced sums, times
  * dbias_scale (SyncBN: 1/world, so that the data-parallel gradient average
  * over ranks gives the global sum's average, as the reference's DDP does) */
+/* single-process BN backward in ONE launch: um_bn_elu_bwd_reduce whose last
+ * blocks (two-level ticket tree, f64) finish k1..k3, dgamma, dbeta and the
+ * closed-form conv-bias gradient (as um_bn_bwd_stats_coeffs); fin_ws:
+ * um_bn_bwd_fin_ws(M, C) bytes */
+long um_bn_bwd_fin_ws(long M, int C);
+int um_bn_elu_bwd_reduce_coeffs(int dtype, long M, int C, long HW, const void* da, int ldda,
+                                const void* y, int ldy, const float* mean, const float* invstd,
+                                const float* scale, const float* shift, const float* add_nc,
+                                int apply_elu, float* parts, double* fin_ws, const float* gamma,
+                                float* dgamma, float* dbeta, float* dbias, float* k1, float* k2,
+                                float* k3, hipStream_t stream);
 int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamma,
                      const float* invstd, const double* stats_local, float* dgamma,
                      float* dbeta, float* dbias, float dbias_scale, int accumulate, float* k1,
@@ -247,9 +262,12 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
                       int accumulate, float* dscale, float* ws, hipStream_t stream);
 int um_channel_mean(int dtype, int N, long S, int C, const void* x, int ld, float* out,
                     hipStream_t stream);
-int um_se_mlp_fwd(int N, int C, int R, const float* pooled, const float* w1, const float* w2,
-                  float* z1, float* s, hipStream_t stream);
-/* dw1/dw2 accumulate (+=); dz: f32 [N][R] scratch */
+/* pooled[n][c] = inv_hw * sum of the image's parts_per_image pool rows (written
+ * for the backward), then z1 = relu(W1 pooled), s = sigmoid(W2 z1) */
+int um_se_mlp_fwd(int N, int C, int R, const float* pool_parts, int parts_per_image,
+                  float inv_hw, float* pooled, const float* w1, const float* w2, float* z1,
+                  float* s, hipStream_t stream);
+/* dw1/dw2 written (=); dz: f32 [N][R] scratch */
 int um_se_mlp_bwd(int N, int C, int R, const float* ds, const float* s, const float* z1,
                   const float* pooled, const float* w1, const float* w2, float* dw1,
                   float* dw2, float* dpool_scaled, float* dz, float inv_S, hipStream_t stream);

@@ -49,41 +49,158 @@ __global__ void coeffs_kernel(const double* __restrict__ st, double count, int C
 
 // RowMap layout (as the backward kernels): a thread owns 8 channels, keeps
 // their scale/shift in registers and walks rows of its block's row chunk.
+// pool (optional): per-block channel sums of the stored a, [blocks][C] --
+// the SE squeeze of reference decoder.py:124-136 (a block's rows lie in one
+// image: rows_per_block divides HW), finished by um_se_mlp_fwd.
 template <typename T>
 __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
     const float* __restrict__ y, int ldy, long M, int C, const float* __restrict__ scale,
     const float* __restrict__ shift, T* __restrict__ a, int lda, int apply_elu,
-    int rows_per_block) {
+    int rows_per_block, float* __restrict__ pool) {
+  extern __shared__ float red[];  // [256][8] when pooling
   const int cg = C / 8;
   const RowMap rm(cg);
   const long m0 = (long)blockIdx.x * rows_per_block;
   const long m1 = min(M, m0 + rows_per_block);
   for (int g0 = 0; g0 < cg; g0 += rm.G) {
     const int g = g0 + rm.g;
-    if (!rm.active() || g >= cg) continue;
-    const int c = g * 8;
-    float sc[8], sh[8];
-    load8(scale + c, sc);
-    load8(shift + c, sh);
+    float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (rm.active() && g < cg) {
+      const int c = g * 8;
+      float sc[8], sh[8];
+      load8(scale + c, sc);
+      load8(shift + c, sh);
 #pragma unroll 4
-    for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
-      float v[8];
-      load8(y + m * ldy + c, v);
+      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+        float v[8];
+        load8(y + m * ldy + c, v);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float z = v[e] * sc[e] + sh[e];
-        v[e] = apply_elu ? eluf_(z) : z;
+        for (int e = 0; e < 8; ++e) {
+          const float z = v[e] * sc[e] + sh[e];
+          v[e] = apply_elu ? eluf_(z) : z;
+        }
+        store8(a + m * lda + c, v);
+        if (pool) {
+          float r[8];
+          load8_rounded(v, r, a);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ps[e] += r[e];
+        }
       }
-      store8(a + m * lda + c, v);
+    }
+    if (pool) {
+      lane_reduce<8>(red, rm, ps);
+      if (rm.lane == 0 && g < cg) store8(pool + (long)blockIdx.x * C + g * 8, ps);
     }
   }
 }
 
-// rows per forward block: ~2048 blocks over the chip, >= 16 rows each
-inline int fwd_rows(long M) {
+// rows per forward block: ~2048 blocks over the chip, >= 16 rows each; with
+// SE pooling a divisor of HW, so no block straddles two images
+inline int fwd_rows(long M, long HW) {
   long r = (M + 2047) / 2048;
   if (r < 16) r = 16;
+  if (HW > 0) {
+    if (r > HW) r = HW;
+    while (HW % r) --r;
+  }
   return (int)r;
+}
+
+// Optional in-kernel finish of the backward reduction (single-process BN):
+// the partial rows are combined by a two-level last-arriver tree -- the last
+// block of each group of FIN_GROUP rows sums them into an f64 level-2 row,
+// the last group to finish sums those and writes the coefficients -- so the
+// coefficients need no separate reduction launch.  Agent-scope release /
+// acquire around each ticket (the publish recipe of reduce.hip).
+constexpr int FIN_GROUP = 32;
+constexpr int FIN_MAX_GROUPS = 1024;
+__device__ unsigned int g_fin_t1[FIN_MAX_GROUPS];
+__device__ unsigned int g_fin_t2;
+
+struct BwdFin {
+  double* lvl2;  // [groups][C][2]; null: no finish
+  double count;
+  const float* gamma;
+  const float* invstd;
+  float *dgamma, *dbeta, *dbias, *k1, *k2, *k3;
+};
+
+// returns true in the block that must continue (the last arriver)
+__device__ __forceinline__ bool ticket_last(unsigned int* ctr, unsigned int expected, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = t == expected - 1;
+    if (*flag) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// sum rows [r0, r0+n) of a [rows][W] array (float or double) into out[W]
+// (double), 256 threads: W/lanes columns x row lanes, combined in LDS
+template <typename S>
+__device__ __forceinline__ void sum_rows(const S* __restrict__ src, int r0, int n, int W,
+                                         double* __restrict__ out, double* red) {
+  const int CU = W < 256 ? W : 256;
+  const int L = 256 / CU;
+  const int u = threadIdx.x % CU, l = threadIdx.x / CU;
+  for (int w0 = 0; w0 < W; w0 += CU) {
+    const int w = w0 + u;
+    double s = 0.0;
+    if (l < L && w < W) {
+      int r = l;
+      for (; r + 3 * L < n; r += 4 * L) {
+        const double a0 = src[(long)(r0 + r) * W + w], a1 = src[(long)(r0 + r + L) * W + w];
+        const double a2 = src[(long)(r0 + r + 2 * L) * W + w];
+        const double a3 = src[(long)(r0 + r + 3 * L) * W + w];
+        s += (a0 + a1) + (a2 + a3);
+      }
+      for (; r < n; r += L) s += src[(long)(r0 + r) * W + w];
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (l == 0 && w < W) {
+      for (int q = 1; q < L; ++q) s += red[q * CU + u];
+      out[w] = s;
+    }
+    __syncthreads();
+  }
+}
+
+__device__ void bwd_finish(const float* __restrict__ parts, int nb, int C, const BwdFin& f) {
+  __shared__ double red[256];
+  __shared__ int flag;
+  const int W = 2 * C;
+  const int g = blockIdx.x / FIN_GROUP;
+  const int g0 = g * FIN_GROUP, gn = min(FIN_GROUP, nb - g0);
+  const int ng = (nb + FIN_GROUP - 1) / FIN_GROUP;
+  if (!ticket_last(&g_fin_t1[g], gn, &flag)) return;
+  sum_rows<float>(parts, g0, gn, W, f.lvl2 + (long)g * W, red);
+  if (!ticket_last(&g_fin_t2, ng, &flag)) return;
+  double* tot = f.lvl2 + (long)ng * W;  // one spare row after the groups
+  sum_rows<double>(f.lvl2, 0, ng, W, tot, red);
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const double s0 = tot[2 * c], s1 = tot[2 * c + 1];
+    const float gm = f.gamma ? f.gamma[c] : 1.f;
+    const float a1 = gm * f.invstd[c], a2 = (float)(s0 / f.count);
+    f.k1[c] = a1;
+    f.k2[c] = a2;
+    f.k3[c] = (float)(s1 / f.count);
+    if (f.dgamma) f.dgamma[c] = (float)s1;
+    if (f.dbeta) f.dbeta[c] = (float)s0;
+    // conv-bias gradient sum_m dy = k1 (s0 - n k2 - k3 sum xhat), sum xhat = 0
+    if (f.dbias) f.dbias[c] = a1 * (float)(s0 - f.count * (double)a2);
+  }
 }
 
 // Backward reduce: dz = (da + add[n][c]) * ELU'(z), z = y*scale + shift,
@@ -94,7 +211,7 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
     long HW, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ add_nc, int apply_elu, float* __restrict__ parts,
-    int rows_per_block) {
+    int rows_per_block, BwdFin fin) {
   extern __shared__ float red[];  // [256][16]
   const int cg = C / 8;
   const RowMap rm(cg);
@@ -140,6 +257,7 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
       }
     }
   }
+  if (fin.lvl2 != nullptr) bwd_finish(parts, gridDim.x, C, fin);
 }
 
 __global__ void bwd_coeffs_kernel(const double* __restrict__ st, double count, int C,
@@ -252,41 +370,80 @@ int um_bn_coeffs(const double* stats, double count, int C, const float* gamma, c
   return UM_OK;
 }
 
+int um_bn_fwd_pool_parts(long M, long HW) {
+  return HW > 0 && M % HW == 0 ? (int)(M / fwd_rows(M, HW)) : 0;
+}
+
 int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
-                  const float* shift, void* a, int lda, int apply_elu, hipStream_t st) {
+                  const float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
+                  hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0 && ldy % 8 == 0 && lda % 8 == 0, "um_bn_elu_fwd: C/ld not multiple of 8");
-  const int rows = fwd_rows(M);
+  UM_CHECK_ARG(pool_parts == nullptr || (HW > 0 && M % HW == 0), "um_bn_elu_fwd: HW");
+  const int rows = fwd_rows(M, pool_parts ? HW : 0);
   const int g = ceil_div(M, rows);
+  const size_t shm = pool_parts ? 256 * 8 * sizeof(float) : 0;
   if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const float*)y,
-                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu, rows);
+    hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, dim3(g), dim3(256), shm, st, (const float*)y,
+                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu, rows, pool_parts);
   else
-    hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)y, ldy,
-                       M, C, scale, shift, (float*)a, lda, apply_elu, rows);
+    hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, dim3(g), dim3(256), shm, st, (const float*)y,
+                       ldy, M, C, scale, shift, (float*)a, lda, apply_elu, rows, pool_parts);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
 
 int um_bn_bwd_parts(long M) { return parts_for(M); }
 
-int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int ldda,
-                         const void* y, int ldy, const float* mean, const float* invstd,
-                         const float* scale, const float* shift, const float* add_nc,
-                         int apply_elu, float* parts, hipStream_t st) {
-  UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_reduce: C %% 8");
+static int bwd_reduce_launch(int dtype, long M, int C, long HW, const void* da, int ldda,
+                             const void* y, int ldy, const float* mean, const float* invstd,
+                             const float* scale, const float* shift, const float* add_nc,
+                             int apply_elu, float* parts, const BwdFin& fin, hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_reduce: C %% 8");
   const int blocks = um_bn_bwd_parts(M);
   const size_t shm = 256 * 16 * sizeof(float);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
                        (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M));
+                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M), fin);
   else
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), shm, st,
                        (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M));
+                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M), fin);
   UM_LAUNCH_CHECK();
   return UM_OK;
+}
+
+int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int ldda,
+                         const void* y, int ldy, const float* mean, const float* invstd,
+                         const float* scale, const float* shift, const float* add_nc,
+                         int apply_elu, float* parts, hipStream_t st) {
+  BwdFin fin{};
+  return bwd_reduce_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
+                           apply_elu, parts, fin, st);
+}
+
+long um_bn_bwd_fin_ws(long M, int C) {
+  const int ng = (um_bn_bwd_parts(M) + FIN_GROUP - 1) / FIN_GROUP;
+  return (long)(ng + 1) * 2 * C * sizeof(double);
+}
+
+int um_bn_elu_bwd_reduce_coeffs(int dtype, long M, int C, long HW, const void* da, int ldda,
+                                const void* y, int ldy, const float* mean, const float* invstd,
+                                const float* scale, const float* shift, const float* add_nc,
+                                int apply_elu, float* parts, double* fin_ws, const float* gamma,
+                                float* dgamma, float* dbeta, float* dbias, float* k1, float* k2,
+                                float* k3, hipStream_t st) {
+  const int ng = (um_bn_bwd_parts(M) + FIN_GROUP - 1) / FIN_GROUP;
+  UM_CHECK_ARG(fin_ws != nullptr && ng <= FIN_MAX_GROUPS, "um_bn_elu_bwd_reduce_coeffs: ws/groups");
+  BwdFin fin{};
+  fin.lvl2 = fin_ws;
+  fin.count = (double)M;
+  fin.gamma = gamma;
+  fin.invstd = invstd;
+  fin.dgamma = dgamma; fin.dbeta = dbeta; fin.dbias = dbias;
+  fin.k1 = k1; fin.k2 = k2; fin.k3 = k3;
+  return bwd_reduce_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
+                           apply_elu, parts, fin, st);
 }
 
 int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamma,

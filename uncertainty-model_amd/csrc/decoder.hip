@@ -462,14 +462,24 @@ __global__ void __launch_bounds__(256) channel_mean_kernel(const T* __restrict__
   }
 }
 
-__global__ void se_mlp_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ w1,
+// one block per image: pooled = (sum of the image's pool partial rows) / HW
+// (written out for the backward), then the excite MLP
+__global__ void se_mlp_fwd_kernel(const float* __restrict__ parts, int nparts, float inv_hw,
+                                  float* __restrict__ pooled, const float* __restrict__ w1,
                                   const float* __restrict__ w2, int C, int R,
                                   float* __restrict__ z1, float* __restrict__ s) {
   extern __shared__ float sh[];
   const int n = blockIdx.x;
   float* p = sh;       // [C]
   float* z = sh + C;   // [R]
-  for (int c = threadIdx.x; c < C; c += blockDim.x) p[c] = pooled[n * C + c];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float* q = parts + (long)n * nparts * C + c;
+    float t = 0.f;
+    for (int b = 0; b < nparts; ++b) t += q[(long)b * C];
+    t *= inv_hw;
+    p[c] = t;
+    pooled[n * C + c] = t;
+  }
   __syncthreads();
   for (int r = threadIdx.x; r < R; r += blockDim.x) {
     float t = 0.f;
@@ -486,7 +496,7 @@ __global__ void se_mlp_fwd_kernel(const float* __restrict__ pooled, const float*
   }
 }
 
-// single block; dw1 [R][C], dw2 [C][R] accumulated; dpool_scaled[n][c] = dpool / S
+// dw1 [R][C], dw2 [C][R] written (not accumulated); dpool_scaled[n][c] = dpool / S
 // SE excite backward, two launches:
 //  (1) dz[n][r] = relu'(z1) * sum_c w2[c][r] * ds[n][c] s(1-s): one wave per
 //      (n, r), lanes over c;
@@ -529,13 +539,13 @@ __global__ void __launch_bounds__(256) se_wgrad_kernel(int N, int C, int R, cons
       const float sv = s[n * C + c];
       t += ds[n * C + c] * sv * (1.f - sv) * z1[n * R + r];
     }
-    dw2[i] += t;
+    dw2[i] = t;
   } else if (i < 2 * CR) {  // dw1[r][c]
     const long j = i - CR;
     const int r = j / C, c = j % C;
     float t = 0.f;
     for (int n = 0; n < N; ++n) t += dz[n * R + r] * pooled[n * C + c];
-    dw1[j] += t;
+    dw1[j] = t;
   } else if (i < 2 * CR + (long)N * C) {  // dpool[n][c]
     const long j = i - 2 * CR;
     const int n = j / C, c = j % C;
@@ -710,10 +720,11 @@ int um_channel_mean(int dtype, int N, long S, int C, const void* x, int ld, floa
   return UM_OK;
 }
 
-int um_se_mlp_fwd(int N, int C, int R, const float* pooled, const float* w1, const float* w2,
-                  float* z1, float* s, hipStream_t st) {
-  hipLaunchKernelGGL(se_mlp_fwd_kernel, dim3(N), dim3(256), (C + R) * sizeof(float), st, pooled,
-                     w1, w2, C, R, z1, s);
+int um_se_mlp_fwd(int N, int C, int R, const float* pool_parts, int parts_per_image,
+                  float inv_hw, float* pooled, const float* w1, const float* w2, float* z1,
+                  float* s, hipStream_t st) {
+  hipLaunchKernelGGL(se_mlp_fwd_kernel, dim3(N), dim3(256), (C + R) * sizeof(float), st,
+                     pool_parts, parts_per_image, inv_hw, pooled, w1, w2, C, R, z1, s);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

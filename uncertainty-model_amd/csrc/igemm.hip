@@ -179,6 +179,101 @@ __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ sr
   to_raw(v, out);
 }
 
+// Epilogue shared by the register-staged and the LDS-DMA main loops: split-K
+// partial tile, or bias / residual / sigmoid-scale / stores and the BN
+// partial statistics (sStat: WM x BN x 2 floats of LDS).
+template <typename T, int BM, int BN, int WM, int WN, bool SPLIT, bool CLS>
+__device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restrict__ ws,
+                                               f32x4_t (&acc)[BM / WM / 16][BN / WN / 16],
+                                               int bm, int bn, float* sStatp) {
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  auto sStat = reinterpret_cast<float(*)[BN][2]>(sStatp);
+  const int col_l = lane & 15;
+  const int row_g = (lane >> 4) * 4;
+  if (SPLIT) {
+    float* o = ws + (long)blockIdx.z * a.M * a.NC;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = bn + wn * (BN / WN) + j * 16 + col_l;
+      if (n >= a.NC) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
+          if (m < a.M) o[(long)m * a.NC + n] = acc[i][j][q];
+        }
+    }
+    return;
+  }
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = bn + wn * (BN / WN) + j * 16 + col_l;
+    const bool nok = n < a.NC;
+    const float bv = (a.bias != nullptr && nok) ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
+        if (!nok || m >= a.M) continue;
+        float v = acc[i][j][q] + bv;
+        const long off = out_row<CLS>(a, m) + n;
+        if (a.epilogue == UM_EPI_RESIDUAL)
+          v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
+        if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
+        if (a.out_f32) {
+          float* o = reinterpret_cast<float*>(a.out) + off;
+          if (a.accumulate) v += *o;
+          *o = v;
+        } else {
+          T* o = reinterpret_cast<T*>(a.out) + off;
+          if (a.accumulate) v += to_f32(*o);
+          *o = from_f32<T>(v);
+        }
+        csum[j] += v;
+        csq[j] += v * v;
+      }
+  }
+  if (a.epilogue == UM_EPI_STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float sm = csum[j], sq = csq[j];
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      sq += __shfl_xor(sq, 16, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      if (lane < 16) {
+        sStat[wm][wn * (BN / WN) + j * 16 + lane][0] = sm;
+        sStat[wm][wn * (BN / WN) + j * 16 + lane][1] = sq;
+      }
+    }
+    __syncthreads();
+    // stats row blocks of SR rows (BM % SR == 0): waves of rows [w*BM/WM, (w+1)*BM/WM)
+    constexpr int WROWS = BM / WM;
+    const int SR = a.stats_rows;
+    const int NSB = BM / SR;
+    for (int c = tid; c < BN * NSB; c += (int)blockDim.x) {
+      const int col = c % BN, sb = c / BN;
+      const int n = bn + col;
+      if (n >= a.NC || bm + sb * SR >= a.M) continue;
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w)
+        if ((w * WROWS) / SR == sb) { sm += sStat[w][col][0]; sq += sStat[w][col][1]; }
+      float* o = a.stats + ((long)(bm / SR + sb) * a.NC + n) * 2;
+      o[0] = sm;
+      o[1] = sq;
+    }
+  }
+}
+
 template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT, bool CLS>
 __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict__ ws,
                                                      int steps, int steps_per_split, int ntn) {
@@ -308,88 +403,177 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
     __syncthreads();
   }
 
-  // ------------------------------------------------------------- epilogue --
-  const int col_l = lane & 15;
-  const int row_g = (lane >> 4) * 4;
-  if (SPLIT) {
-    float* o = ws + (long)blockIdx.z * a.M * a.NC;
+  igemm_epilogue<T, BM, BN, WM, WN, SPLIT, CLS>(a, ws, acc, bm, bn, &sStat[0][0][0]);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA main loop (bf16, BK = 64, no reflect fold): A and B tiles go
+// global -> LDS with global_load_lds_dwordx4, NST stages deep, so a block
+// keeps NST-1 k-steps of loads in flight instead of one register set.
+// The LDS image is the register path's Img<bf16, 64> (chunk ^ (row & 7)): one
+// wave instruction fills 8 rows x 128 B lane-linearly, so lane L loads the
+// global chunk (L & 7) ^ (row & 7) of row L >> 3.  Out-of-range rows, padding
+// taps and channel chunks past ach read a zero page.  All LDS is one
+// __shared__ array, waits are counted (vmcnt never 0 inside the loop) and the
+// barriers are raw s_barrier, so the DMA stays in flight across them.
+__device__ __attribute__((aligned(16))) unsigned int g_zero_page[4];
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool CLS>
+__device__ __forceinline__ const bf16_t* gather_ptr(const IgArgs& a, const bf16_t* src,
+                                                     const ARow& w, int r, int s, int c) {
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_page);
+  if (!w.ok || c >= a.ach) return zero;
+  int yy = CLS ? w.y0 - r : w.y0 + r, xx = CLS ? w.x0 - s : w.x0 + s;
+  if (a.pmode == umamd::IG_PAD_REFLECT) {
+    yy = reflect_idx(yy, a.ah);
+    xx = reflect_idx(xx, a.aw);
+  } else if (yy < 0 || yy >= a.ah || xx < 0 || xx >= a.aw) {
+    return zero;
+  }
+  return src + w.base + ((long)yy * a.aw + xx) * a.lda + c;
+}
+
+// NW = 4 or 8 waves; with 8, a 64x64 tile gives each wave a 16x32 sub-tile
+// and every SIMD two waves of the block to overlap the per-step latencies.
+template <int BM, int BN, int NW, bool SPLIT, bool CLS>
+__global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __restrict__ ws,
+                                                              int steps, int steps_per_split,
+                                                              int ntn) {
+  constexpr int BK = 64, NST = 3, WM = NW == 8 ? 4 : 2, WN = 2;
+  using I = Img<bf16_t, BK>;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int STAGE = (BM + BN) * BK;  // elements
+  constexpr int A_INS = BM / 8 / NW, B_INS = BN / 8 / NW;  // 8-row glds per wave per k-step
+  static_assert(A_INS >= 1 && B_INS >= 1, "rows per wave");
+  constexpr int PER = A_INS + B_INS;
+  static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
+  static_assert(NST * STAGE * 2 >= WM * BN * 2 * 4, "stats scratch fits the staging LDS");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  int t = blockIdx.x;
+  {
+    const int nb = gridDim.x;
+    if (nb >= 16) {
+      const int xcd = t & 7, q = nb >> 3, rr = nb & 7;
+      t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
+    }
+  }
+  const int bm = (t / ntn) * BM;
+  const int bn = (t - (t / ntn) * ntn) * BN;
+  const bf16_t* __restrict__ asrc = reinterpret_cast<const bf16_t*>(a.a);
+  const bf16_t* __restrict__ bsrc = reinterpret_cast<const bf16_t*>(a.b);
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_page);
+
+  // this lane's rows: A rows wave*(BM/4) + 8i + (lane >> 3), B likewise
+  const int lr = lane >> 3, lp = lane & 7;
+  ARow arow[A_INS];
+  int ac8[A_INS];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = bn + wn * (BN / WN) + j * 16 + col_l;
-      if (n >= a.NC) continue;
+  for (int i = 0; i < A_INS; ++i) {
+    const int row = wave * (BM / NW) + i * 8 + lr;
+    ac8[i] = lp ^ (row & 7);
+    arow[i] = decode_row<CLS>(a, bm + row);
+  }
+  int bc8[B_INS];
+  long boff_row[B_INS];
+  bool bok[B_INS];
+#pragma unroll
+  for (int i = 0; i < B_INS; ++i) {
+    const int row = wave * (BN / NW) + i * 8 + lr;
+    bc8[i] = lp ^ (row & 7);
+    bok[i] = bn + row < a.NC;
+    boff_row[i] = (long)(bn + row) * a.ldb;
+  }
+
+  const int s_begin = SPLIT ? blockIdx.z * steps_per_split : 0;
+  const int s_end = SPLIT ? min(steps, s_begin + steps_per_split) : steps;
+  const int nsteps = s_end - s_begin;
+  const int nchunk = (a.ach + BK - 1) / BK;
+  int tap = s_begin / nchunk;
+  int c0 = (s_begin - tap * nchunk) * BK;
+  const int RX = CLS ? a.Rx : a.R;
+  int r = tap / RX, s = tap - (tap / RX) * RX;
+
+  // issue the k-step at the cursor (r, s, c0) into stage `st`, then advance
+  auto issue = [&](int st) {
+    bf16_t* base = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+      const bf16_t* g = gather_ptr<CLS>(a, asrc, arow[i], r, s, c0 + ac8[i] * 8);
+      __builtin_amdgcn_global_load_lds(
+          g, (__attribute__((address_space(3))) void*)(base + (wave * (BM / NW) + i * 8) * BK), 16,
+          0, 0);
+    }
+    const int btap = CLS ? (a.r0y + 2 * r) * a.wR + (a.r0x + 2 * s)
+                         : (a.flip ? (a.R - 1 - r) * a.R + (a.R - 1 - s) : r * a.R + s);
+    const long boff = (long)btap * a.ach;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+      const int c = c0 + bc8[i] * 8;
+      const bf16_t* g = (bok[i] && c < a.ach) ? bsrc + boff_row[i] + boff + c : zero;
+      __builtin_amdgcn_global_load_lds(
+          g,
+          (__attribute__((address_space(3))) void*)(base + BM * BK +
+                                                    (wave * (BN / NW) + i * 8) * BK),
+          16, 0, 0);
+    }
+    c0 += BK;
+    if (c0 >= a.ach) {
+      c0 = 0;
+      if (++s == RX) { s = 0; ++r; }
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fg = lane >> 4;
+  const int npro = nsteps < NST ? nsteps : NST;
+  for (int p = 0; p < npro; ++p) issue(p);
+  for (int k = 0; k < nsteps; ++k) {
+    // this wave's loads of step k have landed when at most the later issued
+    // steps' loads are outstanding
+    const int later = nsteps - 1 - k;
+    if (later >= 2) wait_vm<2 * PER>();
+    else if (later == 1) wait_vm<PER>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for step k is in LDS
+    const int cur = k % NST;
+    const bf16_t* sA = smem + cur * STAGE;
+    const bf16_t* sB = sA + BM * BK;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      Frag<bf16_t> fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        lds_frag(&sA[I::off(wm * (BM / WM) + i * 16 + frow, kk * 4 + fg)], fa[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        lds_frag(&sB[I::off(wn * (BN / WN) + j * 16 + frow, kk * 4 + fg)], fb[j]);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
-          if (m < a.M) o[(long)m * a.NC + n] = acc[i][j][q];
-        }
+        for (int j = 0; j < TN; ++j) mfma(acc[i][j], fa[i], fb[j]);
     }
-    return;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage `cur` is free again
+    if (k + NST < nsteps) issue(cur);
   }
-  float csum[TN], csq[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = bn + wn * (BN / WN) + j * 16 + col_l;
-    const bool nok = n < a.NC;
-    const float bv = (a.bias != nullptr && nok) ? a.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
-        if (!nok || m >= a.M) continue;
-        float v = acc[i][j][q] + bv;
-        const long off = out_row<CLS>(a, m) + n;
-        if (a.epilogue == UM_EPI_RESIDUAL)
-          v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
-        if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
-        if (a.out_f32) {
-          float* o = reinterpret_cast<float*>(a.out) + off;
-          if (a.accumulate) v += *o;
-          *o = v;
-        } else {
-          T* o = reinterpret_cast<T*>(a.out) + off;
-          if (a.accumulate) v += to_f32(*o);
-          *o = from_f32<T>(v);
-        }
-        csum[j] += v;
-        csq[j] += v * v;
-      }
-  }
-  if (a.epilogue == UM_EPI_STATS) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float sm = csum[j], sq = csq[j];
-      sm += __shfl_xor(sm, 16, 64);
-      sm += __shfl_xor(sm, 32, 64);
-      sq += __shfl_xor(sq, 16, 64);
-      sq += __shfl_xor(sq, 32, 64);
-      if (lane < 16) {
-        sStat[wm][wn * (BN / WN) + j * 16 + lane][0] = sm;
-        sStat[wm][wn * (BN / WN) + j * 16 + lane][1] = sq;
-      }
-    }
-    __syncthreads();
-    // stats row blocks of SR rows (BM % SR == 0): waves of rows [w*BM/WM, (w+1)*BM/WM)
-    constexpr int WROWS = BM / WM;
-    const int SR = a.stats_rows;
-    const int NSB = BM / SR;
-    for (int c = tid; c < BN * NSB; c += 256) {
-      const int col = c % BN, sb = c / BN;
-      const int n = bn + col;
-      if (n >= a.NC || bm + sb * SR >= a.M) continue;
-      float sm = 0.f, sq = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w)
-        if ((w * WROWS) / SR == sb) { sm += sStat[w][col][0]; sq += sStat[w][col][1]; }
-      float* o = a.stats + ((long)(bm / SR + sb) * a.NC + n) * 2;
-      o[0] = sm;
-      o[1] = sq;
-    }
-  }
+  // all DMA retired (the last iteration waited vmcnt(0)); reuse LDS for stats
+  __syncthreads();
+  igemm_epilogue<bf16_t, BM, BN, WM, WN, SPLIT, CLS>(a, ws, acc, bm, bn,
+                                                     reinterpret_cast<float*>(smem));
+  static_assert(WM * WN == NW, "waves");
 }
 
 // sum the split-K partials and apply the epilogue.  Block = a.stats_rows rows x
@@ -466,6 +650,7 @@ struct Plan {
 // tuning knobs (read once; UMAMD_IG_* environment variables for sweeps)
 struct Knobs {
   int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles, odd_bn, bk64;
+  int glds;
   Knobs() {
     auto env = [](const char* n, int d) {
       const char* v = getenv(n);
@@ -477,14 +662,23 @@ struct Knobs {
     // block, ~1 us per k-step at 1 block per CU), so more, smaller and split
     // tiles help: 160/320/8/256 -> 600/1024/4/1024 took 578 -> 599 pairs/s
     small_tiles = env("UMAMD_IG_SMALL_TILES", 1024);
-    split_below = env("UMAMD_IG_SPLIT_BELOW", 600);
-    split_target = env("UMAMD_IG_SPLIT_TARGET", 1024);
+    // with the 8-wave LDS-DMA loop (glds bit 2) a 64x64-tile block hides
+    // more of its own latency: measured per conv (tools/ig_micro.sh), split
+    // only below 256 tiles and to ~512 blocks -- 16x32x256->256 27 -> 24 us,
+    // 32x64x128->128 27 -> 19 us, 8x16x512->512 28 -> 25 us
+    split_below = env("UMAMD_IG_SPLIT_BELOW", 256);
+    split_target = env("UMAMD_IG_SPLIT_TARGET", 512);
     split_minsteps = env("UMAMD_IG_SPLIT_MINSTEPS", 4);
     halo = env("UMAMD_HALO", 1);
     halo_min_tiles = env("UMAMD_HALO_MIN_TILES", 256);
     odd_bn = env("UMAMD_IG_ODD_BN", 1);
     // bit 0: 64-deep k-steps for the 64x64 tiles, bit 1: for the 128-row tiles
     bk64 = env("UMAMD_IG_BK64", 3);
+    // bit 0: LDS-DMA main loop for the 64x64 tiles, bit 1: for the 128-row
+    // tiles, bit 2: 8 waves per 64x64 tile.  Step sweep (tools/sweep.sh):
+    // 0 -> 653.6, 7 -> 654.8, 5 -> 661.3 pairs/s (the 128-row tiles keep the
+    // register path: 3 LDS stages of 128-row tiles leave 1 block per CU)
+    glds = env("UMAMD_IG_GLDS", 5);
   }
 };
 Knobs& knobs() {
@@ -547,6 +741,29 @@ Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes) {
 template <typename T, int BK, int BM, int BN, int WM, int WN, bool CLS>
 int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
   const int ntm = ceil_div(a.M, BM), ntn = ceil_div(a.NC, BN);
+  if constexpr (sizeof(T) == 2 && BK == 64 && WM == 2 && WN == 2) {
+    if (a.pmode != umamd::IG_FOLD && (knobs().glds & (BM == 64 ? 1 : 2))) {
+      const bool w8 = BM == 64 && (knobs().glds & 4);
+      if (w8 && p.splits > 1)
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, true, CLS>), dim3(ntm * ntn, 1, p.splits),
+                           dim3(512), 0, st, a, ws, p.steps, p.per, ntn);
+      else if (w8)
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, false, CLS>), dim3(ntm * ntn, 1, 1),
+                           dim3(512), 0, st, a, ws, p.steps, p.per, ntn);
+      else if (p.splits > 1)
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, true, CLS>), dim3(ntm * ntn, 1, p.splits),
+                           dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
+      else
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, false, CLS>), dim3(ntm * ntn, 1, 1),
+                           dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
+      if (p.splits > 1)
+        hipLaunchKernelGGL((splitk_epilogue_kernel<T, CLS>),
+                           dim3(ceil_div(a.M, a.stats_rows), ceil_div(a.NC, EPI_COLS)), dim3(256), 0,
+                           st, a, (const float*)ws, p.splits);
+      UM_LAUNCH_CHECK();
+      return UM_OK;
+    }
+  }
   if (p.splits > 1) {
     hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, true, CLS>),
                        dim3(ntm * ntn, 1, p.splits), dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
@@ -630,6 +847,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "split_minsteps")) f = &k.split_minsteps;
   else if (!strcmp(key, "odd_bn")) f = &k.odd_bn;
   else if (!strcmp(key, "bk64")) f = &k.bk64;
+  else if (!strcmp(key, "glds")) f = &k.glds;
   if (!f) return -1;
   const int old = *f;
   *f = value;

@@ -62,8 +62,12 @@ _SIG = {
                                 's']),
     'um_bn_bwd_stats_coeffs': (_I, [_P, _I, _I, _P, _D, _P, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_coeffs': (_I, [_P, _D, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, 's']),
-    'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, 's']),
+    'um_bn_fwd_pool_parts': (_I, [_L, _L]),
+    'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, _L, _P, 's']),
     'um_bn_bwd_parts': (_I, [_L]),
+    'um_bn_bwd_fin_ws': (_L, [_L, _I]),
+    'um_bn_elu_bwd_reduce_coeffs': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
+                                        _P, _P, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_elu_bwd_reduce': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P,
                                   's']),
     'um_bn_bwd_coeffs': (_I, [_P, _D, _I, _P, _P, _P, _P, _P, _P, _F, _I, _P, _P, _P, 's']),
@@ -86,7 +90,7 @@ _SIG = {
     'um_concat_bwd_ws': (_L, [_I, _I, _I, _I]),
     'um_concat_bwd_src': (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _I, _P, _P, 's']),
     'um_channel_mean': (_I, [_I, _I, _L, _I, _P, _I, _P, 's']),
-    'um_se_mlp_fwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, 's']),
+    'um_se_mlp_fwd': (_I, [_I, _I, _I, _P, _I, _F, _P, _P, _P, _P, _P, 's']),
     'um_se_mlp_bwd': (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, 's']),
     'um_pyramid': (_I, [_P, _I, _I, _I, _I, _P, 's']),
     'um_warp': (_I, [_P, _I, _I, _I, _I, _P, _L, _L, _F, _P, 's']),

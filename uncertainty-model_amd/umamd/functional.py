@@ -167,6 +167,14 @@ def _colsum(y, C):
 
 
 _CONSTS = {}
+# A/B switches for two fused paths, both measured slower on MI355X and so off
+# by default (bench step, tools/sweep.sh): the BN backward coefficients
+# finished inside the reduce kernel by a two-level last-arriver tree
+# (638 vs 654 pairs/s: every block's agent-scope release + ticket costs more
+# than the separate reduction launch it replaces), and the SE squeeze summed
+# inside the BN forward (654 vs 659: the image-aligned row chunks)
+_FUSED_BN_BWD = os.environ.get('UMAMD_FUSED_BN_BWD', '0') == '1'
+_FUSED_SE = os.environ.get('UMAMD_FUSED_SE', '0') == '1'
 
 
 def _const_vec(value: float, n: int, device) -> torch.Tensor:
@@ -196,8 +204,14 @@ class BNSync:
             self.group = bn.process_group or dist.group.WORLD
             self.world = dist.get_world_size(self.group)
 
+    @property
+    def collective(self) -> bool:
+        """statistics go through the process group (else the one-launch
+        single-process kernels are used)"""
+        return self.group is not None and (self.world > 1 or self.force)
+
     def all_reduce(self, t: torch.Tensor):
-        if self.group is not None and (self.world > 1 or self.force):
+        if self.collective:
             dist.all_reduce(t, group=self.group)
 
 
@@ -215,7 +229,7 @@ def _bn_forward_coeffs(parts, nparts, K, count, bn, sync: BNSync, training: bool
         ws = _colred_ws(nparts, K, 2, device)
         rs = (ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
               ptr(bn.num_batches_tracked) if upd and bn.num_batches_tracked is not None else None)
-        if sync.world == 1:
+        if not sync.collective:
             # one launch: reduce the conv-epilogue partials and finish the coefficients
             call('um_bn_stats_coeffs', ptr(parts), nparts, K, ptr(ws), float(count), ptr(gamma),
                  ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs, ptr(mean),
@@ -285,18 +299,27 @@ class ConvBNELUFn(torch.autograd.Function):
             mean = shift = _const_vec(0.0, K, dev)
             invstd = scale = _const_vec(1.0, K, dev)
         a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y is f32 (pre-BN)
+        pool = None
+        if w1 is not None and _FUSED_SE:  # the SE squeeze rides in the BN-apply pass
+            npool = query('um_bn_fwd_pool_parts', M, P * Q)
+            pool = torch.empty((npool, K), dtype=torch.float32, device=dev)
         call('um_bn_elu_fwd', _dt(a), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
-             int(spec.elu))
+             int(spec.elu), P * Q, ptr(pool))
+        inv_hw = 1.0 / (P * Q)
+        if w1 is not None and not _FUSED_SE:  # separate squeeze: the means, one row per image
+            npool, inv_hw = N, 1.0
+            pool = torch.zeros((N, K), dtype=torch.float32, device=dev)
+            call('um_channel_mean', _dt(a), N, P * Q, K, ptr(a), K, ptr(pool))
         outs = [a]
         se = None
         if w1 is not None:
             R1 = w1.shape[0]
-            pooled = torch.zeros((N, K), dtype=torch.float32, device=dev)
-            call('um_channel_mean', _dt(a), N, P * Q, K, ptr(a), K, ptr(pooled))
+            pooled = torch.empty((N, K), dtype=torch.float32, device=dev)
             z1 = torch.empty((N, R1), dtype=torch.float32, device=dev)
             s = torch.empty((N, K), dtype=torch.float32, device=dev)
             w1c, w2c = w1.detach().float().contiguous(), w2.detach().float().contiguous()
-            call('um_se_mlp_fwd', N, K, R1, ptr(pooled), ptr(w1c), ptr(w2c), ptr(z1), ptr(s))
+            call('um_se_mlp_fwd', N, K, R1, ptr(pool), npool // N, inv_hw, ptr(pooled),
+                 ptr(w1c), ptr(w2c), ptr(z1), ptr(s))
             se = (pooled, z1, s)
             outs.append(s)
         ctx.spec = spec
@@ -323,8 +346,8 @@ class ConvBNELUFn(torch.autograd.Function):
         if ctx.se is not None and ds is not None:
             pooled, z1, s = ctx.se
             R1 = w1.shape[0]
-            dw1 = torch.zeros(w1.shape, dtype=torch.float32, device=dev)
-            dw2 = torch.zeros(w2.shape, dtype=torch.float32, device=dev)
+            dw1 = torch.empty(w1.shape, dtype=torch.float32, device=dev)
+            dw2 = torch.empty(w2.shape, dtype=torch.float32, device=dev)
             add_nc = torch.empty((N, K), dtype=torch.float32, device=dev)
             dz = torch.empty((N, R1), dtype=torch.float32, device=dev)
             dsc = ds.float().contiguous()
@@ -343,17 +366,31 @@ class ConvBNELUFn(torch.autograd.Function):
                 dbias = torch.empty(K, dtype=torch.float32, device=dev)
             nb = query('um_bn_bwd_parts', M)
             parts = torch.empty((nb, K, 2), dtype=torch.float32, device=dev)
-            call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
-                 ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(parts))
             world = ctx.sync.world if ctx.sync is not None else 1
             if gamma is not None:
                 dgamma = torch.empty(K, dtype=torch.float32, device=dev)
                 dbeta = torch.empty(K, dtype=torch.float32, device=dev)
-            ws = _colred_ws(nb, K, 2, dev)
-            if world == 1:
-                call('um_bn_bwd_stats_coeffs', ptr(parts), nb, K, ptr(ws), float(M), ptr(gamma),
-                     ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(k1), ptr(k2), ptr(k3))
+            single = ctx.sync is None or not ctx.sync.collective
+            if single and _FUSED_BN_BWD:
+                # one launch: the reduce kernel's last blocks finish the coefficients
+                fin = torch.empty((query('um_bn_bwd_fin_ws', M, K) // 8,), dtype=torch.float64,
+                                  device=dev)
+                call('um_bn_elu_bwd_reduce_coeffs', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+                     ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+                     ptr(parts), ptr(fin), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dbias),
+                     ptr(k1), ptr(k2), ptr(k3))
+            elif single:
+                call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+                     ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+                     ptr(parts))
+                call('um_bn_bwd_stats_coeffs', ptr(parts), nb, K, ptr(_colred_ws(nb, K, 2, dev)),
+                     float(M), ptr(gamma), ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(dbias),
+                     ptr(k1), ptr(k2), ptr(k3))
             else:
+                call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+                     ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+                     ptr(parts))
+                ws = _colred_ws(nb, K, 2, dev)
                 st = torch.empty((K + 1, 2), dtype=torch.float64, device=dev)
                 st[K].fill_(float(M))  # this rank's count, summed by the all-reduce
                 call('um_bn_stats_reduce', ptr(parts), nb, K, ptr(st), ptr(ws))
