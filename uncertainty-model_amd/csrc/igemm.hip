@@ -182,10 +182,14 @@ __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ sr
 // Epilogue shared by the register-staged and the LDS-DMA main loops: split-K
 // partial tile, or bias / residual / sigmoid-scale / stores and the BN
 // partial statistics (sStat: WM x BN x 2 floats of LDS).
+// sOut (optional, BM x BN elements of T in LDS): outputs of type T are
+// staged there and leave as 16-byte rows (8 channels per lane) instead of
+// the MFMA layout's 2-byte column scatter -- the 1x1 convs and data
+// gradients are store-bound (dx at full resolution is 2/3 of their bytes).
 template <typename T, int BM, int BN, int WM, int WN, bool SPLIT, bool CLS>
 __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restrict__ ws,
                                                f32x4_t (&acc)[BM / WM / 16][BN / WN / 16],
-                                               int bm, int bn, float* sStatp) {
+                                               int bm, int bn, float* sStatp, T* sOut) {
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -209,6 +213,8 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
     }
     return;
   }
+  const bool staged = sOut != nullptr && !a.out_f32 && a.NC % 8 == 0 && a.ld_out % 8 == 0 &&
+                      !(a.accumulate && a.epilogue == UM_EPI_STATS);
   float csum[TN], csq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
@@ -232,6 +238,8 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
           float* o = reinterpret_cast<float*>(a.out) + off;
           if (a.accumulate) v += *o;
           *o = v;
+        } else if (staged) {  // accumulate (if any) happens at the row store
+          sOut[(m - bm) * BN + (n - bn)] = from_f32<T>(v);
         } else {
           T* o = reinterpret_cast<T*>(a.out) + off;
           if (a.accumulate) v += to_f32(*o);
@@ -272,6 +280,28 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
       o[1] = sq;
     }
   }
+  if (staged) {
+    __syncthreads();
+    constexpr int CPR = BN / 8;
+    for (int c = tid; c < BM * CPR; c += (int)blockDim.x) {
+      const int r = c / CPR, c8 = (c - r * CPR) * 8;
+      const int m = bm + r, n = bn + c8;
+      if (m >= a.M || n >= a.NC) continue;
+      T* o = reinterpret_cast<T*>(a.out) + out_row<CLS>(a, m) + n;
+      if (a.accumulate) {
+        float x[8], y[8];
+        load8(&sOut[r * BN + c8], x);
+        load8(o, y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] += y[e];
+        store8(o, x);
+      } else {
+        Raw8<T> v;
+        raw_load8(&sOut[r * BN + c8], v);
+        raw_store8(o, v);
+      }
+    }
+  }
 }
 
 template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT, bool CLS>
@@ -287,8 +317,11 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
   constexpr int B_PER = (B_CH + 255) / 256;
   static_assert(WM * WN == 4, "4 waves");
 
-  __shared__ __attribute__((aligned(16))) T sA[2][BM * I::ROW];
-  __shared__ __attribute__((aligned(16))) T sB[2][BN * I::ROW];
+  // one LDS array: the two A and B stages, reused by the staged epilogue
+  constexpr int SMEM = 2 * (BM + BN) * I::ROW;
+  __shared__ __attribute__((aligned(16))) T smem[SMEM];
+  T(*sA)[BM * I::ROW] = reinterpret_cast<T(*)[BM * I::ROW]>(smem);
+  T(*sB)[BN * I::ROW] = reinterpret_cast<T(*)[BN * I::ROW]>(smem + 2 * BM * I::ROW);
   __shared__ float sStat[WM][BN][2];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -403,7 +436,8 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
     __syncthreads();
   }
 
-  igemm_epilogue<T, BM, BN, WM, WN, SPLIT, CLS>(a, ws, acc, bm, bn, &sStat[0][0][0]);
+  igemm_epilogue<T, BM, BN, WM, WN, SPLIT, CLS>(a, ws, acc, bm, bn, &sStat[0][0][0],
+                                               BM * BN <= SMEM ? smem : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -571,8 +605,11 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
   }
   // all DMA retired (the last iteration waited vmcnt(0)); reuse LDS for stats
   __syncthreads();
+  constexpr int STAT_ELEMS = (WM * BN * 2 * 4 + 15) / 16 * 8;  // bf16 elements, 16-B aligned
+  static_assert(STAT_ELEMS + BM * BN <= NST * STAGE, "staged epilogue fits the staging LDS");
   igemm_epilogue<bf16_t, BM, BN, WM, WN, SPLIT, CLS>(a, ws, acc, bm, bn,
-                                                     reinterpret_cast<float*>(smem));
+                                                     reinterpret_cast<float*>(smem),
+                                                     smem + STAT_ELEMS);
   static_assert(WM * WN == NW, "waves");
 }
 
