@@ -463,24 +463,37 @@ __global__ void __launch_bounds__(256) channel_mean_kernel(const T* __restrict__
 }
 
 // one block per image: pooled = (sum of the image's pool partial rows) / HW
-// (written out for the backward), then the excite MLP
-__global__ void se_mlp_fwd_kernel(const float* __restrict__ parts, int nparts, float inv_hw,
-                                  float* __restrict__ pooled, const float* __restrict__ w1,
-                                  const float* __restrict__ w2, int C, int R,
-                                  float* __restrict__ z1, float* __restrict__ s) {
+// (written out for the backward), then the excite MLP.  The partial rows are
+// summed by column lanes x row lanes (256 threads) and combined in LDS.
+__global__ void __launch_bounds__(256) se_mlp_fwd_kernel(
+    const float* __restrict__ parts, int nparts, float inv_hw, float* __restrict__ pooled,
+    const float* __restrict__ w1, const float* __restrict__ w2, int C, int R,
+    float* __restrict__ z1, float* __restrict__ s) {
   extern __shared__ float sh[];
   const int n = blockIdx.x;
-  float* p = sh;       // [C]
-  float* z = sh + C;   // [R]
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float* q = parts + (long)n * nparts * C + c;
+  float* p = sh;            // [C]
+  float* z = sh + C;        // [R]
+  float* red = z + R;       // [256]
+  const int CU = C < 256 ? C : 256;
+  const int L = 256 / CU;
+  const int u = threadIdx.x % CU, l = threadIdx.x / CU;
+  for (int c0 = 0; c0 < C; c0 += CU) {
+    const int c = c0 + u;
     float t = 0.f;
-    for (int b = 0; b < nparts; ++b) t += q[(long)b * C];
-    t *= inv_hw;
-    p[c] = t;
-    pooled[n * C + c] = t;
+    if (l < L && c < C) {
+      const float* q = parts + (long)n * nparts * C + c;
+      for (int b = l; b < nparts; b += L) t += q[(long)b * C];
+    }
+    red[threadIdx.x] = t;
+    __syncthreads();
+    if (l == 0 && c < C) {
+      for (int k = 1; k < L; ++k) t += red[k * CU + u];
+      t *= inv_hw;
+      p[c] = t;
+      pooled[n * C + c] = t;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int r = threadIdx.x; r < R; r += blockDim.x) {
     float t = 0.f;
     for (int c = 0; c < C; ++c) t += w1[r * C + c] * p[c];
@@ -723,7 +736,7 @@ int um_channel_mean(int dtype, int N, long S, int C, const void* x, int ld, floa
 int um_se_mlp_fwd(int N, int C, int R, const float* pool_parts, int parts_per_image,
                   float inv_hw, float* pooled, const float* w1, const float* w2, float* z1,
                   float* s, hipStream_t st) {
-  hipLaunchKernelGGL(se_mlp_fwd_kernel, dim3(N), dim3(256), (C + R) * sizeof(float), st,
+  hipLaunchKernelGGL(se_mlp_fwd_kernel, dim3(N), dim3(256), (C + R + 256) * sizeof(float), st,
                      pool_parts, parts_per_image, inv_hw, pooled, w1, w2, C, R, z1, s);
   UM_LAUNCH_CHECK();
   return UM_OK;

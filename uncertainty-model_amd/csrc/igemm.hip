@@ -687,6 +687,7 @@ struct Plan {
 // tuning knobs (read once; UMAMD_IG_* environment variables for sweeps)
 struct Knobs {
   int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles, odd_bn, bk64;
+  int glds_split_below, glds_split_target;
   int glds;
   Knobs() {
     auto env = [](const char* n, int d) {
@@ -699,12 +700,15 @@ struct Knobs {
     // block, ~1 us per k-step at 1 block per CU), so more, smaller and split
     // tiles help: 160/320/8/256 -> 600/1024/4/1024 took 578 -> 599 pairs/s
     small_tiles = env("UMAMD_IG_SMALL_TILES", 1024);
-    // with the 8-wave LDS-DMA loop (glds bit 2) a 64x64-tile block hides
-    // more of its own latency: measured per conv (tools/ig_micro.sh), split
-    // only below 256 tiles and to ~512 blocks -- 16x32x256->256 27 -> 24 us,
-    // 32x64x128->128 27 -> 19 us, 8x16x512->512 28 -> 25 us
-    split_below = env("UMAMD_IG_SPLIT_BELOW", 256);
-    split_target = env("UMAMD_IG_SPLIT_TARGET", 512);
+    split_below = env("UMAMD_IG_SPLIT_BELOW", 600);
+    split_target = env("UMAMD_IG_SPLIT_TARGET", 1024);
+    // the 8-wave LDS-DMA loop (glds bit 2) hides more of a 64x64-tile
+    // block's own latency: measured per conv (tools/ig_micro.sh), split only
+    // below 256 tiles and to ~512 blocks -- 16x32x256->256 27 -> 24 us,
+    // 32x64x128->128 27 -> 19 us, 8x16x512->512 28 -> 25 us.  The register
+    // path (reflect-fold data gradients, f32) keeps the thresholds above.
+    glds_split_below = env("UMAMD_IG_GLDS_SPLIT_BELOW", 256);
+    glds_split_target = env("UMAMD_IG_GLDS_SPLIT_TARGET", 512);
     split_minsteps = env("UMAMD_IG_SPLIT_MINSTEPS", 4);
     halo = env("UMAMD_HALO", 1);
     halo_min_tiles = env("UMAMD_HALO_MIN_TILES", 256);
@@ -732,7 +736,9 @@ bool small_tiles(int M, int NC) {
   return k.small && NC > 64 && (long)ceil_div(M, 128) * ceil_div(NC, 128) < k.small_tiles;
 }
 
-Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes) {
+// glds: the launch will take the LDS-DMA loop (its split thresholds); the
+// workspace query passes false, whose split counts bound the LDS-DMA ones
+Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes, bool glds) {
   const Knobs& kn = knobs();
   Plan p{};
   p.bk = 32;
@@ -763,8 +769,10 @@ Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes) {
   // of partials.
   const long tiles = (long)ceil_div(M, p.bm) * ceil_div(NC, p.bn);
   p.splits = 1;
-  if (tiles < kn.split_below && NC % 4 == 0) {
-    long sp = (kn.split_target + tiles - 1) / tiles;
+  const int below = glds ? kn.glds_split_below : kn.split_below;
+  const int target = glds ? kn.glds_split_target : kn.split_target;
+  if (tiles < below && NC % 4 == 0) {
+    long sp = (target + tiles - 1) / tiles;
     sp = std::min<long>(sp, p.steps / kn.split_minsteps);
     sp = std::min<long>(sp, (32l << 20) / ((long)M * NC * 4));
     if (ws_bytes >= 0) sp = std::min<long>(sp, ws_bytes / ((long)M * NC * 4));
@@ -852,7 +860,7 @@ int dispatch_tiles(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
 namespace umamd {
 
 long igemm_ws_bytes(int dtype, int M, int NC, int taps, int ach) {
-  const Plan p = make_plan(dtype, M, NC, taps, ach, -1);
+  const Plan p = make_plan(dtype, M, NC, taps, ach, -1, false);
   return p.splits > 1 ? (long)p.splits * M * NC * 4 : 0;
 }
 
@@ -863,7 +871,10 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   IgArgs a = a_in;
   a.stats_rows = igemm_stats_rows(a.M, a.NC);
   if (knobs().halo && halo_applicable(dtype, a, knobs().halo_min_tiles)) return halo_run(a, st);
-  const Plan p = make_plan(dtype, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0);
+  // the LDS-DMA loop serves the bf16 64x64 tiles without the reflect fold
+  Plan p = make_plan(dtype, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0, false);
+  if (dtype == UM_BF16 && p.bm == 64 && p.bk == 64 && a.pmode != IG_FOLD && (knobs().glds & 1))
+    p = make_plan(dtype, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0, true);
   if (dtype == UM_BF16) return dispatch_tiles<bf16_t>(a, p, ws, st);
   return dispatch_tiles<float>(a, p, ws, st);
 }
@@ -881,6 +892,8 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "small_tiles")) f = &k.small_tiles;
   else if (!strcmp(key, "split_below")) f = &k.split_below;
   else if (!strcmp(key, "split_target")) f = &k.split_target;
+  else if (!strcmp(key, "glds_split_below")) f = &k.glds_split_below;
+  else if (!strcmp(key, "glds_split_target")) f = &k.glds_split_target;
   else if (!strcmp(key, "split_minsteps")) f = &k.split_minsteps;
   else if (!strcmp(key, "odd_bn")) f = &k.odd_bn;
   else if (!strcmp(key, "bk64")) f = &k.bk64;

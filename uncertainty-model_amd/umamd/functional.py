@@ -167,14 +167,15 @@ def _colsum(y, C):
 
 
 _CONSTS = {}
-# A/B switches for two fused paths, both measured slower on MI355X and so off
-# by default (bench step, tools/sweep.sh): the BN backward coefficients
-# finished inside the reduce kernel by a two-level last-arriver tree
-# (638 vs 654 pairs/s: every block's agent-scope release + ticket costs more
-# than the separate reduction launch it replaces), and the SE squeeze summed
-# inside the BN forward (654 vs 659: the image-aligned row chunks)
+# A/B switches for two fused paths (bench step, tools/sweep.sh):
+#  - the SE squeeze summed inside the BN forward (per-block channel sums,
+#    finished by the SE MLP kernel): on, 676 -> 678 pairs/s (-10 launches)
+#  - the BN backward coefficients finished inside the reduce kernel by a
+#    two-level last-arriver tree: off, 676 -> 652 -- every block's
+#    agent-scope release + ticket costs more than the separate reduction
+#    launch it replaces
 _FUSED_BN_BWD = os.environ.get('UMAMD_FUSED_BN_BWD', '0') == '1'
-_FUSED_SE = os.environ.get('UMAMD_FUSED_SE', '0') == '1'
+_FUSED_SE = os.environ.get('UMAMD_FUSED_SE', '1') == '1'
 
 
 def _const_vec(value: float, n: int, device) -> torch.Tensor:
