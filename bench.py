@@ -100,6 +100,16 @@ def step(m, lf, opt, left, right, scale):
     return dl, el
 
 
+def baseline_config(a, world, cfg):
+    """which BASELINE.json config the run's shape is"""
+    nodes = cfg['model']['encoder'].get('nodes')
+    if nodes == 10 and (a.height, a.width) == (512, 1024):
+        return '5'
+    if (a.height, a.width) == (128, 256):
+        return '1'
+    return '2' if world == 1 else '4'
+
+
 def time_eager(m, lf, opt, left, right, scale, batch, steps):
     """The same step launched eagerly from Python, for comparison with the
     captured graph (after the timed region; the graphs are not replayed
@@ -402,12 +412,14 @@ def main():
             'dtype': a.dtype, 'data': 'synthetic U[0,1) stereo pairs (device-resident), '
                                       'formula-free random init (torch.manual_seed(0))',
             'config': {'workload': f'depth+uncertainty train step (BASELINE config '
-                                   f'{"2" if world == 1 else "4"}): fwd+4-scale loss+bwd+Adam',
+                                   f'{baseline_config(a, world, cfg)}): '
+                                   f'fwd+4-scale loss+bwd+Adam',
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch,
                        'height': a.height, 'width': a.width, 'loss': a.loss_type,
                        'parallelism': f'dp{world}' + ('+syncbn' if dp else ''),
                        'launch': 'hip-graph' if use_graph else 'eager',
-                       'graph': 'config.yml (nodes=5, K5 stage graphs)'},
+                       'graph': f'{a.config} (nodes={cfg["model"]["encoder"].get("nodes")} '
+                                f'stage graphs)'},
             'eager_launch': eager,
             'fp32_line': fp32,
             'final_losses': {'disp': round(losses[0], 5), 'error': round(losses[1], 5)},

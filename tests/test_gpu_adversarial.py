@@ -167,3 +167,41 @@ def test_adversarial_bf16_runs():
     assert all(torch.isfinite(t) for t in (dl, el, dsl))
     for k, p in d.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), k
+
+
+def test_adversarial_config3_full_size():
+    """BASELINE config 3 shape (config 2 + discriminator: B=8, 256x512,
+    bayesian, bf16, config.yml's discriminator with its 32768-feature head):
+    one adversarial step past perceptual_start -- finite losses and gradients
+    on both networks, and the bf16 disparity/error losses within the bf16 bar
+     of an fp32 step from the same weights."""
+    from copy import deepcopy
+    import model as M
+    from test_gpu_model import _uniform_pair
+    from train.loss import TukraUncertaintyLoss
+    from train.train import train_step
+    from umamd.optim import Adam
+    cfg = _cfg()
+    dcfg = dict(cfg['discriminator'])
+    dcfg['load_graph'] = os.path.join(REPO, dcfg['load_graph'])
+    left, right = _uniform_pair(8, 256, 512, seed=7)
+    left, right = left.to(DEV), right.to(DEV)
+    torch.manual_seed(0)
+    d16 = M.RandomDiscriminator(**dcfg, dtype='bf16').to(DEV).train()
+    d32 = M.RandomDiscriminator(**dcfg, dtype='fp32').to(DEV).train()
+    d32.load_state_dict(d16.state_dict())
+    m16 = _model(cfg, 'bf16').train()
+    m32 = _model(cfg, 'fp32').train()
+    res = []
+    for m, d in ((m16, d16), (m32, d32)):
+        lf = TukraUncertaintyLoss(**cfg['loss'])
+        dl, el, dsl = train_step(m, left, right, lf, Adam(m.parameters(), 1e-4), 0.3, 4, 5, d,
+                                 deepcopy(d), Adam(d.parameters(), 1e-4), torch.nn.BCELoss())
+        torch.cuda.synchronize()
+        assert all(torch.isfinite(t) for t in (dl, el, dsl))
+        for net in (m, d):
+            for k, p in net.named_parameters():
+                assert p.grad is not None and torch.isfinite(p.grad).all(), k
+        res.append((float(dl), float(el), float(dsl)))
+    (a16, e16, _), (a32, e32, _) = res
+    assert abs(a16 / a32 - 1) < 2e-2 and abs(e16 / e32 - 1) < 3e-2, res

@@ -414,3 +414,30 @@ def test_nodes10_train_step_matches_oracle():
         if abs(got - ref) > 2e-2 * ref + atol:
             bad.append((k, got, ref))
     assert not bad, bad[:8]
+
+
+def test_config5_nodes10_512x1024_properties():
+    """BASELINE config 5 per-GPU shape (B=8, 512x1024, nodes=10 graphs,
+    bayesian, bf16): one training step through the out-of-place GraphBlock
+    sum -- finite losses and gradients, and the bf16 loss scalars
+    within the bf16 bar of an fp32 step from the same weights."""
+    from train.loss import TukraUncertaintyLoss
+    from train.train import train_step
+    from umamd.optim import Adam
+    cfg = _cfg('config_nodes10.yml')
+    cfg['loss']['error_loss_config']['loss_type'] = 'bayesian'
+    m16 = _model(cfg, 'bf16').train()
+    m32 = _model(cfg, 'fp32').train()
+    left, right = _uniform_pair(8, 512, 1024, seed=5)
+    left, right = left.to(DEV), right.to(DEV)
+    losses = []
+    for m in (m16, m32):
+        lf = TukraUncertaintyLoss(**cfg['loss'])
+        dl, el, _ = train_step(m, left, right, lf, Adam(m.parameters(), 1e-4), 0.3)
+        torch.cuda.synchronize()
+        assert torch.isfinite(dl) and torch.isfinite(el)
+        for k, p in m.named_parameters():
+            assert p.grad is not None and torch.isfinite(p.grad).all(), k
+        losses.append((float(dl), float(el)))
+    (d16, e16), (d32, e32) = losses
+    assert abs(d16 / d32 - 1) < 1e-2 and abs(e16 / e32 - 1) < 3e-2, losses
