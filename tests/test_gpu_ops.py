@@ -156,7 +156,8 @@ def test_merge(dtype):
         assert _rel(a.grad, b.grad) < tol
 
 
-@pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 8), (512, 2, 4), (256, 4, 8)])
+@pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 8), (512, 2, 4), (256, 4, 8),
+                                   (32, 20, 30), (128, 12, 16), (64, 40, 72)])
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 def test_attention_block(C, H, W, dtype):
     from oracle.model import efficient_attention
@@ -174,7 +175,9 @@ def test_attention_block(C, H, W, dtype):
     yd = U.attention_block(xd, ad)
     (yd.float() * _nhwc(g)).sum().backward()
     tol = 1e-4 if dtype == torch.float32 else 5e-2
-    assert _rel(_nchw(yd), yr) < tol / 10
+    # bf16 output: one rounding of the stored activation is up to 2^-8 of
+    # the largest value, so the forward bar is ~2.5 ulp there
+    assert _rel(_nchw(yd), yr) < (tol / 10 if dtype == torch.float32 else 1e-2)
     assert _rel(_nchw(xd.grad), xr.grad) < tol
     for name in ('keys', 'queries', 'values', 'reprojection'):
         for t in ('weight', 'bias'):
