@@ -343,6 +343,258 @@ __global__ void k_bwd_kernel(const T* __restrict__ qkv, int ld, long M, int S, i
   }
 }
 
+// ------------------------------------------------ narrow heads (d = 4, 8) --
+// The stage-1/2 attention (C = 32/64, 8 heads) has d = 4/8: one head of one
+// pixel is 8-16 bytes.  These kernels give each thread one (pixel, head) pair
+// in registers -- a block row of H threads covers a pixel's C contiguous
+// channels -- and reduce the d x d outer products of the context / its
+// gradient across the block with cross-lane shuffles (lanes H apart hold the
+// same head) and one LDS pass over the 4 waves.
+constexpr int NT_PX = 4;  // pixels per thread in the reducing kernels
+
+template <int D, typename T>
+__device__ __forceinline__ void loadD(const T* p, float* v) {
+  if constexpr (D == 8) {
+    load8(p, v);
+  } else if constexpr (sizeof(T) == 2) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else {
+    const float4 f = *reinterpret_cast<const float4*>(p);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+  }
+}
+template <int D, typename T>
+__device__ __forceinline__ void storeD(T* p, const float* v) {
+  if constexpr (D == 8) {
+    store8(p, v);
+  } else if constexpr (sizeof(T) == 2) {
+    uint2 u;
+    u.x = pack_bf16x2(v[0], v[1]);
+    u.y = pack_bf16x2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(p) = u;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// sum acc[K] over the threads of the block that share a head (t % H) and
+// leave each wave's head sums in red[wave][h][K] (4 * H * K floats of LDS);
+// the caller adds the 4 wave rows
+template <int K>
+__device__ __forceinline__ void head_reduce(float (&acc)[K], int H, float* red) {
+  for (int o = H; o < 64; o <<= 1)
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+  const int wave = threadIdx.x >> 6, wl = threadIdx.x & 63;
+  if (wl < H)
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[(wave * H + wl) * K + k] = acc[k];
+  __syncthreads();
+}
+
+// ctx partial over a chunk: parts[n][chunk][h][D][D]
+template <typename T, int D>
+__global__ void __launch_bounds__(256) ctx_small_kernel(
+    const T* __restrict__ qkv, int ld, int S, int C, int H, const float* __restrict__ kmax,
+    const float* __restrict__ ksum, int chunk_px, int nchunks, float* __restrict__ parts) {
+  __shared__ float red[4 * 64 * D];  // 4 waves x H x D*D (H*D <= 64)
+  const int n = blockIdx.y, chunk = blockIdx.x;
+  const int h = threadIdx.x % H, pl = threadIdx.x / H, PL = 256 / H;
+  const int s0 = chunk * chunk_px, s1 = min(S, s0 + chunk_px);
+  float km[D], kinv[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    km[c] = kmax[n * C + h * D + c];
+    kinv[c] = 1.f / ksum[n * C + h * D + c];
+  }
+  float acc[D * D];
+#pragma unroll
+  for (int k = 0; k < D * D; ++k) acc[k] = 0.f;
+  for (int s = s0 + pl; s < s1; s += PL) {
+    const long row = ((long)n * S + s) * ld;
+    float k[D], v[D];
+    loadD<D>(qkv + row + h * D, k);
+    loadD<D>(qkv + row + 2 * C + h * D, v);
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      const float ks = __expf(k[c] - km[c]) * kinv[c];
+#pragma unroll
+      for (int cp = 0; cp < D; ++cp) acc[c * D + cp] += ks * v[cp];
+    }
+  }
+  head_reduce<D * D>(acc, H, red);
+  for (int o = threadIdx.x; o < H * D * D; o += 256) {
+    const int hh = o / (D * D), r = o - hh * D * D;
+    float t = 0.f;
+    for (int w = 0; w < 4; ++w) t += red[(w * H + hh) * D * D + r];
+    parts[(((long)n * nchunks + chunk) * H + hh) * D * D + r] = t;
+  }
+}
+
+// att = softmax_d(Q) ctx: one (pixel, head) per thread
+template <typename T, int D>
+__global__ void __launch_bounds__(256) apply_small_kernel(const T* __restrict__ qkv, int ld,
+                                                          int S, int C, int H,
+                                                          const float* __restrict__ ctx,
+                                                          T* __restrict__ att, int ldo) {
+  __shared__ float sC[64 * D];  // H x D x D (C = H*D <= 64)
+  const int n = blockIdx.y;
+  for (int i = threadIdx.x; i < C * D; i += 256) sC[i] = ctx[(long)n * C * D + i];
+  __syncthreads();
+  const int h = threadIdx.x % H, pl = threadIdx.x / H, PL = 256 / H;
+  const int s = blockIdx.x * PL + pl;
+  if (s >= S) return;
+  const long row = (long)n * S + s;
+  float q[D];
+  loadD<D>(qkv + row * ld + C + h * D, q);
+  float mx = q[0];
+#pragma unroll
+  for (int c = 1; c < D; ++c) mx = fmaxf(mx, q[c]);
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    q[c] = __expf(q[c] - mx);
+    sum += q[c];
+  }
+  const float inv = 1.f / sum;
+  const float* cm = sC + h * D * D;
+  float o[D];
+#pragma unroll
+  for (int cp = 0; cp < D; ++cp) {
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) a += q[c] * cm[c * D + cp];
+    o[cp] = a * inv;
+  }
+  storeD<D>(att + row * ldo + h * D, o);
+}
+
+// dQ and the partial dctx per tile of NT_PX * 256/H pixels
+template <typename T, int D>
+__global__ void __launch_bounds__(256) apply_bwd_small_kernel(
+    const T* __restrict__ qkv, int ld, int S, int C, int H, const float* __restrict__ ctx,
+    const T* __restrict__ datt, int ldd, T* __restrict__ dqkv, int ldq, int ntiles,
+    float* __restrict__ parts) {
+  __shared__ float sC[64 * D];
+  __shared__ float red[4 * 64 * D];
+  const int n = blockIdx.y, tile = blockIdx.x;
+  for (int i = threadIdx.x; i < C * D; i += 256) sC[i] = ctx[(long)n * C * D + i];
+  __syncthreads();
+  const int h = threadIdx.x % H, pl = threadIdx.x / H, PL = 256 / H;
+  const float* cm = sC + h * D * D;
+  float acc[D * D];
+#pragma unroll
+  for (int k = 0; k < D * D; ++k) acc[k] = 0.f;
+  for (int it = 0; it < NT_PX; ++it) {
+    const int s = (tile * NT_PX + it) * PL + pl;
+    if (s >= S) break;
+    const long row = (long)n * S + s;
+    float q[D], g[D];
+    loadD<D>(qkv + row * ld + C + h * D, q);
+    loadD<D>(datt + row * ldd + h * D, g);
+    float mx = q[0];
+#pragma unroll
+    for (int c = 1; c < D; ++c) mx = fmaxf(mx, q[c]);
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      q[c] = __expf(q[c] - mx);
+      sum += q[c];
+    }
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int c = 0; c < D; ++c) q[c] *= inv;
+    float dqs[D], dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      float a = 0.f;
+#pragma unroll
+      for (int cp = 0; cp < D; ++cp) a += cm[c * D + cp] * g[cp];
+      dqs[c] = a;
+      dot += q[c] * a;
+    }
+    float dq[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      dq[c] = q[c] * (dqs[c] - dot);
+#pragma unroll
+      for (int cp = 0; cp < D; ++cp) acc[c * D + cp] += q[c] * g[cp];
+    }
+    storeD<D>(dqkv + row * ldq + C + h * D, dq);
+  }
+  head_reduce<D * D>(acc, H, red);
+  for (int o = threadIdx.x; o < H * D * D; o += 256) {
+    const int hh = o / (D * D), r = o - hh * D * D;
+    float t = 0.f;
+    for (int w = 0; w < 4; ++w) t += red[(w * H + hh) * D * D + r];
+    parts[(((long)n * ntiles + tile) * H + hh) * D * D + r] = t;
+  }
+}
+
+// dV, dKs (f32 [m][C]) and the partial r[c] = sum_s Ks dKs per tile
+template <typename T, int D>
+__global__ void __launch_bounds__(256) kv_bwd_small_kernel(
+    const T* __restrict__ qkv, int ld, int S, int C, int H, const float* __restrict__ kmax,
+    const float* __restrict__ ksum, const float* __restrict__ dctx, T* __restrict__ dqkv,
+    int ldq, float* __restrict__ dks, int ntiles, float* __restrict__ parts) {
+  __shared__ float sC[64 * D];
+  __shared__ float red[4 * 64];
+  const int n = blockIdx.y, tile = blockIdx.x;
+  for (int i = threadIdx.x; i < C * D; i += 256) sC[i] = dctx[(long)n * C * D + i];
+  __syncthreads();
+  const int h = threadIdx.x % H, pl = threadIdx.x / H, PL = 256 / H;
+  const float* cm = sC + h * D * D;
+  float km[D], kinv[D], acc[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    km[c] = kmax[n * C + h * D + c];
+    kinv[c] = 1.f / ksum[n * C + h * D + c];
+    acc[c] = 0.f;
+  }
+  for (int it = 0; it < NT_PX; ++it) {
+    const int s = (tile * NT_PX + it) * PL + pl;
+    if (s >= S) break;
+    const long row = (long)n * S + s;
+    float k[D], v[D];
+    loadD<D>(qkv + row * ld + h * D, k);
+    loadD<D>(qkv + row * ld + 2 * C + h * D, v);
+#pragma unroll
+    for (int c = 0; c < D; ++c) k[c] = __expf(k[c] - km[c]) * kinv[c];
+    float g[D], dv[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int cp = 0; cp < D; ++cp) {
+        a += cm[c * D + cp] * v[cp];  // dKs[c]
+        b += k[cp] * cm[cp * D + c];  // dV[c]
+      }
+      g[c] = a;
+      dv[c] = b;
+      acc[c] += k[c] * a;
+    }
+    float* dk = dks + row * C + h * D;
+#pragma unroll
+    for (int c = 0; c < D; c += 4)
+      *reinterpret_cast<float4*>(dk + c) = make_float4(g[c], g[c + 1], g[c + 2], g[c + 3]);
+    storeD<D>(dqkv + row * ldq + 2 * C + h * D, dv);
+  }
+  head_reduce<D>(acc, H, red);
+  for (int o = threadIdx.x; o < H * D; o += 256) {
+    const int hh = o / D, r = o - hh * D;
+    float t = 0.f;
+    for (int w = 0; w < 4; ++w) t += red[(w * H + hh) * D + r];
+    parts[((long)n * ntiles + tile) * C + o] = t;
+  }
+}
+
+static inline bool small_heads(int C, int heads) {
+  const int d = C / heads;
+  return (d == 4 || d == 8) && C <= 64 && 64 % heads == 0;
+}
+
 inline int grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -354,6 +606,53 @@ inline int ctx_chunk(int d) {  // keeps the ctx kernel's LDS <= 33 KB
   int c = 4096 / d;
   if (c > 1024) c = 1024;
   return c;
+}
+
+// the backward for narrow heads: the register kernels, tiles of
+// NT_PX * 256/H pixels (never more tiles than um_attn_ws_tiles sizes for)
+template <typename T, int D>
+int attn_bwd_small_t(int N, int S, int C, int heads, const void* qkv, int ld, const float* kmax,
+                     const float* ksum, const float* ctx, const void* datt, int ldd, void* dqkv,
+                     int ldq, float* dks_ws, float* ws, float* dctx, float* r, hipStream_t st) {
+  const int tp = NT_PX * (256 / heads);
+  const int nt = ceil_div(S, tp);
+  hipLaunchKernelGGL((apply_bwd_small_kernel<T, D>), dim3(nt, N), dim3(256), 0, st,
+                     (const T*)qkv, ld, S, C, heads, ctx, (const T*)datt, ldd, (T*)dqkv, ldq, nt,
+                     ws);
+  const int L = heads * D * D;
+  {
+    const int jl = sum_parts_cols(L, nt);
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div(L, jl), N), dim3(256), 0, st, ws, N, nt, L,
+                       dctx, jl);
+  }
+  hipLaunchKernelGGL((kv_bwd_small_kernel<T, D>), dim3(nt, N), dim3(256), 0, st, (const T*)qkv,
+                     ld, S, C, heads, kmax, ksum, dctx, (T*)dqkv, ldq, dks_ws, nt, ws);
+  {
+    const int jl = sum_parts_cols(C, nt);
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(ceil_div(C, jl), N), dim3(256), 0, st, ws, N, nt, C,
+                       r, jl);
+  }
+  const long M = (long)N * S;
+  hipLaunchKernelGGL(k_bwd_kernel<T>, dim3(grid_for(M * C)), dim3(256), 0, st, (const T*)qkv, ld,
+                     M, S, C, kmax, ksum, dks_ws, r, (T*)dqkv, ldq);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int attn_bwd_small(int dtype, int N, int S, int C, int heads, const void* qkv, int ld,
+                   const float* kmax, const float* ksum, const float* ctx, const void* datt,
+                   int ldd, void* dqkv, int ldq, float* dks_ws, float* ws, float* dctx, float* r,
+                   hipStream_t st) {
+  const int d = C / heads;
+  if (dtype == UM_BF16)
+    return d == 4 ? attn_bwd_small_t<bf16_t, 4>(N, S, C, heads, qkv, ld, kmax, ksum, ctx, datt,
+                                                ldd, dqkv, ldq, dks_ws, ws, dctx, r, st)
+                  : attn_bwd_small_t<bf16_t, 8>(N, S, C, heads, qkv, ld, kmax, ksum, ctx, datt,
+                                                ldd, dqkv, ldq, dks_ws, ws, dctx, r, st);
+  return d == 4 ? attn_bwd_small_t<float, 4>(N, S, C, heads, qkv, ld, kmax, ksum, ctx, datt, ldd,
+                                             dqkv, ldq, dks_ws, ws, dctx, r, st)
+                : attn_bwd_small_t<float, 8>(N, S, C, heads, qkv, ld, kmax, ksum, ctx, datt, ldd,
+                                             dqkv, ldq, dks_ws, ws, dctx, r, st);
 }
 
 }  // namespace
@@ -394,8 +693,16 @@ int um_attn_fwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
   }
   hipLaunchKernelGGL(kstats_combine_kernel, dim3(ceil_div(N * C, 4)), dim3(256), 0, st, ws, N,
                      nks, C, kmax, ksum);
+  const bool small = small_heads(C, heads) && ld % 8 == 0 && ldo % 8 == 0;
   const size_t shm_ctx = (2 * (size_t)cch * d + 256) * sizeof(float);
-  if (dtype == UM_BF16)
+  if (small) {
+#define UM_CTXS(T_, D_)                                                                       \
+  hipLaunchKernelGGL((ctx_small_kernel<T_, D_>), dim3(nctx, N), dim3(256), 0, st,             \
+                     (const T_*)qkv, ld, S, C, heads, kmax, ksum, cch, nctx, ws)
+    if (dtype == UM_BF16) { if (d == 4) UM_CTXS(bf16_t, 4); else UM_CTXS(bf16_t, 8); }
+    else { if (d == 4) UM_CTXS(float, 4); else UM_CTXS(float, 8); }
+#undef UM_CTXS
+  } else if (dtype == UM_BF16)
     hipLaunchKernelGGL(ctx_kernel<bf16_t>, dim3(nctx, heads, N), dim3(256), shm_ctx, st,
                        (const bf16_t*)qkv, ld, S, C, heads, kmax, ksum, cch, nctx, ws);
   else
@@ -409,7 +716,15 @@ int um_attn_fwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
   }
   const size_t shm_ap = ((size_t)d * d + PT * (d + 1)) * sizeof(float);
   const dim3 g(ceil_div(S, PT), heads, N);
-  if (dtype == UM_BF16)
+  if (small) {
+    const dim3 gs(ceil_div(S, 256 / heads), N);
+#define UM_APS(T_, D_)                                                                        \
+  hipLaunchKernelGGL((apply_small_kernel<T_, D_>), gs, dim3(256), 0, st, (const T_*)qkv, ld, S, \
+                     C, heads, ctx, (T_*)att, ldo)
+    if (dtype == UM_BF16) { if (d == 4) UM_APS(bf16_t, 4); else UM_APS(bf16_t, 8); }
+    else { if (d == 4) UM_APS(float, 4); else UM_APS(float, 8); }
+#undef UM_APS
+  } else if (dtype == UM_BF16)
     hipLaunchKernelGGL(apply_kernel<bf16_t>, g, dim3(256), shm_ap, st, (const bf16_t*)qkv, ld, S,
                        C, heads, ctx, (bf16_t*)att, ldo);
   else
@@ -427,6 +742,9 @@ int um_attn_bwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
                 hipStream_t st) {
   const int d = C / heads;
   UM_CHECK_ARG(d <= 64 && C % heads == 0, "um_attn_bwd: head dim");
+  if (small_heads(C, heads) && ld % 8 == 0 && ldd % 8 == 0 && ldq % 8 == 0)
+    return attn_bwd_small(dtype, N, S, C, heads, qkv, ld, kmax, ksum, ctx, datt, ldd, dqkv, ldq,
+                          dks_ws, ws, dctx, r, st);
   const int nt = ceil_div(S, PT);
   const dim3 g(nt, heads, N);
   const size_t shm_a = ((size_t)d * d + 3 * PT * (d + 1)) * sizeof(float);
