@@ -494,12 +494,16 @@ __global__ void __launch_bounds__(256) se_mlp_fwd_kernel(
     }
     __syncthreads();
   }
-  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+  // z = relu(W1 p): one wave per output row, lanes over the C inputs
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int r = wave; r < R; r += 4) {
     float t = 0.f;
-    for (int c = 0; c < C; ++c) t += w1[r * C + c] * p[c];
-    t = fmaxf(t, 0.f);
-    z[r] = t;
-    z1[n * R + r] = t;
+    for (int c = lane; c < C; c += 64) t += w1[r * C + c] * p[c];
+    t = fmaxf(wave_sum(t), 0.f);
+    if (lane == 0) {
+      z[r] = t;
+      z1[n * R + r] = t;
+    }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
