@@ -437,3 +437,54 @@ def test_dgrad_odd_tiles(dtype, case):
     for o in outs:
         assert _rel(o, ref) < tol, _rel(o, ref)
     assert _rel(outs[0], outs[1]) < tol
+
+
+# reflect-pad data gradient: the zero-pad transposed conv over all pixels
+# (halo / LDS-DMA / register paths) plus the border-list fold GEMM that adds
+# the mirrored taps' gradient, against f64 autograd through F.pad(reflect) on
+# the same quantised operands; tiny images (every row a fold row), odd widths,
+# accumulate into an existing dx
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [
+    (48, 32, 3, 2, 32, 64, False),    # halo path (NC <= 64, 8x32 tiles)
+    (32, 8, 3, 2, 40, 64, False),     # disparity-head shape (K = 8)
+    (168, 128, 3, 2, 16, 32, False),  # 64x64 LDS-DMA tiles
+    (88, 64, 3, 2, 24, 40, True),     # 96-wide register tiles, accumulate
+    (64, 64, 3, 1, 3, 5, False),      # H = 3: rows 1 and H-2 coincide
+    (32, 16, 3, 1, 2, 7, True),       # H = 2: both rows fold
+    (320, 256, 3, 2, 8, 16, False),   # split-K
+])
+def test_dgrad_reflect(dtype, case):
+    from umamd import functional as U
+    from umamd._lib import PAD_REFLECT, lib
+    C, K, R, N, H, W, accumulate = case
+    pad = 1
+    g = torch.Generator().manual_seed(5)
+    w = (torch.rand(K, C, R, R, generator=g) - 0.5) * 0.2
+    dy = torch.randn(N, K, H, W, generator=g)
+    dx0 = torch.randn(N, C, H, W, generator=g) if accumulate else None
+    wq = w.to(dtype).double()
+    dyq = dy.to(dtype).double()
+    x = torch.zeros(N, C, H, W, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(F.pad(x, (pad,) * 4, mode='reflect'), wq)
+    y.backward(dyq)
+    ref = x.grad + (dx0.to(dtype).double() if accumulate else 0)
+    _, wT = U._pack(w.to(DEV), C, dtype, wf=False)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    # default plan, the halo kernel wherever it applies, then the one-pass
+    # fold and the split form forced
+    for hmin, snc in ((256, 64), (1, 64), (256, 0), (256, 4096)):
+        old = lib().um_set_tuning(b'halo_min_tiles', hmin)
+        old_s = lib().um_set_tuning(b'fold_split_nc', snc)
+        try:
+            dx = _nhwc(dx0).to(dtype).contiguous() if accumulate else None
+            out = U._conv_dgrad(_nhwc(dy).to(dtype), wT, (N, H, W, C), K, R, 1, pad, PAD_REFLECT,
+                                dx=dx, accumulate=accumulate)
+            torch.cuda.synchronize()
+        finally:
+            lib().um_set_tuning(b'halo_min_tiles', old)
+            lib().um_set_tuning(b'fold_split_nc', old_s)
+        err = _rel(_nchw(out), ref)
+        print(f'dgrad_reflect {case} {dtype} halo_min_tiles={hmin} fold_split_nc={snc}: '
+              f'rel {err:.3e}')
+        assert err < tol, err

@@ -70,7 +70,8 @@ def main():
             print(f'{ms * 1e3:8.1f} us  {name} splits={args[1]} K={args[2]} R={args[4]} C={args[5]}')
             continue
         tf = (work / (ms * 1e-3) / 1e12) if work else 0.0
-        print(f'{ms * 1e3:8.1f} us  {name[10:]:6s} N{N} {H}x{W} C{C} K{K} R{R} s{s}  '
+        pm = ' refl' if name != 'um_conv2d_wgrad' and args[13] == 1 else ''
+        print(f'{ms * 1e3:8.1f} us  {name[10:]:6s} N{N} {H}x{W} C{C} K{K} R{R} s{s}{pm}  '
               f'{tf:7.1f} TFLOP/s')
 
 

@@ -11,7 +11,10 @@ rows.sort(key=lambda r: int(r['Dispatch_Id']))
 name = [r['Kernel_Name'].replace('(anonymous namespace)::', '').replace('void ', '').split('(')[0]
         for r in rows]
 idx = [i for i, n in enumerate(name) if 'adam_kernel' in n]
-a, b = idx[-2] + 1, idx[-1] + 1
+# the last replayed bf16 step (the bench also runs an fp32 line after it)
+pairs = [(idx[j] + 1, idx[j + 1] + 1) for j in range(len(idx) - 1)]
+bf = [(x, y) for x, y in pairs if any('bfloat16' in name[i] for i in range(x, y))]
+a, b = (bf or pairs)[-1]
 tot = collections.defaultdict(lambda: [0, 0.0])
 t0, t1 = int(rows[a]['Start_Timestamp']), int(rows[b - 1]['End_Timestamp'])
 for i in range(a, b):

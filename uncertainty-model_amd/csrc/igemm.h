@@ -22,6 +22,12 @@ struct IgArgs {
   // of the wR x wR kernel; output row (n, i', j') -> pixel (2i'+ay, 2j'+ax) of
   // an outH x outW image
   int cls, wR, r0y, r0x, ay, ax, outH, outW;
+  // border-list mode (with IG_FOLD, reflect data gradient): GEMM row m is the
+  // m-th pixel of [on] x {pixels of an oh x ow image whose row is in rr[] or
+  // whose column is in rc[]} -- the pixels a reflect pad folds into -- and the
+  // gather sums only the folded sources (the zero-pad part comes from a plain
+  // same-size data gradient launched before it)
+  int border, nrr, nrc, rr[4], rc[4];
   // weights ("B"): row n (output channel) at b + n*ldb, element tap*ach + c
   const void* b;
   long ldb;
@@ -44,5 +50,14 @@ int igemm_stats_rows(int M, int NC);
 long igemm_ws_bytes(int dtype, int M, int NC, int taps, int ach);
 // launch; ws may be null (then no split)
 int igemm_run(int dtype, const IgArgs& a, float* ws, long ws_bytes, hipStream_t st);
+
+// reflect data gradients with more input channels than this run as one fold
+// pass, the others as a zero-pad pass + the border-list pass (knob
+// "fold_split_nc", UMAMD_FOLD_SPLIT_NC)
+int igemm_fold_split_nc();
+
+// fill the border-list fields of a (oh, ow, fold_pad set) and return the
+// number of listed pixels per image
+int igemm_border_list(IgArgs& a);
 
 }  // namespace umamd

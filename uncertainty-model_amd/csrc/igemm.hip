@@ -112,11 +112,48 @@ struct ARow {
   bool ok;
 };
 
-template <bool CLS>
+__device__ __forceinline__ int pick4(const int (&v)[4], int i) {
+  return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
+}
+
+// border-list mode: listed pixel m -> (n, y, x); rows rr[] (ascending) are
+// listed whole, the other rows at the columns rc[]
+__device__ __forceinline__ void border_pixel(const IgArgs& a, int m, int& n, int& y, int& x) {
+  const int W = a.ow, full = a.nrr * W;
+  const int per = full + (a.oh - a.nrr) * a.nrc;
+  n = m / per;
+  int k = m - n * per;
+  if (k < full) {
+    const int i = k / W;
+    y = pick4(a.rr, i);
+    x = k - i * W;
+    return;
+  }
+  k -= full;
+  const int idx = k / a.nrc;
+  x = pick4(a.rc, k - idx * a.nrc);
+  y = idx;  // the idx-th row not in rr[]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < a.nrr && pick4(a.rr, j) <= y) ++y;
+}
+
+// MODE: 0 plain rows, 1 parity class rows (stride-2 data gradient), 2 the
+// border list of the reflect fold (IgArgs::border)
+template <int MODE>
 __device__ __forceinline__ ARow decode_row(const IgArgs& a, int m) {
+  constexpr bool CLS = MODE == 1;
   ARow w;
   w.ok = m < a.M;
   const int mm = w.ok ? m : 0;
+  if constexpr (MODE == 2) {
+    int n, y, x;
+    border_pixel(a, mm, n, y, x);
+    w.base = (long)n * a.ah * a.aw * a.lda;
+    w.y0 = y - a.pad;
+    w.x0 = x - a.pad;
+    return w;
+  }
   const int hw = a.oh * a.ow;
   const int n = mm / hw;
   const int rem = mm - n * hw;
@@ -129,8 +166,14 @@ __device__ __forceinline__ ARow decode_row(const IgArgs& a, int m) {
 
 // element offset of output row m (class mode: the row (n, i', j') of parity
 // class (ay, ax) is output pixel (n, 2i'+ay, 2j'+ax) of the full image)
-template <bool CLS>
+template <int MODE>
 __device__ __forceinline__ long out_row(const IgArgs& a, int m) {
+  constexpr bool CLS = MODE == 1;
+  if constexpr (MODE == 2) {
+    int n, y, x;
+    border_pixel(a, m, n, y, x);
+    return (((long)n * a.oh + y) * a.ow + x) * a.ld_out;
+  }
   if (!CLS) return (long)m * a.ld_out;
   const int hw = a.oh * a.ow;
   const int n = m / hw, rem = m - n * hw;
@@ -138,9 +181,10 @@ __device__ __forceinline__ long out_row(const IgArgs& a, int m) {
   return (((long)n * a.outH + 2 * i + a.ay) * a.outW + 2 * j + a.ax) * a.ld_out;
 }
 
-template <bool CLS, typename T>
+template <int MODE, typename T>
 __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ src, const ARow& w,
                                        int r, int s, int c, Raw8<T>& out) {
+  constexpr bool CLS = MODE == 1, BRD = MODE == 2;
   raw_zero(out);
   if (!w.ok || c >= a.ach) return;
   int yy = CLS ? w.y0 - r : w.y0 + r, xx = CLS ? w.x0 - s : w.x0 + s;
@@ -163,7 +207,7 @@ __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ sr
   const bool lo_y = oy >= 1 && oy <= fp, hi_y = oy >= H - 1 - fp && oy <= H - 2;
   const bool lo_x = ox >= 1 && ox <= fp, hi_x = ox >= W - 1 - fp && ox <= W - 2;
   if (!(lo_y || hi_y || lo_x || hi_x)) {
-    if (iny && inx) raw_load8(src + w.base + ((long)yy * a.aw + xx) * a.lda + c, out);
+    if (iny && inx && !BRD) raw_load8(src + w.base + ((long)yy * a.aw + xx) * a.lda + c, out);
     return;
   }
   int ys[3], xs[3], ny = 0, nx = 0;
@@ -174,8 +218,13 @@ __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ sr
   if (lo_x) { const int t = -ox - a.pad + s; if (t >= 0 && t < a.aw) xs[nx++] = t; }
   if (hi_x) { const int t = 2 * (W - 1) - ox - a.pad + s; if (t >= 0 && t < a.aw) xs[nx++] = t; }
   float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // border-list mode: the plain (zero-pad) source was summed by the same-size
+  // data gradient already
+  const bool skip0 = BRD && iny && inx;
   for (int u = 0; u < ny; ++u)
-    for (int q = 0; q < nx; ++q) add8(src + w.base + ((long)ys[u] * a.aw + xs[q]) * a.lda + c, v);
+    for (int q = 0; q < nx; ++q)
+      if (!(skip0 && u == 0 && q == 0))
+        add8(src + w.base + ((long)ys[u] * a.aw + xs[q]) * a.lda + c, v);
   to_raw(v, out);
 }
 
@@ -186,7 +235,7 @@ __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ sr
 // staged there and leave as 16-byte rows (8 channels per lane) instead of
 // the MFMA layout's 2-byte column scatter -- the 1x1 convs and data
 // gradients are store-bound (dx at full resolution is 2/3 of their bytes).
-template <typename T, int BM, int BN, int WM, int WN, bool SPLIT, bool CLS>
+template <typename T, int BM, int BN, int WM, int WN, bool SPLIT, int MODE>
 __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restrict__ ws,
                                                f32x4_t (&acc)[BM / WM / 16][BN / WN / 16],
                                                int bm, int bn, float* sStatp, T* sOut) {
@@ -230,7 +279,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
         const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
         if (!nok || m >= a.M) continue;
         float v = acc[i][j][q] + bv;
-        const long off = out_row<CLS>(a, m) + n;
+        const long off = out_row<MODE>(a, m) + n;
         if (a.epilogue == UM_EPI_RESIDUAL)
           v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
         if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
@@ -287,7 +336,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
       const int r = c / CPR, c8 = (c - r * CPR) * 8;
       const int m = bm + r, n = bn + c8;
       if (m >= a.M || n >= a.NC) continue;
-      T* o = reinterpret_cast<T*>(a.out) + out_row<CLS>(a, m) + n;
+      T* o = reinterpret_cast<T*>(a.out) + out_row<MODE>(a, m) + n;
       if (a.accumulate) {
         float x[8], y[8];
         load8(&sOut[r * BN + c8], x);
@@ -304,9 +353,10 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
   }
 }
 
-template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT, bool CLS>
+template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT, int MODE>
 __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict__ ws,
                                                      int steps, int steps_per_split, int ntn) {
+  constexpr bool CLS = MODE == 1;
   using I = Img<T, BK>;
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
@@ -349,7 +399,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
     const int c = tid + i * 256;
     arow_i[i] = c / CPR;
     akc[i] = c % CPR;
-    arow[i] = decode_row<CLS>(a, bm + arow_i[i]);
+    arow[i] = decode_row<MODE>(a, bm + arow_i[i]);
   }
   int brow_i[B_PER], bkc[B_PER];
   bool bok[B_PER];
@@ -372,7 +422,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
   Raw8<T> ra[A_PER], rb[B_PER];
   auto load = [&]() {
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) gather<CLS>(a, asrc, arow[i], r, s, c0 + akc[i] * 8, ra[i]);
+    for (int i = 0; i < A_PER; ++i) gather<MODE>(a, asrc, arow[i], r, s, c0 + akc[i] * 8, ra[i]);
     const int btap = CLS ? (a.r0y + 2 * r) * a.wR + (a.r0x + 2 * s)
                          : (a.flip ? (a.R - 1 - r) * a.R + (a.R - 1 - s) : r * a.R + s);
     const long boff = (long)btap * a.ach;
@@ -436,7 +486,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
     __syncthreads();
   }
 
-  igemm_epilogue<T, BM, BN, WM, WN, SPLIT, CLS>(a, ws, acc, bm, bn, &sStat[0][0][0],
+  igemm_epilogue<T, BM, BN, WM, WN, SPLIT, MODE>(a, ws, acc, bm, bn, &sStat[0][0][0],
                                                BM * BN <= SMEM ? smem : nullptr);
 }
 
@@ -457,9 +507,10 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool CLS>
+template <int MODE>
 __device__ __forceinline__ const bf16_t* gather_ptr(const IgArgs& a, const bf16_t* src,
                                                      const ARow& w, int r, int s, int c) {
+  constexpr bool CLS = MODE == 1;
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_page);
   if (!w.ok || c >= a.ach) return zero;
   int yy = CLS ? w.y0 - r : w.y0 + r, xx = CLS ? w.x0 - s : w.x0 + s;
@@ -474,10 +525,12 @@ __device__ __forceinline__ const bf16_t* gather_ptr(const IgArgs& a, const bf16_
 
 // NW = 4 or 8 waves; with 8, a 64x64 tile gives each wave a 16x32 sub-tile
 // and every SIMD two waves of the block to overlap the per-step latencies.
-template <int BM, int BN, int NW, bool SPLIT, bool CLS>
+template <int BM, int BN, int NW, bool SPLIT, int MODE>
 __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __restrict__ ws,
                                                               int steps, int steps_per_split,
                                                               int ntn) {
+  constexpr bool CLS = MODE == 1;
+  static_assert(MODE != 2, "the reflect fold gathers through registers");
   constexpr int BK = 64, NST = 3, WM = NW == 8 ? 4 : 2, WN = 2;
   using I = Img<bf16_t, BK>;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
@@ -513,7 +566,7 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
   for (int i = 0; i < A_INS; ++i) {
     const int row = wave * (BM / NW) + i * 8 + lr;
     ac8[i] = lp ^ (row & 7);
-    arow[i] = decode_row<CLS>(a, bm + row);
+    arow[i] = decode_row<MODE>(a, bm + row);
   }
   int bc8[B_INS];
   long boff_row[B_INS];
@@ -540,7 +593,7 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
     bf16_t* base = smem + st * STAGE;
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
-      const bf16_t* g = gather_ptr<CLS>(a, asrc, arow[i], r, s, c0 + ac8[i] * 8);
+      const bf16_t* g = gather_ptr<MODE>(a, asrc, arow[i], r, s, c0 + ac8[i] * 8);
       __builtin_amdgcn_global_load_lds(
           g, (__attribute__((address_space(3))) void*)(base + (wave * (BM / NW) + i * 8) * BK), 16,
           0, 0);
@@ -607,7 +660,7 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
   __syncthreads();
   constexpr int STAT_ELEMS = (WM * BN * 2 * 4 + 15) / 16 * 8;  // bf16 elements, 16-B aligned
   static_assert(STAT_ELEMS + BM * BN <= NST * STAGE, "staged epilogue fits the staging LDS");
-  igemm_epilogue<bf16_t, BM, BN, WM, WN, SPLIT, CLS>(a, ws, acc, bm, bn,
+  igemm_epilogue<bf16_t, BM, BN, WM, WN, SPLIT, MODE>(a, ws, acc, bm, bn,
                                                      reinterpret_cast<float*>(smem),
                                                      smem + STAT_ELEMS);
   static_assert(WM * WN == NW, "waves");
@@ -616,7 +669,7 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
 // sum the split-K partials and apply the epilogue.  Block = a.stats_rows rows x
 // 64 columns: thread (g, lane) owns columns 4g..4g+3 and rows lane, lane+16, ...
 constexpr int EPI_COLS = 64;
-template <typename T, bool CLS>
+template <typename T, int MODE>
 __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const float* __restrict__ ws,
                                                                int splits) {
   __shared__ float red[16][16][8];
@@ -651,7 +704,7 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const fl
         if (a.epilogue == UM_EPI_RESIDUAL)
           v[e] += to_f32(reinterpret_cast<const T*>(a.residual)[m * a.ldr + n + e]);
         if (a.epilogue == UM_EPI_SIGMOID_SCALE) v[e] = a.epi_scale * sigmoidf_(v[e]);
-        const long off = out_row<CLS>(a, (int)m) + n + e;
+        const long off = out_row<MODE>(a, (int)m) + n + e;
         if (a.out_f32) {
           float* o = reinterpret_cast<float*>(a.out) + off;
           if (a.accumulate) v[e] += *o;
@@ -689,6 +742,7 @@ struct Knobs {
   int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles, odd_bn, bk64;
   int glds_split_below, glds_split_target;
   int glds;
+  int fold_split_nc;
   Knobs() {
     auto env = [](const char* n, int d) {
       const char* v = getenv(n);
@@ -720,6 +774,10 @@ struct Knobs {
     // 0 -> 653.6, 7 -> 654.8, 5 -> 661.3 pairs/s (the 128-row tiles keep the
     // register path: 3 LDS stages of 128-row tiles leave 1 block per CU)
     glds = env("UMAMD_IG_GLDS", 5);
+    // per conv (tools/conv_table.py): split form 256x512 C48 171 -> 117 us,
+    // C32 K8 125 -> 85; one pass stays ahead from C = 128 up (16x32 C640:
+    // 106 vs 140, 8x16 C512: 53 vs 79)
+    fold_split_nc = env("UMAMD_FOLD_SPLIT_NC", 64);
   }
 };
 Knobs& knobs() {
@@ -735,6 +793,8 @@ bool small_tiles(int M, int NC) {
   const Knobs& k = knobs();
   return k.small && NC > 64 && (long)ceil_div(M, 128) * ceil_div(NC, 128) < k.small_tiles;
 }
+
+void split_plan(Plan& p, int M, int NC, int taps, int ach, long ws_bytes, bool glds);
 
 // glds: the launch will take the LDS-DMA loop (its split thresholds); the
 // workspace query passes false, whose split counts bound the LDS-DMA ones
@@ -762,6 +822,12 @@ Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes, bool 
     }
     if (dtype == UM_BF16 && ach % 64 == 0 && (kn.bk64 & 2)) p.bk = 64;  // 64-83 KB of LDS: 1-2 blocks/CU
   }
+  split_plan(p, M, NC, taps, ach, ws_bytes, glds);
+  return p;
+}
+
+void split_plan(Plan& p, int M, int NC, int taps, int ach, long ws_bytes, bool glds) {
+  const Knobs& kn = knobs();
   p.steps = taps * ((ach + p.bk - 1) / p.bk);
   // Split grids that leave CUs with too few blocks to hide load latency: the
   // partials cost an f32 write + read of splits*M*NC (about 1 us per 8 MB
@@ -780,29 +846,28 @@ Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes, bool 
   }
   p.per = ceil_div(p.steps, p.splits);
   p.splits = ceil_div(p.steps, p.per);  // no empty splits
-  return p;
 }
 
-template <typename T, int BK, int BM, int BN, int WM, int WN, bool CLS>
+template <typename T, int BK, int BM, int BN, int WM, int WN, int MODE>
 int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
   const int ntm = ceil_div(a.M, BM), ntn = ceil_div(a.NC, BN);
-  if constexpr (sizeof(T) == 2 && BK == 64 && WM == 2 && WN == 2) {
+  if constexpr (sizeof(T) == 2 && BK == 64 && WM == 2 && WN == 2 && MODE != 2) {
     if (a.pmode != umamd::IG_FOLD && (knobs().glds & (BM == 64 ? 1 : 2))) {
       const bool w8 = BM == 64 && (knobs().glds & 4);
       if (w8 && p.splits > 1)
-        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, true, CLS>), dim3(ntm * ntn, 1, p.splits),
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, true, MODE>), dim3(ntm * ntn, 1, p.splits),
                            dim3(512), 0, st, a, ws, p.steps, p.per, ntn);
       else if (w8)
-        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, false, CLS>), dim3(ntm * ntn, 1, 1),
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, false, MODE>), dim3(ntm * ntn, 1, 1),
                            dim3(512), 0, st, a, ws, p.steps, p.per, ntn);
       else if (p.splits > 1)
-        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, true, CLS>), dim3(ntm * ntn, 1, p.splits),
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, true, MODE>), dim3(ntm * ntn, 1, p.splits),
                            dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
       else
-        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, false, CLS>), dim3(ntm * ntn, 1, 1),
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, false, MODE>), dim3(ntm * ntn, 1, 1),
                            dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
       if (p.splits > 1)
-        hipLaunchKernelGGL((splitk_epilogue_kernel<T, CLS>),
+        hipLaunchKernelGGL((splitk_epilogue_kernel<T, MODE>),
                            dim3(ceil_div(a.M, a.stats_rows), ceil_div(a.NC, EPI_COLS)), dim3(256), 0,
                            st, a, (const float*)ws, p.splits);
       UM_LAUNCH_CHECK();
@@ -810,13 +875,13 @@ int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
     }
   }
   if (p.splits > 1) {
-    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, true, CLS>),
+    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, true, MODE>),
                        dim3(ntm * ntn, 1, p.splits), dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
-    hipLaunchKernelGGL((splitk_epilogue_kernel<T, CLS>),
+    hipLaunchKernelGGL((splitk_epilogue_kernel<T, MODE>),
                        dim3(ceil_div(a.M, a.stats_rows), ceil_div(a.NC, EPI_COLS)), dim3(256), 0, st,
                        a, (const float*)ws, p.splits);
   } else {
-    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, false, CLS>), dim3(ntm * ntn, 1, 1),
+    hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, false, MODE>), dim3(ntm * ntn, 1, 1),
                        dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
   }
   UM_LAUNCH_CHECK();
@@ -825,8 +890,8 @@ int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
 
 template <typename T, int BK, int BM, int BN, int WM, int WN>
 int launch(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
-  return a.cls ? launch_cls<T, BK, BM, BN, WM, WN, true>(a, p, ws, st)
-               : launch_cls<T, BK, BM, BN, WM, WN, false>(a, p, ws, st);
+  return a.cls ? launch_cls<T, BK, BM, BN, WM, WN, 1>(a, p, ws, st)
+               : launch_cls<T, BK, BM, BN, WM, WN, 0>(a, p, ws, st);
 }
 
 template <typename T>
@@ -859,6 +924,20 @@ int dispatch_tiles(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
 
 namespace umamd {
 
+int igemm_fold_split_nc() { return knobs().fold_split_nc; }
+
+int igemm_border_list(IgArgs& a) {
+  const int H = a.oh, W = a.ow, p = a.fold_pad;
+  auto receives = [p](int i, int n) { return (i >= 1 && i <= p) || (i >= n - 1 - p && i <= n - 2); };
+  a.border = 1;
+  a.nrr = a.nrc = 0;
+  for (int i = 0; i < H && a.nrr < 4; ++i)
+    if (receives(i, H)) a.rr[a.nrr++] = i;
+  for (int j = 0; j < W && a.nrc < 4; ++j)
+    if (receives(j, W)) a.rc[a.nrc++] = j;
+  return a.nrr * W + (H - a.nrr) * a.nrc;
+}
+
 long igemm_ws_bytes(int dtype, int M, int NC, int taps, int ach) {
   const Plan p = make_plan(dtype, M, NC, taps, ach, -1, false);
   return p.splits > 1 ? (long)p.splits * M * NC * 4 : 0;
@@ -870,6 +949,14 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   if (a_in.M == 0) return UM_OK;
   IgArgs a = a_in;
   a.stats_rows = igemm_stats_rows(a.M, a.NC);
+  if (a.border) {
+    // the reflect fold's border list: a few thousand rows, one small plan
+    Plan p{};
+    p.bk = 32; p.bm = 64; p.bn = 64; p.wm = 2; p.wn = 2;
+    split_plan(p, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0, false);
+    if (dtype == UM_BF16) return launch_cls<bf16_t, 32, 64, 64, 2, 2, 2>(a, p, ws, st);
+    return launch_cls<float, 32, 64, 64, 2, 2, 2>(a, p, ws, st);
+  }
   if (knobs().halo && halo_applicable(dtype, a, knobs().halo_min_tiles)) return halo_run(a, st);
   // the LDS-DMA loop serves the bf16 64x64 tiles without the reflect fold
   Plan p = make_plan(dtype, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0, false);
@@ -898,6 +985,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "odd_bn")) f = &k.odd_bn;
   else if (!strcmp(key, "bk64")) f = &k.bk64;
   else if (!strcmp(key, "glds")) f = &k.glds;
+  else if (!strcmp(key, "fold_split_nc")) f = &k.fold_split_nc;
   if (!f) return -1;
   const int old = *f;
   *f = value;
