@@ -37,8 +37,13 @@ enum {
   UM_EPI_NONE = 0,           /* y = acc (+ bias)                               */
   UM_EPI_STATS = 1,          /* y = acc + bias, per-block BN partial sums      */
   UM_EPI_SIGMOID_SCALE = 2,  /* y(f32) = scale * sigmoid(acc + bias)           */
-  UM_EPI_RESIDUAL = 3        /* y = acc + bias + residual                      */
+  UM_EPI_RESIDUAL = 3,       /* y = acc + bias + residual                      */
+  UM_EPI_STAT_SLOTS = 4      /* y = acc + bias, BN sums f64-atomically added into
+                                stats_partials viewed as double[UM_STAT_SLOTS][K][2]
+                                (zeroed by the caller; see um_bn_elu_fwd_slots)  */
 };
+/* f64 slots of the atomic BN statistics (UM_EPI_STAT_SLOTS, *_slots entries) */
+#define UM_STAT_SLOTS 16
 
 const char* um_last_error(void);
 int um_version(void);
@@ -56,7 +61,9 @@ int um_set_tuning(const char* key, int value);
  *   attention 1x1 K/Q/V/reprojection: reference model/layers/attention.py:37-40,66-76
  * Implicit GEMM on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32).
  */
-/* number of BN partial rows written by um_conv2d_fwd with UM_EPI_STATS for M output pixels and K channels */
+/* number of BN partial rows written by um_conv2d_fwd with UM_EPI_STATS for M
+ * output pixels and K channels (UM_EPI_STAT_SLOTS writes UM_STAT_SLOTS f64 rows
+ * instead, through the same stats_partials pointer) */
 int um_conv_stats_parts(int M, int K);
 
 /* split-K workspace (bytes) the kernels want for a shape; 0 = no split.
@@ -176,6 +183,33 @@ int um_bn_fwd_pool_parts(long M, long HW);
 int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
                   const float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
                   hipStream_t stream);
+/* Single-process BN with the statistics in f64 slots (no reduction launch):
+ * the conv ran with UM_EPI_STAT_SLOTS into `slots` ([UM_STAT_SLOTS][C][2],
+ * count = M elements per channel); every workgroup sums the slots and
+ * derives scale/shift itself, workgroup 0 also writes mean/invstd/scale/shift
+ * (kept for the backward) and updates the running statistics -- the
+ * semantics of um_bn_stats_coeffs + um_bn_elu_fwd in one launch. */
+int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const double* slots,
+                        double count, const float* gamma, const float* beta, float eps,
+                        float momentum, float* running_mean, float* running_var,
+                        long long* num_batches_tracked, float* mean, float* invstd, float* scale,
+                        float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
+                        hipStream_t stream);
+/* backward sums (sum dz, sum dz*xhat) added into zeroed f64 slots
+ * [UM_STAT_SLOTS][C][2] instead of partial rows */
+int um_bn_elu_bwd_reduce_slots(int dtype, long M, int C, long HW, const void* da, int ldda,
+                               const void* y, int ldy, const float* mean, const float* invstd,
+                               const float* scale, const float* shift, const float* add_nc,
+                               int apply_elu, double* slots, hipStream_t stream);
+/* dy from the slot sums: every workgroup derives k1..k3 (as
+ * um_bn_bwd_stats_coeffs), workgroup 0 writes dgamma, dbeta and the
+ * closed-form conv-bias gradient dbias (each optional) */
+int um_bn_elu_bwd_apply_slots(int dtype, long M, int C, long HW, const void* da, int ldda,
+                              const void* y, int ldy, const float* mean, const float* invstd,
+                              const float* scale, const float* shift, const float* add_nc,
+                              int apply_elu, const double* slots, double count,
+                              const float* gamma, float* dgamma, float* dbeta, float* dbias,
+                              void* dy, int lddy, hipStream_t stream);
 int um_bn_bwd_parts(long M);
 int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int ldda,
                          const void* y, int ldy, const float* mean, const float* invstd,

@@ -76,7 +76,23 @@ def test_conv_bn_elu_halo(case):
 
 @pytest.mark.parametrize('case', CONV_CASES)
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
-def test_conv_bn_elu(case, dtype):
+def test_conv_bn_elu_slots(case, dtype):
+    """BN statistics as f64 atomics into slots (the model-forward path):
+    same bars as the partial-row reductions, with the halo kernel forced on
+    for bf16 so its slot epilogue is covered too"""
+    from umamd import functional as U
+    from umamd._lib import lib
+    old = lib().um_set_tuning(b'halo_min_tiles', 1)
+    try:
+        test_conv_bn_elu(case, dtype, arena=U.StatArena())
+    finally:
+        lib().um_set_tuning(b'halo_min_tiles', old)
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_conv_bn_elu(case, dtype, arena=None):
+    import contextlib
     from umamd import functional as U
     from umamd._lib import PAD_REFLECT, PAD_ZERO
     Cin, Cout, k, stride, mode, H, W = case
@@ -100,7 +116,8 @@ def test_conv_bn_elu(case, dtype):
     # HIP
     cd, bd = conv.to(DEV), bn.to(DEV)
     xd = _nhwc(x).to(dtype).requires_grad_(True)
-    yd = U.conv_bn_elu(xd, cd, bd, pad, PAD_REFLECT if mode == 'reflect' else PAD_ZERO)
+    with U.stat_scope(arena, DEV) if arena is not None else contextlib.nullcontext():
+        yd = U.conv_bn_elu(xd, cd, bd, pad, PAD_REFLECT if mode == 'reflect' else PAD_ZERO)
     (yd.float() * _nhwc(g)).sum().backward()
     tol = 1e-4 if dtype == torch.float32 else 5e-2
     assert _rel(_nchw(yd), yr) < tol

@@ -52,16 +52,64 @@ __global__ void coeffs_kernel(const double* __restrict__ st, double count, int C
 // pool (optional): per-block channel sums of the stored a, [blocks][C] --
 // the SE squeeze of reference decoder.py:124-136 (a block's rows lie in one
 // image: rows_per_block divides HW), finished by um_se_mlp_fwd.
+// Forward coefficients from the f64 statistics slots (UM_EPI_STAT_SLOTS):
+// every workgroup derives scale/shift for all C channels into LDS from the
+// same slot sums (so all of them agree bit for bit), workgroup 0 also
+// publishes mean/invstd/scale/shift and updates the running statistics --
+// the COLRED_BN_FWD finish of reduce.hip without its launch.
+struct FwdFin {
+  const double* slots;  // null: scale/shift are given
+  double count;
+  const float *gamma, *beta;
+  float eps, momentum;
+  float *running_mean, *running_var;
+  long long* nbt;
+  float *mean, *invstd, *scale, *shift;
+};
+
+__device__ __forceinline__ void fwd_fin_coeffs(const FwdFin& f, int C, float* s_sc, float* s_sh) {
+  const bool pub = blockIdx.x == 0;
+  stat_slots_finish(f.slots, C, [&](int c, double s0, double s1) {
+    const double mean = s0 / f.count;
+    double var = s1 / f.count - mean * mean;
+    if (var < 0) var = 0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+    const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
+    const float sc = g * invstd, sh = b - (float)mean * g * invstd;
+    s_sc[c] = sc;
+    s_sh[c] = sh;
+    if (pub) {
+      f.mean[c] = (float)mean;
+      f.invstd[c] = invstd;
+      f.scale[c] = sc;
+      f.shift[c] = sh;
+      if (f.running_mean != nullptr) {
+        const double unb = f.count > 1 ? var * f.count / (f.count - 1) : var;
+        f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
+        f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unb;
+      }
+    }
+  });
+  if (pub && threadIdx.x == 0 && f.nbt != nullptr) *f.nbt += 1;
+  __syncthreads();
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
     const float* __restrict__ y, int ldy, long M, int C, const float* __restrict__ scale,
     const float* __restrict__ shift, T* __restrict__ a, int lda, int apply_elu,
-    int rows_per_block, float* __restrict__ pool) {
-  extern __shared__ float red[];  // [256][8] when pooling
+    int rows_per_block, float* __restrict__ pool, FwdFin fin) {
+  extern __shared__ float red[];  // [256][8] when pooling, then [2][C] coefficients (fin)
   const int cg = C / 8;
   const RowMap rm(cg);
   const long m0 = (long)blockIdx.x * rows_per_block;
   const long m1 = min(M, m0 + rows_per_block);
+  if (fin.slots != nullptr) {
+    float* s_sc = red + (pool ? 256 * 8 : 0);
+    fwd_fin_coeffs(fin, C, s_sc, s_sc + C);
+    scale = s_sc;
+    shift = s_sc + C;
+  }
   for (int g0 = 0; g0 < cg; g0 += rm.G) {
     const int g = g0 + rm.g;
     float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -70,10 +118,7 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
       float sc[8], sh[8];
       load8(scale + c, sc);
       load8(shift + c, sh);
-#pragma unroll 4
-      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
-        float v[8];
-        load8(y + m * ldy + c, v);
+      auto row = [&](long m, float* v) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float z = v[e] * sc[e] + sh[e];
@@ -86,6 +131,12 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
 #pragma unroll
           for (int e = 0; e < 8; ++e) ps[e] += r[e];
         }
+      };
+#pragma unroll 4
+      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+        float v[8];
+        load8(y + m * ldy + c, v);
+        row(m, v);
       }
     }
     if (pool) {
@@ -211,7 +262,7 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
     long HW, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ add_nc, int apply_elu, float* __restrict__ parts,
-    int rows_per_block, BwdFin fin) {
+    int rows_per_block, BwdFin fin, double* __restrict__ slots) {
   extern __shared__ float red[];  // [256][16]
   const int cg = C / 8;
   const RowMap rm(cg);
@@ -248,12 +299,25 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
       }
     }
     lane_reduce<16>(red, rm, acc);
-    if (rm.lane == 0 && g < cg) {
-      float* o = parts + ((long)blockIdx.x * C + g * 8) * 2;
+    if (slots != nullptr) {  // stage [8G channels][2] in LDS, then contiguous f64 atomics
+      if (rm.lane == 0 && g < cg)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        o[2 * e] = acc[e];
-        o[2 * e + 1] = acc[8 + e];
+        for (int e = 0; e < 8; ++e) {
+          red[(rm.g * 8 + e) * 2] = acc[e];
+          red[(rm.g * 8 + e) * 2 + 1] = acc[8 + e];
+        }
+      __syncthreads();
+      stat_slots_add_row(slots, blockIdx.x, C, g0 * 8, min(rm.G * 8, C - g0 * 8),
+                         [&](int i) { return red[i]; });
+      __syncthreads();
+    } else if (rm.lane == 0 && g < cg) {
+      {
+        float* o = parts + ((long)blockIdx.x * C + g * 8) * 2;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[2 * e] = acc[e];
+          o[2 * e + 1] = acc[8 + e];
+        }
       }
     }
   }
@@ -286,6 +350,36 @@ __global__ void bwd_coeffs_kernel(const double* __restrict__ st, double count, i
   if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)sl[2 * c];
 }
 
+// Backward coefficients from the f64 slots of bn_elu_bwd_reduce (as
+// COLRED_BN_BWD in reduce.hip): every workgroup derives k1..k3 into LDS,
+// workgroup 0 writes dgamma, dbeta and the closed-form conv-bias gradient.
+struct ApplyFin {
+  const double* slots;  // null: k1..k3 are given
+  double count;
+  const float* gamma;
+  float *dgamma, *dbeta, *dbias;
+};
+
+__device__ __forceinline__ void apply_fin_coeffs(const ApplyFin& f, int C,
+                                                 const float* __restrict__ invstd, float* s_k1,
+                                                 float* s_k2, float* s_k3) {
+  const bool pub = blockIdx.x == 0;
+  stat_slots_finish(f.slots, C, [&](int c, double s0, double s1) {
+    const float g = f.gamma ? f.gamma[c] : 1.f;
+    const float a1 = g * invstd[c], a2 = (float)(s0 / f.count);
+    s_k1[c] = a1;
+    s_k2[c] = a2;
+    s_k3[c] = (float)(s1 / f.count);
+    if (pub) {
+      if (f.dgamma) f.dgamma[c] = (float)s1;
+      if (f.dbeta) f.dbeta[c] = (float)s0;
+      // conv-bias gradient sum_m dy = k1 (s0 - n k2 - k3 sum xhat), sum xhat = 0
+      if (f.dbias) f.dbias[c] = a1 * (float)(s0 - f.count * (double)a2);
+    }
+  });
+  __syncthreads();
+}
+
 // dy = k1*(dz - k2 - xhat*k3); optional per-block partial sums of dy
 // ([blk][C], the conv-bias gradient) written to sum_parts.
 template <typename T>
@@ -295,12 +389,19 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ add_nc, int apply_elu, const float* __restrict__ k1,
     const float* __restrict__ k2, const float* __restrict__ k3, T* __restrict__ dy, int lddy,
-    float* __restrict__ sum_parts, int rows_per_block) {
-  extern __shared__ float red[];  // [256][8]
+    float* __restrict__ sum_parts, int rows_per_block, ApplyFin fin) {
+  extern __shared__ float red[];  // [256][8], then [3][C] coefficients (fin)
   const int cg = C / 8;
   const RowMap rm(cg);
   const long m0 = (long)blockIdx.x * rows_per_block;
   const long m1 = min(M, m0 + rows_per_block);
+  if (fin.slots != nullptr) {
+    float* s_k = red + 256 * 8;
+    apply_fin_coeffs(fin, C, invstd, s_k, s_k + C, s_k + 2 * C);
+    k1 = s_k;
+    k2 = s_k + C;
+    k3 = s_k + 2 * C;
+  }
   for (int g0 = 0; g0 < cg; g0 += rm.G) {
     const int g = g0 + rm.g;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -324,11 +425,8 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
           D[e] = -a1[e] * a2[e] + a1[e] * a3[e] * mu[e] * is[e];
         }
       }
-#pragma unroll 4
-      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
-        float dv[8], yv[8], ad[8], o[8];
-        load8(da + m * ldda + c, dv);
-        load8(y + m * ldy + c, yv);
+      auto row = [&](long m, const float* dv, const float* yv) {
+        float ad[8], o[8];
         if (add_nc) load8(add_nc + (m / HW) * C + c, ad);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -346,6 +444,13 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
 #pragma unroll
           for (int e = 0; e < 8; ++e) acc[e] += r[e];
         }
+      };
+#pragma unroll 4
+      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+        float dv[8], yv[8];
+        load8(da + m * ldda + c, dv);
+        load8(y + m * ldy + c, yv);
+        row(m, dv, yv);
       }
     }
     if (sum_parts) {
@@ -374,22 +479,47 @@ int um_bn_fwd_pool_parts(long M, long HW) {
   return HW > 0 && M % HW == 0 ? (int)(M / fwd_rows(M, HW)) : 0;
 }
 
-int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
-                  const float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
-                  hipStream_t st) {
+static int bn_fwd_launch(int dtype, long M, int C, const void* y, int ldy, const float* scale,
+                         const float* shift, void* a, int lda, int apply_elu, long HW,
+                         float* pool_parts, const FwdFin& fin, hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0 && ldy % 8 == 0 && lda % 8 == 0, "um_bn_elu_fwd: C/ld not multiple of 8");
   UM_CHECK_ARG(pool_parts == nullptr || (HW > 0 && M % HW == 0), "um_bn_elu_fwd: HW");
   const int rows = fwd_rows(M, pool_parts ? HW : 0);
   const int g = ceil_div(M, rows);
-  const size_t shm = pool_parts ? 256 * 8 * sizeof(float) : 0;
+  const size_t shm = (pool_parts ? 256 * 8 * sizeof(float) : 0) +
+                     (fin.slots ? 2 * (size_t)C * sizeof(float) : 0);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, dim3(g), dim3(256), shm, st, (const float*)y,
-                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu, rows, pool_parts);
+                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu, rows, pool_parts, fin);
   else
     hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, dim3(g), dim3(256), shm, st, (const float*)y,
-                       ldy, M, C, scale, shift, (float*)a, lda, apply_elu, rows, pool_parts);
+                       ldy, M, C, scale, shift, (float*)a, lda, apply_elu, rows, pool_parts, fin);
   UM_LAUNCH_CHECK();
   return UM_OK;
+}
+
+int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
+                  const float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
+                  hipStream_t st) {
+  FwdFin fin{};
+  return bn_fwd_launch(dtype, M, C, y, ldy, scale, shift, a, lda, apply_elu, HW, pool_parts, fin, st);
+}
+
+int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const double* slots,
+                        double count, const float* gamma, const float* beta, float eps,
+                        float momentum, float* running_mean, float* running_var,
+                        long long* num_batches_tracked, float* mean, float* invstd, float* scale,
+                        float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
+                        hipStream_t st) {
+  UM_CHECK_ARG(slots != nullptr && count > 0 && mean && invstd && scale && shift,
+               "um_bn_elu_fwd_slots: slots / count / coefficient outputs");
+  FwdFin fin{};
+  fin.slots = slots; fin.count = count; fin.gamma = gamma; fin.beta = beta;
+  fin.eps = eps; fin.momentum = momentum;
+  fin.running_mean = running_mean; fin.running_var = running_var; fin.nbt = num_batches_tracked;
+  fin.mean = mean; fin.invstd = invstd; fin.scale = scale; fin.shift = shift;
+  return bn_fwd_launch(dtype, M, C, y, ldy, nullptr, nullptr, a, lda, apply_elu, HW, pool_parts,
+                       fin, st);
 }
 
 int um_bn_bwd_parts(long M) { return parts_for(M); }
@@ -397,18 +527,19 @@ int um_bn_bwd_parts(long M) { return parts_for(M); }
 static int bwd_reduce_launch(int dtype, long M, int C, long HW, const void* da, int ldda,
                              const void* y, int ldy, const float* mean, const float* invstd,
                              const float* scale, const float* shift, const float* add_nc,
-                             int apply_elu, float* parts, const BwdFin& fin, hipStream_t st) {
+                             int apply_elu, float* parts, const BwdFin& fin, double* slots,
+                             hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_reduce: C %% 8");
   const int blocks = um_bn_bwd_parts(M);
   const size_t shm = 256 * 16 * sizeof(float);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
                        (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M), fin);
+                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M), fin, slots);
   else
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), shm, st,
                        (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M), fin);
+                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M), fin, slots);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -419,7 +550,17 @@ int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int 
                          int apply_elu, float* parts, hipStream_t st) {
   BwdFin fin{};
   return bwd_reduce_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
-                           apply_elu, parts, fin, st);
+                           apply_elu, parts, fin, nullptr, st);
+}
+
+int um_bn_elu_bwd_reduce_slots(int dtype, long M, int C, long HW, const void* da, int ldda,
+                               const void* y, int ldy, const float* mean, const float* invstd,
+                               const float* scale, const float* shift, const float* add_nc,
+                               int apply_elu, double* slots, hipStream_t st) {
+  UM_CHECK_ARG(slots != nullptr, "um_bn_elu_bwd_reduce_slots: slots");
+  BwdFin fin{};
+  return bwd_reduce_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
+                           apply_elu, nullptr, fin, slots, st);
 }
 
 long um_bn_bwd_fin_ws(long M, int C) {
@@ -443,7 +584,7 @@ int um_bn_elu_bwd_reduce_coeffs(int dtype, long M, int C, long HW, const void* d
   fin.dgamma = dgamma; fin.dbeta = dbeta; fin.dbias = dbias;
   fin.k1 = k1; fin.k2 = k2; fin.k3 = k3;
   return bwd_reduce_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
-                           apply_elu, parts, fin, st);
+                           apply_elu, parts, fin, nullptr, st);
 }
 
 int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamma,
@@ -457,26 +598,51 @@ int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamm
   return UM_OK;
 }
 
+static int bwd_apply_launch(int dtype, long M, int C, long HW, const void* da, int ldda,
+                            const void* y, int ldy, const float* mean, const float* invstd,
+                            const float* scale, const float* shift, const float* add_nc,
+                            int apply_elu, const float* k1, const float* k2, const float* k3,
+                            void* dy, int lddy, float* sum_parts, const ApplyFin& fin,
+                            hipStream_t st) {
+  UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_apply: C %% 8");
+  const int blocks = um_bn_bwd_parts(M);
+  const size_t shm = 256 * 8 * sizeof(float) + (fin.slots ? 3 * (size_t)C * sizeof(float) : 0);
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
+                       (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
+                       scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy, sum_parts,
+                       rows_per_part(M), fin);
+  else
+    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, dim3(blocks), dim3(256), shm, st,
+                       (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
+                       scale, shift, add_nc, apply_elu, k1, k2, k3, (float*)dy, lddy, sum_parts,
+                       rows_per_part(M), fin);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
 int um_bn_elu_bwd_apply(int dtype, long M, int C, long HW, const void* da, int ldda,
                         const void* y, int ldy, const float* mean, const float* invstd,
                         const float* scale, const float* shift, const float* add_nc,
                         int apply_elu, const float* k1, const float* k2, const float* k3,
                         void* dy, int lddy, float* sum_parts, hipStream_t st) {
-  UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_apply: C %% 8");
-  const int blocks = um_bn_bwd_parts(M);
-  const size_t shm = 256 * 8 * sizeof(float);
-  if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
-                       (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy, sum_parts,
-                       rows_per_part(M));
-  else
-    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, dim3(blocks), dim3(256), shm, st,
-                       (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, k1, k2, k3, (float*)dy, lddy, sum_parts,
-                       rows_per_part(M));
-  UM_LAUNCH_CHECK();
-  return UM_OK;
+  ApplyFin fin{};
+  return bwd_apply_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
+                          apply_elu, k1, k2, k3, dy, lddy, sum_parts, fin, st);
+}
+
+int um_bn_elu_bwd_apply_slots(int dtype, long M, int C, long HW, const void* da, int ldda,
+                              const void* y, int ldy, const float* mean, const float* invstd,
+                              const float* scale, const float* shift, const float* add_nc,
+                              int apply_elu, const double* slots, double count,
+                              const float* gamma, float* dgamma, float* dbeta, float* dbias,
+                              void* dy, int lddy, hipStream_t st) {
+  UM_CHECK_ARG(slots != nullptr && count > 0, "um_bn_elu_bwd_apply_slots: slots / count");
+  ApplyFin fin{};
+  fin.slots = slots; fin.count = count; fin.gamma = gamma;
+  fin.dgamma = dgamma; fin.dbeta = dbeta; fin.dbias = dbias;
+  return bwd_apply_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
+                          apply_elu, nullptr, nullptr, nullptr, dy, lddy, nullptr, fin, st);
 }
 
 }  // extern "C"

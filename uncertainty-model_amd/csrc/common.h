@@ -190,6 +190,73 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// ------------------------------------------------- BN statistics slots --
+// Per-channel (sum, sum of squares) accumulated straight into f64 "slots"
+// [UM_STAT_SLOTS][C][2] (zeroed by the caller) by no-return f64 atomics: the
+// producer of row block b adds into slot b % UM_STAT_SLOTS, so at most
+// blocks/16 adders meet on one address (the atomics run at the memory side,
+// MI355X_MICROARCH.md "Global float atomics"), and the consumer sums the 16
+// slots -- no partial-row array and no separate reduction launch.
+__device__ __forceinline__ void stat_slot_add(double* slots, long row_block, int C, int c,
+                                              float s0, float s1) {
+  double* p = slots + ((row_block % UM_STAT_SLOTS) * C + c) * 2;
+  unsafeAtomicAdd(p, (double)s0);
+  unsafeAtomicAdd(p + 1, (double)s1);
+}
+
+// Block-wide form: the sums of channels [c0, c0 + ncols) of one row block,
+// val(i) = value i = 2*col + v (v = 0 sum, 1 sum of squares), one atomic per
+// thread on consecutive doubles -- a wave covers 512 contiguous bytes instead
+// of one scattered 8-byte request per lane.
+template <class F>
+__device__ __forceinline__ void stat_slots_add_row(double* slots, long row_block, int C, int c0,
+                                                   int ncols, F val) {
+  double* p = slots + ((row_block % UM_STAT_SLOTS) * C + c0) * 2;
+  for (int i = threadIdx.x; i < 2 * ncols; i += blockDim.x) unsafeAtomicAdd(p + i, (double)val(i));
+}
+
+// Block-wide finish over all C channels: fin(c, s0, s1) is called once per
+// channel with the f64 slot sums.  SPL lanes share a channel (each sums every
+// SPL-th slot with 16-byte loads, all issued before the first add, then a
+// shuffle tree), so a block reads the 16 x C x 16 bytes in one round trip
+// for C <= 256; the fixed order makes every block's sums identical.  Must be
+// reached by all threads of the block.
+template <int SPL, class F>
+__device__ __forceinline__ void stat_slots_finish_t(const double* __restrict__ slots, int C, F fin) {
+  constexpr int PER = UM_STAT_SLOTS / SPL;
+  const int total = C * SPL;
+  for (int base = 0; base < total; base += blockDim.x) {
+    const int idx = base + threadIdx.x;
+    const int c = idx / SPL, part = idx % SPL;
+    double2 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      v[k] = c < C ? *reinterpret_cast<const double2*>(slots + ((long)(part + k * SPL) * C + c) * 2)
+                   : make_double2(0.0, 0.0);
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      s0 += v[k].x;
+      s1 += v[k].y;
+    }
+#pragma unroll
+    for (int o = SPL >> 1; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o, 64);
+      s1 += __shfl_xor(s1, o, 64);
+    }
+    if (c < C && part == 0) fin(c, s0, s1);
+  }
+}
+
+template <class F>
+__device__ __forceinline__ void stat_slots_finish(const double* __restrict__ slots, int C, F fin) {
+  const int nt = blockDim.x;
+  if (16 * C <= nt) stat_slots_finish_t<16>(slots, C, fin);
+  else if (8 * C <= nt) stat_slots_finish_t<8>(slots, C, fin);
+  else if (4 * C <= nt) stat_slots_finish_t<4>(slots, C, fin);
+  else stat_slots_finish_t<2>(slots, C, fin);
+}
+
 // rows per block of the row-chunk reductions (RowMap kernels): aim at about
 // 512 blocks (16..1024 rows): small deep layers still fill the chip and the
 // full-resolution layers do not write thousands of partial rows

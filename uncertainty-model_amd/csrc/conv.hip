@@ -585,7 +585,8 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
   UM_CHECK_ARG(P == (H + 2 * pad - R) / stride + 1 && Q == (W + 2 * pad - R) / stride + 1,
                "um_conv2d_fwd: output size mismatch");
   UM_CHECK_ARG(pad_mode == UM_PAD_ZERO || pad < H, "um_conv2d_fwd: reflect pad too large");
-  UM_CHECK_ARG(epilogue != UM_EPI_STATS || stats != nullptr, "um_conv2d_fwd: stats buffer missing");
+  UM_CHECK_ARG((epilogue != UM_EPI_STATS && epilogue != UM_EPI_STAT_SLOTS) || stats != nullptr,
+               "um_conv2d_fwd: stats buffer missing");
   UM_CHECK_ARG(epilogue != UM_EPI_RESIDUAL || residual != nullptr, "um_conv2d_fwd: residual missing");
   UM_CHECK_ARG(ydtype == dtype || ydtype == UM_F32, "um_conv2d_fwd: ydtype must be dtype or f32");
   umamd::IgArgs a{};
@@ -598,7 +599,9 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
   a.b = wf; a.ldb = (long)R * R * C;
   a.NC = K; a.M = N * P * Q;
   a.bias = bias; a.out = y; a.ld_out = ldy; a.out_f32 = (ydtype == UM_F32);
-  a.epilogue = epilogue; a.accumulate = 0; a.epi_scale = epi_scale;
+  a.epilogue = epilogue == UM_EPI_STAT_SLOTS ? UM_EPI_STATS : epilogue;
+  a.stat_slots = epilogue == UM_EPI_STAT_SLOTS;
+  a.accumulate = 0; a.epi_scale = epi_scale;
   a.residual = residual; a.ldr = ldr; a.stats = stats;
   return umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
 }

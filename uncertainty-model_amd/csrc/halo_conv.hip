@@ -225,6 +225,14 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
     }
     __syncthreads();
     // two partial rows per tile: waves {0,1} (tile rows 0-3) and {2,3} (rows 4-7)
+    if (a.stat_slots) {
+      for (int half = 0; half < 2; ++half)
+        stat_slots_add_row(reinterpret_cast<double*>(a.stats), 2 * blockIdx.x + half, a.NC, bn,
+                           min(BN, a.NC - bn), [&](int i) {
+                             return sStat[2 * half][i >> 1][i & 1] + sStat[2 * half + 1][i >> 1][i & 1];
+                           });
+      return;
+    }
     for (int c = tid; c < 2 * BN; c += 256) {
       const int col = c % BN, half = c / BN;
       const int n = bn + col;

@@ -314,19 +314,29 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
     __syncthreads();
     // stats row blocks of SR rows (BM % SR == 0): waves of rows [w*BM/WM, (w+1)*BM/WM)
     constexpr int WROWS = BM / WM;
-    const int SR = a.stats_rows;
-    const int NSB = BM / SR;
-    for (int c = tid; c < BN * NSB; c += (int)blockDim.x) {
-      const int col = c % BN, sb = c / BN;
-      const int n = bn + col;
-      if (n >= a.NC || bm + sb * SR >= a.M) continue;
-      float sm = 0.f, sq = 0.f;
+    if (a.stat_slots) {  // the whole tile's sums: one f64 atomic per (column, value)
+      stat_slots_add_row(reinterpret_cast<double*>(a.stats), bm / BM, a.NC, bn,
+                         min(BN, a.NC - bn), [&](int i) {
+                           float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < WM; ++w)
-        if ((w * WROWS) / SR == sb) { sm += sStat[w][col][0]; sq += sStat[w][col][1]; }
-      float* o = a.stats + ((long)(bm / SR + sb) * a.NC + n) * 2;
-      o[0] = sm;
-      o[1] = sq;
+                           for (int w = 0; w < WM; ++w) v += sStat[w][i >> 1][i & 1];
+                           return v;
+                         });
+    } else {
+      const int SR = a.stats_rows;
+      const int NSB = BM / SR;
+      for (int c = tid; c < BN * NSB; c += (int)blockDim.x) {
+        const int col = c % BN, sb = c / BN;
+        const int n = bn + col;
+        if (n >= a.NC || bm + sb * SR >= a.M) continue;
+        float sm = 0.f, sq = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w)
+          if ((w * WROWS) / SR == sb) { sm += sStat[w][col][0]; sq += sStat[w][col][1]; }
+        float* o = a.stats + ((long)(bm / SR + sb) * a.NC + n) * 2;
+        o[0] = sm;
+        o[1] = sq;
+      }
     }
   }
   if (staged) {
@@ -727,9 +737,21 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const fl
     for (int l = 1; l < 16; ++l)
 #pragma unroll
       for (int e = 0; e < 4; ++e) { sm[e] += red[l][g][e]; sq[e] += red[l][g][4 + e]; }
-    float* o = a.stats + ((long)blockIdx.x * a.NC + n) * 2;
+    if (!a.stat_slots) {
+      float* o = a.stats + ((long)blockIdx.x * a.NC + n) * 2;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { o[2 * e] = sm[e]; o[2 * e + 1] = sq[e]; }
+      for (int e = 0; e < 4; ++e) { o[2 * e] = sm[e]; o[2 * e + 1] = sq[e]; }
+    }
+  }
+  if (a.stat_slots) {  // stage the 64 column pairs, then contiguous f64 atomics
+    __shared__ float tot[EPI_COLS * 2];
+    if (lane == 0)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { tot[(g * 4 + e) * 2] = sm[e]; tot[(g * 4 + e) * 2 + 1] = sq[e]; }
+    __syncthreads();
+    const int c0 = blockIdx.y * EPI_COLS;
+    stat_slots_add_row(reinterpret_cast<double*>(a.stats), blockIdx.x, a.NC, c0,
+                       min(EPI_COLS, a.NC - c0), [&](int i) { return tot[i]; });
   }
 }
 

@@ -26,13 +26,14 @@ class RandomlyConnectedModel(nn.Module):
         self.decoder = DepthDecoder(**decoder)
         self.compute_dtype = umamd.resolve_dtype(dtype)
         self._packer = P.WeightPacker()  # packed conv weights, one refresh launch per forward
+        self._stats = U.StatArena()      # BN statistics slots, one zero fill per forward
 
     def forward(self, image: Tensor, scale: float = 1) -> DecoderOut:
         _, _, h, w = image.shape
         if h % 32 or w % 32:
             raise ValueError(f'image size {h}x{w}: height and width must be multiples of 32')
         x = U.image_to_nhwc(image, self.compute_dtype)
-        with P.scope(self._packer):
+        with P.scope(self._packer), U.stat_scope(self._stats, x.device):
             feats = self.encoder._fwd(x)
             disps = self.decoder._fwd(x, *feats, scale=float(scale))
         disps = tuple(d.permute(0, 3, 1, 2) for d in disps)  # logical NCHW, NHWC memory

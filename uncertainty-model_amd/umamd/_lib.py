@@ -16,7 +16,8 @@ LIB_PATH = os.path.join(_HERE, 'libumamd.so')
 
 UM_F32, UM_BF16 = 0, 1
 PAD_ZERO, PAD_REFLECT = 0, 1
-EPI_NONE, EPI_STATS, EPI_SIGMOID_SCALE, EPI_RESIDUAL = 0, 1, 2, 3
+EPI_NONE, EPI_STATS, EPI_SIGMOID_SCALE, EPI_RESIDUAL, EPI_STAT_SLOTS = 0, 1, 2, 3, 4
+STAT_SLOTS = 16  # UM_STAT_SLOTS (include/umamd.h)
 CAT_COPY, CAT_UP2, CAT_PSHUF = 0, 1, 2
 
 _P = ctypes.c_void_p
@@ -64,6 +65,12 @@ _SIG = {
     'um_bn_coeffs': (_I, [_P, _D, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_fwd_pool_parts': (_I, [_L, _L]),
     'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, _L, _P, 's']),
+    'um_bn_elu_fwd_slots': (_I, [_I, _L, _I, _P, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P, _P, _P,
+                                 _P, _P, _P, _I, _I, _L, _P, 's']),
+    'um_bn_elu_bwd_reduce_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
+                                        _P, 's']),
+    'um_bn_elu_bwd_apply_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
+                                       _P, _D, _P, _P, _P, _P, _P, _I, 's']),
     'um_bn_bwd_parts': (_I, [_L]),
     'um_bn_bwd_fin_ws': (_L, [_L, _I]),
     'um_bn_elu_bwd_reduce_coeffs': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,

@@ -22,6 +22,7 @@ Granularity (one autograd node each):
 from __future__ import annotations
 
 import os
+from contextlib import contextmanager
 from typing import List, Optional, Sequence
 
 import torch
@@ -176,6 +177,71 @@ _CONSTS = {}
 #    launch it replaces
 _FUSED_BN_BWD = os.environ.get('UMAMD_FUSED_BN_BWD', '0') == '1'
 _FUSED_SE = os.environ.get('UMAMD_FUSED_SE', '1') == '1'
+#  - single-process BN statistics as f64 atomics into zeroed slots, finished
+#    by the consumer kernels (no reduction launch per BN layer and direction)
+_BN_SLOTS = os.environ.get('UMAMD_BN_SLOTS', '1') == '1'
+
+
+class StatArena:
+    """Zeroed f64 scratch for the BN statistics slots of one model forward
+    and its backward (``um_bn_elu_fwd_slots`` / ``*_bwd_*_slots``).
+
+    ``begin`` allocates ONE zeroed buffer (one fill launch per forward, sized
+    by the previous forward's use) and ``take`` hands out views of it; the
+    autograd graph keeps the buffer alive until its backward has run, so two
+    forwards in flight never share slots.  A forward that needs more than the
+    hint grows by further zeroed chunks (the first forward of a model)."""
+
+    CHUNK = 1 << 16
+
+    def __init__(self):
+        self.hint = 0
+        self.buf = None
+        self.off = 0
+        self.used = 0
+
+    def begin(self, device):
+        self.buf = torch.zeros((max(self.hint, self.CHUNK),), dtype=torch.float64, device=device)
+        self.off = 0
+        self.used = 0
+
+    def take(self, n: int) -> torch.Tensor:
+        n = (n + 31) // 32 * 32  # 256-byte aligned views
+        if self.off + n > self.buf.numel():
+            self.buf = torch.zeros((max(n, self.CHUNK),), dtype=torch.float64,
+                                   device=self.buf.device)
+            self.off = 0
+        v = self.buf[self.off:self.off + n]
+        self.off += n
+        self.used += n
+        return v
+
+    def end(self):
+        self.hint = max(self.hint, self.used)
+        self.buf = None
+
+    def __deepcopy__(self, memo):
+        return StatArena()
+
+
+_ARENA: Optional[StatArena] = None
+
+
+@contextmanager
+def stat_scope(arena: Optional[StatArena], device):
+    """Make ``arena`` the BN statistics scratch of the convs called inside
+    (one model forward); without one, BN uses the partial-row reductions."""
+    global _ARENA
+    prev = _ARENA
+    _ARENA = arena if _BN_SLOTS else None
+    try:
+        if _ARENA is not None:
+            _ARENA.begin(device)
+        yield
+    finally:
+        if _ARENA is not None:
+            _ARENA.end()
+        _ARENA = prev
 
 
 def _const_vec(value: float, n: int, device) -> torch.Tensor:
@@ -282,9 +348,25 @@ class ConvBNELUFn(torch.autograd.Function):
         Q = (W + 2 * spec.pad - R) // spec.stride + 1
         M = N * P * Q
         bias_f = bias.detach().float().contiguous() if bias is not None else None
+        slots_f = slots_b = None
         if bn is not None:
             training = bn.training
             sync = BNSync(bn)
+        if bn is not None and training and _ARENA is not None and not sync.collective:
+            # statistics in f64 slots: the conv adds them atomically, the BN
+            # apply finishes them (no reduction launch)
+            if bn.track_running_stats and bn.running_mean is not None and bn.momentum is None:
+                raise NotImplementedError('BatchNorm momentum=None (cumulative average) is not supported')
+            slots_f = _ARENA.take(L.STAT_SLOTS * K * 2)
+            slots_b = _ARENA.take(L.STAT_SLOTS * K * 2)
+            y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
+                          out_dtype=torch.float32, epi=L.EPI_STAT_SLOTS, stats=slots_f,
+                          creal=Creal)
+            mean = torch.empty(K, dtype=torch.float32, device=dev)
+            invstd = torch.empty_like(mean)
+            scale = torch.empty_like(mean)
+            shift = torch.empty_like(mean)
+        elif bn is not None:
             nparts = query('um_conv_stats_parts', M, K)
             parts = torch.empty((nparts, K, 2), dtype=torch.float32, device=dev)
             y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
@@ -304,8 +386,17 @@ class ConvBNELUFn(torch.autograd.Function):
         if w1 is not None and _FUSED_SE:  # the SE squeeze rides in the BN-apply pass
             npool = query('um_bn_fwd_pool_parts', M, P * Q)
             pool = torch.empty((npool, K), dtype=torch.float32, device=dev)
-        call('um_bn_elu_fwd', _dt(a), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
-             int(spec.elu), P * Q, ptr(pool))
+        if slots_f is not None:
+            upd = bn.track_running_stats and bn.running_mean is not None
+            nbt = bn.num_batches_tracked if upd else None
+            call('um_bn_elu_fwd_slots', _dt(a), M, K, ptr(y), K, ptr(slots_f), float(M),
+                 ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0),
+                 ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
+                 ptr(nbt), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K,
+                 int(spec.elu), P * Q, ptr(pool))
+        else:
+            call('um_bn_elu_fwd', _dt(a), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
+                 int(spec.elu), P * Q, ptr(pool))
         inv_hw = 1.0 / (P * Q)
         if w1 is not None and not _FUSED_SE:  # separate squeeze: the means, one row per image
             npool, inv_hw = N, 1.0
@@ -325,6 +416,7 @@ class ConvBNELUFn(torch.autograd.Function):
             outs.append(s)
         ctx.spec = spec
         ctx.sync = sync
+        ctx.slots_b = slots_b
         ctx.has_bn = bn is not None and training
         ctx.geom = (N, H, W, Cp, K, Creal, R, P, Q)
         ctx.se = se
@@ -357,7 +449,18 @@ class ConvBNELUFn(torch.autograd.Function):
                  ptr(w2c), ptr(dw1), ptr(dw2), ptr(add_nc), ptr(dz), 1.0 / (P * Q))
         dgamma = dbeta = dbias = None
         need_b = ctx.needs_input_grad[2]
-        if ctx.has_bn:
+        slots_b = ctx.slots_b
+        if ctx.has_bn and slots_b is not None:
+            # backward sums into the slots; the apply kernel finishes them
+            if need_b:
+                dbias = torch.empty(K, dtype=torch.float32, device=dev)
+            if gamma is not None:
+                dgamma = torch.empty(K, dtype=torch.float32, device=dev)
+                dbeta = torch.empty(K, dtype=torch.float32, device=dev)
+            call('um_bn_elu_bwd_reduce_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+                 ptr(slots_b))
+        elif ctx.has_bn:
             k1 = torch.empty(K, dtype=torch.float32, device=dev)
             k2 = torch.empty_like(k1)
             k3 = torch.empty_like(k1)
@@ -410,9 +513,15 @@ class ConvBNELUFn(torch.autograd.Function):
         nbp = query('um_bn_bwd_parts', M)
         reduce_b = need_b and dbias is None
         bparts = torch.empty((nbp, K), dtype=torch.float32, device=dev) if reduce_b else None
-        call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
-             ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1), ptr(k2),
-             ptr(k3), ptr(dy), K, ptr(bparts))
+        if ctx.has_bn and slots_b is not None:
+            call('um_bn_elu_bwd_apply_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+                 ptr(slots_b), float(M), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dbias),
+                 ptr(dy), K)
+        else:
+            call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
+                 ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1),
+                 ptr(k2), ptr(k3), ptr(dy), K, ptr(bparts))
         dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode,
                          segs=spec.segs)
         if reduce_b:
