@@ -505,3 +505,41 @@ def test_dgrad_reflect(dtype, case):
         print(f'dgrad_reflect {case} {dtype} halo_min_tiles={hmin} fold_split_nc={snc}: '
               f'rel {err:.3e}')
         assert err < tol, err
+
+
+# 64x64 LDS-DMA main loop with 3 stages (several blocks per CU) and with 6
+# stages (grids of <= glds_deep_blocks blocks, one 96 KB block per CU), split
+# and unsplit, row- and column-major tile order, forward and data gradient,
+# against f64 torch on the same bf16 operands
+@pytest.mark.parametrize('case', [(256, 256, 3, 2, 16, 32), (128, 128, 3, 8, 16, 32),
+                                  (512, 512, 3, 2, 8, 16), (128, 192, 1, 4, 16, 32)])
+@pytest.mark.parametrize('deep', [3, 6])
+@pytest.mark.parametrize('split_below', [0, 256])
+@pytest.mark.parametrize('xcd_col', [0, 2])
+def test_glds_stage_depth(case, deep, split_below, xcd_col):
+    from umamd import functional as U
+    from umamd._lib import PAD_ZERO, lib
+    C, K, R, N, H, W = case
+    pad = (R - 1) // 2
+    dtype = torch.bfloat16
+    g = torch.Generator().manual_seed(5)
+    w = (torch.rand(K, C, R, R, generator=g) - 0.5) * 0.2
+    x = torch.randn(N, C, H, W, generator=g)
+    dy = torch.randn(N, K, H, W, generator=g)
+    wq, xq, dyq = (t.to(dtype).double() for t in (w, x, dy))
+    ref_y = F.conv2d(xq, wq, padding=pad)
+    ref_dx = torch.nn.grad.conv2d_input((N, C, H, W), wq, dyq, padding=pad)
+    wf, wT = U._pack(w.to(DEV), C, dtype)
+    knobs = {b'glds_deep': deep, b'glds_deep_blocks': 1024, b'glds_split_below': split_below,
+             b'halo': 0, b'xcd_col': xcd_col}
+    old = {k: lib().um_set_tuning(k, v) for k, v in knobs.items()}
+    try:
+        y = U._conv_fwd(_nhwc(x).to(dtype), wf, None, K, R, 1, pad, PAD_ZERO,
+                        out_dtype=torch.float32)
+        dx = U._conv_dgrad(_nhwc(dy).to(dtype), wT, (N, H, W, C), K, R, 1, pad, PAD_ZERO)
+        torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            lib().um_set_tuning(k, v)
+    assert _rel(_nchw(y), ref_y) < 1e-5
+    assert _rel(_nchw(dx), ref_dx) < 1e-2

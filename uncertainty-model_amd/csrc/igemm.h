@@ -42,6 +42,7 @@ struct IgArgs {
   float* stats;     // [parts][NC][2] f32 partial rows, or (stat_slots) f64 slots
   int stats_rows;   // set by igemm_run (igemm_stats_rows)
   int stat_slots;   // UM_EPI_STAT_SLOTS: stats is double[UM_STAT_SLOTS][NC][2]
+  int colmajor;     // tile order, set by igemm_run (knob xcd_col)
 };
 
 // rows per BN partial-statistics row of a stats epilogue (M, NC of the GEMM)

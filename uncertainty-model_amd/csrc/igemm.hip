@@ -396,8 +396,19 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
       t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
     }
   }
-  const int bm = (t / ntn) * BM;
-  const int bn = (t - (t / ntn) * ntn) * BN;
+  // row-major tile order (an XCD's contiguous t range shares row tiles, so
+  // reads a slice of A and all of B) unless the weights outweigh the
+  // gathered image (deep layers): then column-major, each XCD's L2 holds a
+  // slice of B and the whole (small) A
+  int bm, bn;
+  if (a.colmajor) {
+    const int ntm = gridDim.x / ntn;
+    bn = (t / ntm) * BN;
+    bm = (t - (t / ntm) * ntm) * BM;
+  } else {
+    bm = (t / ntn) * BM;
+    bn = (t - (t / ntn) * ntn) * BN;
+  }
 
   const T* __restrict__ asrc = reinterpret_cast<const T*>(a.a);
   const T* __restrict__ bsrc = reinterpret_cast<const T*>(a.b);
@@ -517,6 +528,17 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// wait until at most min(later, N) k-steps of PER loads each are outstanding
+template <int PER, int N>
+__device__ __forceinline__ void wait_later(int later) {
+  if constexpr (N == 0) {
+    wait_vm<0>();
+  } else {
+    if (later >= N) wait_vm<N * PER>();
+    else wait_later<PER, N - 1>(later);
+  }
+}
+
 template <int MODE>
 __device__ __forceinline__ const bf16_t* gather_ptr(const IgArgs& a, const bf16_t* src,
                                                      const ARow& w, int r, int s, int c) {
@@ -535,13 +557,16 @@ __device__ __forceinline__ const bf16_t* gather_ptr(const IgArgs& a, const bf16_
 
 // NW = 4 or 8 waves; with 8, a 64x64 tile gives each wave a 16x32 sub-tile
 // and every SIMD two waves of the block to overlap the per-step latencies.
-template <int BM, int BN, int NW, bool SPLIT, int MODE>
+// NST stages: 3 (48 KB for 64x64, several blocks per CU) or deeper for grids
+// of at most ~1-2 blocks per CU, whose k-loop is pure load latency (knob
+// glds_deep: 6 stages = 5 k-steps in flight, 96 KB).
+template <int BM, int BN, int NW, bool SPLIT, int MODE, int NST>
 __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __restrict__ ws,
                                                               int steps, int steps_per_split,
                                                               int ntn) {
   constexpr bool CLS = MODE == 1;
   static_assert(MODE != 2, "the reflect fold gathers through registers");
-  constexpr int BK = 64, NST = 3, WM = NW == 8 ? 4 : 2, WN = 2;
+  constexpr int BK = 64, WM = NW == 8 ? 4 : 2, WN = 2;
   using I = Img<bf16_t, BK>;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int STAGE = (BM + BN) * BK;  // elements
@@ -562,8 +587,19 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
       t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
     }
   }
-  const int bm = (t / ntn) * BM;
-  const int bn = (t - (t / ntn) * ntn) * BN;
+  // row-major tile order (an XCD's contiguous t range shares row tiles, so
+  // reads a slice of A and all of B) unless the weights outweigh the
+  // gathered image (deep layers): then column-major, each XCD's L2 holds a
+  // slice of B and the whole (small) A
+  int bm, bn;
+  if (a.colmajor) {
+    const int ntm = gridDim.x / ntn;
+    bn = (t / ntm) * BN;
+    bm = (t - (t / ntm) * ntm) * BM;
+  } else {
+    bm = (t / ntn) * BM;
+    bn = (t - (t / ntn) * ntn) * BN;
+  }
   const bf16_t* __restrict__ asrc = reinterpret_cast<const bf16_t*>(a.a);
   const bf16_t* __restrict__ bsrc = reinterpret_cast<const bf16_t*>(a.b);
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_page);
@@ -640,10 +676,7 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
   for (int k = 0; k < nsteps; ++k) {
     // this wave's loads of step k have landed when at most the later issued
     // steps' loads are outstanding
-    const int later = nsteps - 1 - k;
-    if (later >= 2) wait_vm<2 * PER>();
-    else if (later == 1) wait_vm<PER>();
-    else wait_vm<0>();
+    wait_later<PER, NST - 1>(nsteps - 1 - k);
     __builtin_amdgcn_s_barrier();  // every wave's DMA for step k is in LDS
     const int cur = k % NST;
     const bf16_t* sA = smem + cur * STAGE;
@@ -764,6 +797,8 @@ struct Knobs {
   int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles, odd_bn, bk64;
   int glds_split_below, glds_split_target;
   int glds;
+  int glds_deep, glds_deep_blocks;
+  int xcd_col;
   int fold_split_nc;
   Knobs() {
     auto env = [](const char* n, int d) {
@@ -796,6 +831,15 @@ struct Knobs {
     // 0 -> 653.6, 7 -> 654.8, 5 -> 661.3 pairs/s (the 128-row tiles keep the
     // register path: 3 LDS stages of 128-row tiles leave 1 block per CU)
     glds = env("UMAMD_IG_GLDS", 5);
+    // 6-stage LDS-DMA loop for 8-wave 64x64 grids of at most this many
+    // blocks (one 96 KB block per CU); 3 = off.  Step sweep: 3 -> 721,
+    // 6 -> 715 pairs/s (unsplit deep grids 713-717): five k-steps in flight
+    // do not shorten the deep layers' k-loop, so latency is not its limit
+    glds_deep = env("UMAMD_IG_GLDS_DEEP", 3);
+    glds_deep_blocks = env("UMAMD_IG_GLDS_DEEP_BLOCKS", 256);
+    // column-major tile order for weight-heavy GEMMs (0 off, 1 auto, 2 on):
+    // per conv and per step within noise (714 vs 713 pairs/s), off
+    xcd_col = env("UMAMD_IG_XCD_COL", 0);
     // per conv (tools/conv_table.py): split form 256x512 C48 171 -> 117 us,
     // C32 K8 125 -> 85; one pass stays ahead from C = 128 up (16x32 C640:
     // 106 vs 140, 8x16 C512: 53 vs 79)
@@ -876,17 +920,26 @@ int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
   if constexpr (sizeof(T) == 2 && BK == 64 && WM == 2 && WN == 2 && MODE != 2) {
     if (a.pmode != umamd::IG_FOLD && (knobs().glds & (BM == 64 ? 1 : 2))) {
       const bool w8 = BM == 64 && (knobs().glds & 4);
-      if (w8 && p.splits > 1)
-        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, true, MODE>), dim3(ntm * ntn, 1, p.splits),
+      const long blocks = (long)ntm * ntn * p.splits;
+      const bool deep = BM == 64 && w8 && knobs().glds_deep > 3 && blocks <= knobs().glds_deep_blocks;
+      constexpr int DEEP = BM == 64 ? 6 : 3;  // 96 KB of stages: 64x64 tiles only
+      if (deep && p.splits > 1)
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, true, MODE, DEEP>), dim3(ntm * ntn, 1, p.splits),
+                           dim3(512), 0, st, a, ws, p.steps, p.per, ntn);
+      else if (deep)
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, false, MODE, DEEP>), dim3(ntm * ntn, 1, 1),
+                           dim3(512), 0, st, a, ws, p.steps, p.per, ntn);
+      else if (w8 && p.splits > 1)
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, true, MODE, 3>), dim3(ntm * ntn, 1, p.splits),
                            dim3(512), 0, st, a, ws, p.steps, p.per, ntn);
       else if (w8)
-        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, false, MODE>), dim3(ntm * ntn, 1, 1),
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, false, MODE, 3>), dim3(ntm * ntn, 1, 1),
                            dim3(512), 0, st, a, ws, p.steps, p.per, ntn);
       else if (p.splits > 1)
-        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, true, MODE>), dim3(ntm * ntn, 1, p.splits),
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, true, MODE, 3>), dim3(ntm * ntn, 1, p.splits),
                            dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
       else
-        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, false, MODE>), dim3(ntm * ntn, 1, 1),
+        hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, false, MODE, 3>), dim3(ntm * ntn, 1, 1),
                            dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
       if (p.splits > 1)
         hipLaunchKernelGGL((splitk_epilogue_kernel<T, MODE>),
@@ -971,6 +1024,13 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   if (a_in.M == 0) return UM_OK;
   IgArgs a = a_in;
   a.stats_rows = igemm_stats_rows(a.M, a.NC);
+  {
+    // column-major tile order when B (NC x taps x ach) is larger than the
+    // gathered image A (M x ach): knob xcd_col 0 = never, 1 = auto, 2 = always
+    const int xc = knobs().xcd_col;
+    const long abytes = (long)a.M * a.ach, bbytes = (long)a.NC * a.R * a.Rx * a.ach;
+    a.colmajor = xc == 2 || (xc == 1 && bbytes > abytes);
+  }
   if (a.border) {
     // the reflect fold's border list: a few thousand rows, one small plan
     Plan p{};
@@ -1007,6 +1067,9 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "odd_bn")) f = &k.odd_bn;
   else if (!strcmp(key, "bk64")) f = &k.bk64;
   else if (!strcmp(key, "glds")) f = &k.glds;
+  else if (!strcmp(key, "glds_deep")) f = &k.glds_deep;
+  else if (!strcmp(key, "xcd_col")) f = &k.xcd_col;
+  else if (!strcmp(key, "glds_deep_blocks")) f = &k.glds_deep_blocks;
   else if (!strcmp(key, "fold_split_nc")) f = &k.fold_split_nc;
   if (!f) return -1;
   const int old = *f;
