@@ -543,3 +543,44 @@ def test_glds_stage_depth(case, deep, split_below, xcd_col):
             lib().um_set_tuning(k, v)
     assert _rel(_nchw(y), ref_y) < 1e-5
     assert _rel(_nchw(dx), ref_dx) < 1e-2
+
+
+# 8-channel GEMM operands with 4 taps packed per 32-deep k-step (knob
+# tappack 3, default) and without (0): the 7x7 stride-2 first conv (C = 8
+# after the 3-channel pad), the 8-channel heads' data gradients (zero and
+# reflect pad, the reflect fold) and a stride-2 data gradient whose parity
+# classes gather 8 channels; forward and data gradient against f64 torch on
+# the same quantised operands
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [(8, 32, 7, 2, 'zero', 4, 64, 96), (32, 8, 3, 1, 'reflect', 2, 32, 64),
+                                  (128, 8, 3, 1, 'reflect', 2, 16, 24), (16, 8, 3, 2, 'zero', 2, 24, 40),
+                                  (24, 8, 5, 1, 'zero', 2, 20, 36)])
+@pytest.mark.parametrize('pack', [0, 3])
+def test_tappack(dtype, case, pack):
+    from umamd import functional as U
+    from umamd._lib import PAD_REFLECT, PAD_ZERO, lib
+    C, K, R, stride, mode, N, H, W = case
+    pad = (R - 1) // 2
+    g = torch.Generator().manual_seed(21)
+    w = (torch.rand(K, C, R, R, generator=g) - 0.5) * 0.3
+    x = torch.randn(N, C, H, W, generator=g)
+    wq, xq = w.to(dtype).double(), x.to(dtype).double()
+    xr = xq.clone().requires_grad_(True)
+    xp = F.pad(xr, (pad,) * 4, mode='reflect' if mode == 'reflect' else 'constant')
+    ref_y = F.conv2d(xp, wq, stride=stride)
+    dy = torch.randn(ref_y.shape, generator=g)
+    dyq = dy.to(dtype).double()
+    (ref_y * dyq).sum().backward()
+    wf, wT = U._pack(w.to(DEV), C, dtype)
+    pm = PAD_REFLECT if mode == 'reflect' else PAD_ZERO
+    old = lib().um_set_tuning(b'tappack', pack)
+    try:
+        y = U._conv_fwd(_nhwc(x).to(dtype), wf, None, K, R, stride, pad, pm,
+                        out_dtype=torch.float32)
+        dx = U._conv_dgrad(_nhwc(dy).to(dtype), wT, (N, H, W, C), K, R, stride, pad, pm)
+        torch.cuda.synchronize()
+    finally:
+        lib().um_set_tuning(b'tappack', old)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(_nchw(y), ref_y) < 1e-5
+    assert _rel(_nchw(dx), xr.grad) < tol

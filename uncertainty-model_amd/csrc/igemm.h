@@ -43,6 +43,7 @@ struct IgArgs {
   int stats_rows;   // set by igemm_run (igemm_stats_rows)
   int stat_slots;   // UM_EPI_STAT_SLOTS: stats is double[UM_STAT_SLOTS][NC][2]
   int colmajor;     // tile order, set by igemm_run (knob xcd_col)
+  int tappack;      // 4 taps x 8 channels per k-step (ach == 8), set by igemm_run
 };
 
 // rows per BN partial-statistics row of a stats epilogue (M, NC of the GEMM)

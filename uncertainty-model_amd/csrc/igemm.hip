@@ -440,8 +440,37 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
   const int RX = CLS ? a.Rx : a.R;
   int r = tap / RX, s = tap - (tap / RX) * RX;
 
+  // tap packing (a.tappack: 8-channel operands, BK = 32): a k-step holds 4
+  // taps x 8 channels instead of one tap's 8 channels + 24 zero columns, so
+  // the 7x7 first conv and the 8-channel heads' data gradients take 1/4 of
+  // the k-steps.  Chunk q of step st is tap 4*st + q, channels 0..7.
+  const int taps = a.R * RX;
+  int tb = s_begin * CPR;
+  auto tap_b = [&](int r_, int s_) {
+    return CLS ? (a.r0y + 2 * r_) * a.wR + (a.r0x + 2 * s_)
+               : (a.flip ? (a.R - 1 - r_) * a.R + (a.R - 1 - s_) : r_ * a.R + s_);
+  };
+
   Raw8<T> ra[A_PER], rb[B_PER];
   auto load = [&]() {
+    if (a.tappack) {
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) {
+        const int tp = tb + akc[i];
+        const int r_ = tp / RX, s_ = tp - (tp / RX) * RX;
+        if (tp < taps) gather<MODE>(a, asrc, arow[i], r_, s_, 0, ra[i]);
+        else raw_zero(ra[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        raw_zero(rb[i]);
+        const int tp = tb + bkc[i];
+        const int r_ = tp / RX, s_ = tp - (tp / RX) * RX;
+        if (bok[i] && tp < taps)
+          raw_load8(bsrc + (long)(bn + brow_i[i]) * a.ldb + (long)tap_b(r_, s_) * 8, rb[i]);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) gather<MODE>(a, asrc, arow[i], r, s, c0 + akc[i] * 8, ra[i]);
     const int btap = CLS ? (a.r0y + 2 * r) * a.wR + (a.r0x + 2 * s)
@@ -462,6 +491,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
       if (tid + i * 256 < B_CH) raw_store8(&sB[buf][I::off(brow_i[i], bkc[i])], rb[i]);
   };
   auto advance = [&]() {
+    tb += CPR;
     c0 += BK;
     if (c0 >= a.ach) {
       c0 = 0;
@@ -799,6 +829,7 @@ struct Knobs {
   int glds;
   int glds_deep, glds_deep_blocks;
   int xcd_col;
+  int tappack;
   int fold_split_nc;
   Knobs() {
     auto env = [](const char* n, int d) {
@@ -840,6 +871,10 @@ struct Knobs {
     // column-major tile order for weight-heavy GEMMs (0 off, 1 auto, 2 on):
     // per conv and per step within noise (714 vs 713 pairs/s), off
     xcd_col = env("UMAMD_IG_XCD_COL", 0);
+    // 8-channel operands: bit 0 packs 4 taps per 32-deep k-step, bit 1 also
+    // routes them past the halo kernel.  First conv (7x7 s2, C8) 93 -> 51 us;
+    // step 711 -> 715-716 pairs/s with 1 or 3 (the heads' halo path is as fast)
+    tappack = env("UMAMD_IG_TAPPACK", 1);
     // per conv (tools/conv_table.py): split form 256x512 C48 171 -> 117 us,
     // C32 K8 125 -> 85; one pass stays ahead from C = 128 up (16x32 C640:
     // 106 vs 140, 8x16 C512: 53 vs 79)
@@ -892,9 +927,12 @@ Plan make_plan(int dtype, int M, int NC, int taps, int ach, long ws_bytes, bool 
   return p;
 }
 
+// tap packing applies to 8-channel operands on the 32-deep register path
+bool tappack_ok(int ach, int bk) { return (knobs().tappack & 1) && ach == 8 && bk == 32; }
+
 void split_plan(Plan& p, int M, int NC, int taps, int ach, long ws_bytes, bool glds) {
   const Knobs& kn = knobs();
-  p.steps = taps * ((ach + p.bk - 1) / p.bk);
+  p.steps = tappack_ok(ach, p.bk) ? ceil_div(taps, p.bk / 8) : taps * ((ach + p.bk - 1) / p.bk);
   // Split grids that leave CUs with too few blocks to hide load latency: the
   // partials cost an f32 write + read of splits*M*NC (about 1 us per 8 MB
   // each way), so aim at ~1024 blocks, >= 4 k-steps per split and <= 32 MB
@@ -1036,14 +1074,20 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
     Plan p{};
     p.bk = 32; p.bm = 64; p.bn = 64; p.wm = 2; p.wn = 2;
     split_plan(p, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0, false);
+    a.tappack = tappack_ok(a.ach, p.bk);
     if (dtype == UM_BF16) return launch_cls<bf16_t, 32, 64, 64, 2, 2, 2>(a, p, ws, st);
     return launch_cls<float, 32, 64, 64, 2, 2, 2>(a, p, ws, st);
   }
-  if (knobs().halo && halo_applicable(dtype, a, knobs().halo_min_tiles)) return halo_run(a, st);
+  // 8-channel operands take the tap-packed GEMM instead of the halo kernel
+  // (which stages 32-channel chunks) unless tappack bit 1 is clear
+  const bool pack_first = (knobs().tappack & 3) == 3 && a.ach == 8;
+  if (knobs().halo && !pack_first && halo_applicable(dtype, a, knobs().halo_min_tiles))
+    return halo_run(a, st);
   // the LDS-DMA loop serves the bf16 64x64 tiles without the reflect fold
   Plan p = make_plan(dtype, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0, false);
   if (dtype == UM_BF16 && p.bm == 64 && p.bk == 64 && a.pmode != IG_FOLD && (knobs().glds & 1))
     p = make_plan(dtype, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0, true);
+  a.tappack = tappack_ok(a.ach, p.bk);
   if (dtype == UM_BF16) return dispatch_tiles<bf16_t>(a, p, ws, st);
   return dispatch_tiles<float>(a, p, ws, st);
 }
@@ -1069,6 +1113,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "glds")) f = &k.glds;
   else if (!strcmp(key, "glds_deep")) f = &k.glds_deep;
   else if (!strcmp(key, "xcd_col")) f = &k.xcd_col;
+  else if (!strcmp(key, "tappack")) f = &k.tappack;
   else if (!strcmp(key, "glds_deep_blocks")) f = &k.glds_deep_blocks;
   else if (!strcmp(key, "fold_split_nc")) f = &k.fold_split_nc;
   if (!f) return -1;
