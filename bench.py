@@ -331,6 +331,12 @@ def main():
     # UMAMD_DIST=1 (under torchrun) runs the data-parallel path even with one
     # rank: the DDP wrapper and the captured RCCL all-reduce on a 1-GPU box
     dp = world > 1 or os.environ.get('UMAMD_DIST') == '1'
+    # the ONE JSON line goes to the original stdout; everything else the
+    # libraries print there (RCCL's version banner at communicator init)
+    # is sent to stderr
+    json_out = os.fdopen(os.dup(1), 'w')
+    sys.stdout.flush()
+    os.dup2(2, 1)
     if dp:
         # 'nccl' is RCCL; UMAMD_DIST_BACKEND=gloo rehearses the N>1 path with
         # several ranks on one GPU (RCCL needs a GPU per rank)
@@ -426,7 +432,7 @@ def main():
             'roofline': roof,
             'cpu_baseline': cpu,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), file=json_out, flush=True)
     if dp:
         dist.destroy_process_group()
 

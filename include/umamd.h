@@ -183,12 +183,16 @@ int um_bn_fwd_pool_parts(long M, long HW);
 int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
                   const float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
                   hipStream_t stream);
-/* Single-process BN with the statistics in f64 slots (no reduction launch):
- * the conv ran with UM_EPI_STAT_SLOTS into `slots` ([UM_STAT_SLOTS][C][2],
- * count = M elements per channel); every workgroup sums the slots and
- * derives scale/shift itself, workgroup 0 also writes mean/invstd/scale/shift
- * (kept for the backward) and updates the running statistics -- the
- * semantics of um_bn_stats_coeffs + um_bn_elu_fwd in one launch. */
+/* BN with the statistics in f64 slots (no reduction launch): the conv ran
+ * with UM_EPI_STAT_SLOTS into `slots` ([UM_STAT_SLOTS][C][2], count = M
+ * elements per channel); every workgroup sums the slots and derives
+ * scale/shift itself, workgroup 0 also writes mean/invstd/scale/shift (kept
+ * for the backward) and updates the running statistics -- the semantics of
+ * um_bn_stats_coeffs + um_bn_elu_fwd in one launch.  The conv (and
+ * um_bn_elu_bwd_reduce_slots) also store the element count after the slots
+ * (slots[UM_STAT_SLOTS*C*2], so a slot buffer holds UM_STAT_SLOTS*C*2 + 1
+ * doubles); SyncBN all-reduces slots + count and passes count <= 0 to read
+ * the global count there. */
 int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const double* slots,
                         double count, const float* gamma, const float* beta, float eps,
                         float momentum, float* running_mean, float* running_var,
@@ -203,13 +207,18 @@ int um_bn_elu_bwd_reduce_slots(int dtype, long M, int C, long HW, const void* da
                                int apply_elu, double* slots, hipStream_t stream);
 /* dy from the slot sums: every workgroup derives k1..k3 (as
  * um_bn_bwd_stats_coeffs), workgroup 0 writes dgamma, dbeta and the
- * closed-form conv-bias gradient dbias (each optional) */
+ * closed-form conv-bias gradient dbias times dbias_scale (each optional).
+ * SyncBN: slots are all-reduced (count <= 0 reads the count after them, as
+ * um_bn_elu_fwd_slots), local_slots are this rank's slots before the
+ * all-reduce (dgamma/dbeta from local sums, as torch SyncBatchNorm) and
+ * dbias_scale = 1/world; single process: local_slots null, dbias_scale 1 */
 int um_bn_elu_bwd_apply_slots(int dtype, long M, int C, long HW, const void* da, int ldda,
                               const void* y, int ldy, const float* mean, const float* invstd,
                               const float* scale, const float* shift, const float* add_nc,
                               int apply_elu, const double* slots, double count,
-                              const float* gamma, float* dgamma, float* dbeta, float* dbias,
-                              void* dy, int lddy, hipStream_t stream);
+                              const double* local_slots, const float* gamma, float* dgamma,
+                              float* dbeta, float* dbias, float dbias_scale, void* dy, int lddy,
+                              hipStream_t stream);
 int um_bn_bwd_parts(long M);
 int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int ldda,
                          const void* y, int ldy, const float* mean, const float* invstd,

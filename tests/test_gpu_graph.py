@@ -207,16 +207,7 @@ def test_captured_ddp_step_one_rank():
         m_e = _model(cfg).train()
         m_e.load_state_dict(unwrap(m_g).state_dict())
         opt_e = _adam_clone(opt_g, unwrap(m_g), m_e)
-        # the eager single-process step on the same BN reduction (partial
-        # rows, as the SyncBN path): the l1 NLL gradient sign(sigma - e)
-        # flips with the summation order of the f64 slot atomics, which
-        # test_conv_bn_elu_slots covers on its own
-        import umamd.functional as U
-        slots, U._BN_SLOTS = U._BN_SLOTS, False
-        try:
-            dl_e, el_e, _ = train_step(m_e, left, right, lf, opt_e, 0.3)
-        finally:
-            U._BN_SLOTS = slots
+        dl_e, el_e, _ = train_step(m_e, left, right, lf, opt_e, 0.3)
         dl_g, el_g = cap()
         torch.cuda.synchronize()
         for a, b in ((float(dl_e), float(dl_g)), (float(el_e), float(el_g))):

@@ -69,9 +69,11 @@ struct FwdFin {
 
 __device__ __forceinline__ void fwd_fin_coeffs(const FwdFin& f, int C, float* s_sc, float* s_sh) {
   const bool pub = blockIdx.x == 0;
+  // count <= 0: the element count follows the slots (SyncBN: all-reduced with them)
+  const double count = f.count > 0 ? f.count : f.slots[(long)UM_STAT_SLOTS * C * 2];
   stat_slots_finish(f.slots, C, [&](int c, double s0, double s1) {
-    const double mean = s0 / f.count;
-    double var = s1 / f.count - mean * mean;
+    const double mean = s0 / count;
+    double var = s1 / count - mean * mean;
     if (var < 0) var = 0;
     const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
     const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
@@ -84,7 +86,7 @@ __device__ __forceinline__ void fwd_fin_coeffs(const FwdFin& f, int C, float* s_
       f.scale[c] = sc;
       f.shift[c] = sh;
       if (f.running_mean != nullptr) {
-        const double unb = f.count > 1 ? var * f.count / (f.count - 1) : var;
+        const double unb = count > 1 ? var * count / (count - 1) : var;
         f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
         f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unb;
       }
@@ -300,6 +302,7 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
     }
     lane_reduce<16>(red, rm, acc);
     if (slots != nullptr) {  // stage [8G channels][2] in LDS, then contiguous f64 atomics
+      if (g0 == 0) stat_slots_count(slots, C, M);
       if (rm.lane == 0 && g < cg)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -355,28 +358,40 @@ __global__ void bwd_coeffs_kernel(const double* __restrict__ st, double count, i
 // workgroup 0 writes dgamma, dbeta and the closed-form conv-bias gradient.
 struct ApplyFin {
   const double* slots;  // null: k1..k3 are given
-  double count;
+  double count;         // <= 0: read after the slots (SyncBN)
   const float* gamma;
   float *dgamma, *dbeta, *dbias;
+  const double* local;  // SyncBN: this rank's slots before the all-reduce (dgamma/dbeta)
+  float dbias_scale;    // SyncBN: 1/world (DDP averages the ranks' bias gradients)
 };
 
 __device__ __forceinline__ void apply_fin_coeffs(const ApplyFin& f, int C,
                                                  const float* __restrict__ invstd, float* s_k1,
                                                  float* s_k2, float* s_k3) {
   const bool pub = blockIdx.x == 0;
+  const double count = f.count > 0 ? f.count : f.slots[(long)UM_STAT_SLOTS * C * 2];
   stat_slots_finish(f.slots, C, [&](int c, double s0, double s1) {
     const float g = f.gamma ? f.gamma[c] : 1.f;
-    const float a1 = g * invstd[c], a2 = (float)(s0 / f.count);
+    const float a1 = g * invstd[c], a2 = (float)(s0 / count);
     s_k1[c] = a1;
     s_k2[c] = a2;
-    s_k3[c] = (float)(s1 / f.count);
+    s_k3[c] = (float)(s1 / count);
     if (pub) {
-      if (f.dgamma) f.dgamma[c] = (float)s1;
-      if (f.dbeta) f.dbeta[c] = (float)s0;
+      if (f.local == nullptr) {
+        if (f.dgamma) f.dgamma[c] = (float)s1;
+        if (f.dbeta) f.dbeta[c] = (float)s0;
+      }
       // conv-bias gradient sum_m dy = k1 (s0 - n k2 - k3 sum xhat), sum xhat = 0
-      if (f.dbias) f.dbias[c] = a1 * (float)(s0 - f.count * (double)a2);
+      // (global sums; dbias_scale spreads it over the ranks' gradient average)
+      if (f.dbias) f.dbias[c] = f.dbias_scale * a1 * (float)(s0 - count * (double)a2);
     }
   });
+  // parameter grads from this rank's sums, like torch SyncBatchNorm
+  if (pub && f.local != nullptr)
+    stat_slots_finish(f.local, C, [&](int c, double s0, double s1) {
+      if (f.dgamma) f.dgamma[c] = (float)s1;
+      if (f.dbeta) f.dbeta[c] = (float)s0;
+    });
   __syncthreads();
 }
 
@@ -511,8 +526,8 @@ int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const 
                         long long* num_batches_tracked, float* mean, float* invstd, float* scale,
                         float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
                         hipStream_t st) {
-  UM_CHECK_ARG(slots != nullptr && count > 0 && mean && invstd && scale && shift,
-               "um_bn_elu_fwd_slots: slots / count / coefficient outputs");
+  UM_CHECK_ARG(slots != nullptr && mean && invstd && scale && shift,
+               "um_bn_elu_fwd_slots: slots / coefficient outputs");
   FwdFin fin{};
   fin.slots = slots; fin.count = count; fin.gamma = gamma; fin.beta = beta;
   fin.eps = eps; fin.momentum = momentum;
@@ -635,12 +650,13 @@ int um_bn_elu_bwd_apply_slots(int dtype, long M, int C, long HW, const void* da,
                               const void* y, int ldy, const float* mean, const float* invstd,
                               const float* scale, const float* shift, const float* add_nc,
                               int apply_elu, const double* slots, double count,
-                              const float* gamma, float* dgamma, float* dbeta, float* dbias,
-                              void* dy, int lddy, hipStream_t st) {
-  UM_CHECK_ARG(slots != nullptr && count > 0, "um_bn_elu_bwd_apply_slots: slots / count");
+                              const double* local_slots, const float* gamma, float* dgamma,
+                              float* dbeta, float* dbias, float dbias_scale, void* dy, int lddy,
+                              hipStream_t st) {
+  UM_CHECK_ARG(slots != nullptr, "um_bn_elu_bwd_apply_slots: slots");
   ApplyFin fin{};
-  fin.slots = slots; fin.count = count; fin.gamma = gamma;
-  fin.dgamma = dgamma; fin.dbeta = dbeta; fin.dbias = dbias;
+  fin.slots = slots; fin.count = count; fin.gamma = gamma; fin.local = local_slots;
+  fin.dgamma = dgamma; fin.dbeta = dbeta; fin.dbias = dbias; fin.dbias_scale = dbias_scale;
   return bwd_apply_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
                           apply_elu, nullptr, nullptr, nullptr, dy, lddy, nullptr, fin, st);
 }

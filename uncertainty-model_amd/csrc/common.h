@@ -215,6 +215,14 @@ __device__ __forceinline__ void stat_slots_add_row(double* slots, long row_block
   for (int i = threadIdx.x; i < 2 * ncols; i += blockDim.x) unsafeAtomicAdd(p + i, (double)val(i));
 }
 
+// the element count after the slots (read by the consumers when the host
+// passes count <= 0, i.e. after a SyncBN all-reduce of slots + count): one
+// plain store by the launch's first workgroup
+__device__ __forceinline__ void stat_slots_count(double* slots, int C, long count) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
+    slots[(long)UM_STAT_SLOTS * C * 2] = (double)count;
+}
+
 // Block-wide finish over all C channels: fin(c, s0, s1) is called once per
 // channel with the f64 slot sums.  SPL lanes share a channel (each sums every
 // SPL-th slot with 16-byte loads, all issued before the first add, then a

@@ -226,6 +226,7 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
     __syncthreads();
     // two partial rows per tile: waves {0,1} (tile rows 0-3) and {2,3} (rows 4-7)
     if (a.stat_slots) {
+      stat_slots_count(reinterpret_cast<double*>(a.stats), a.NC, a.M);
       for (int half = 0; half < 2; ++half)
         stat_slots_add_row(reinterpret_cast<double*>(a.stats), 2 * blockIdx.x + half, a.NC, bn,
                            min(BN, a.NC - bn), [&](int i) {

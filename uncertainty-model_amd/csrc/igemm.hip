@@ -315,6 +315,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
     // stats row blocks of SR rows (BM % SR == 0): waves of rows [w*BM/WM, (w+1)*BM/WM)
     constexpr int WROWS = BM / WM;
     if (a.stat_slots) {  // the whole tile's sums: one f64 atomic per (column, value)
+      stat_slots_count(reinterpret_cast<double*>(a.stats), a.NC, a.M);
       stat_slots_add_row(reinterpret_cast<double*>(a.stats), bm / BM, a.NC, bn,
                          min(BN, a.NC - bn), [&](int i) {
                            float v = 0.f;
@@ -813,6 +814,7 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const fl
       for (int e = 0; e < 4; ++e) { tot[(g * 4 + e) * 2] = sm[e]; tot[(g * 4 + e) * 2 + 1] = sq[e]; }
     __syncthreads();
     const int c0 = blockIdx.y * EPI_COLS;
+    stat_slots_count(reinterpret_cast<double*>(a.stats), a.NC, a.M);
     stat_slots_add_row(reinterpret_cast<double*>(a.stats), blockIdx.x, a.NC, c0,
                        min(EPI_COLS, a.NC - c0), [&](int i) { return tot[i]; });
   }

@@ -70,7 +70,7 @@ _SIG = {
     'um_bn_elu_bwd_reduce_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
                                         _P, 's']),
     'um_bn_elu_bwd_apply_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
-                                       _P, _D, _P, _P, _P, _P, _P, _I, 's']),
+                                       _P, _D, _P, _P, _P, _P, _P, _F, _P, _I, 's']),
     'um_bn_bwd_parts': (_I, [_L]),
     'um_bn_bwd_fin_ws': (_L, [_L, _I]),
     'um_bn_elu_bwd_reduce_coeffs': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,

@@ -352,16 +352,23 @@ class ConvBNELUFn(torch.autograd.Function):
         if bn is not None:
             training = bn.training
             sync = BNSync(bn)
-        if bn is not None and training and _ARENA is not None and not sync.collective:
+        count = float(M)
+        if bn is not None and training and _ARENA is not None:
             # statistics in f64 slots: the conv adds them atomically, the BN
-            # apply finishes them (no reduction launch)
+            # apply finishes them (no reduction launch).  SyncBN: the slots
+            # and this rank's element count after them are all-reduced in
+            # place (the count rides along: uneven per-rank batches)
             if bn.track_running_stats and bn.running_mean is not None and bn.momentum is None:
                 raise NotImplementedError('BatchNorm momentum=None (cumulative average) is not supported')
-            slots_f = _ARENA.take(L.STAT_SLOTS * K * 2)
-            slots_b = _ARENA.take(L.STAT_SLOTS * K * 2)
+            nslot = L.STAT_SLOTS * K * 2
+            slots_f = _ARENA.take(nslot + 1)
+            slots_b = _ARENA.take(nslot + 1)
             y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
                           out_dtype=torch.float32, epi=L.EPI_STAT_SLOTS, stats=slots_f,
                           creal=Creal)
+            if sync.collective:  # the conv stored this rank's count after the slots
+                sync.all_reduce(slots_f)
+                count = -1.0  # read the all-reduced count after the slots
             mean = torch.empty(K, dtype=torch.float32, device=dev)
             invstd = torch.empty_like(mean)
             scale = torch.empty_like(mean)
@@ -389,7 +396,7 @@ class ConvBNELUFn(torch.autograd.Function):
         if slots_f is not None:
             upd = bn.track_running_stats and bn.running_mean is not None
             nbt = bn.num_batches_tracked if upd else None
-            call('um_bn_elu_fwd_slots', _dt(a), M, K, ptr(y), K, ptr(slots_f), float(M),
+            call('um_bn_elu_fwd_slots', _dt(a), M, K, ptr(y), K, ptr(slots_f), count,
                  ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0),
                  ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
                  ptr(nbt), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K,
@@ -460,6 +467,13 @@ class ConvBNELUFn(torch.autograd.Function):
             call('um_bn_elu_bwd_reduce_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
                  ptr(slots_b))
+            local, bcount, bscale = None, float(M), 1.0
+            if ctx.sync is not None and ctx.sync.collective:
+                # dgamma/dbeta from this rank's sums (torch SyncBatchNorm),
+                # k1..k3 and the conv-bias gradient from the global ones
+                local = slots_b.clone()  # the reduce kernel stored the count after the slots
+                ctx.sync.all_reduce(slots_b)
+                bcount, bscale = -1.0, 1.0 / ctx.sync.world
         elif ctx.has_bn:
             k1 = torch.empty(K, dtype=torch.float32, device=dev)
             k2 = torch.empty_like(k1)
@@ -516,8 +530,8 @@ class ConvBNELUFn(torch.autograd.Function):
         if ctx.has_bn and slots_b is not None:
             call('um_bn_elu_bwd_apply_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
-                 ptr(slots_b), float(M), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dbias),
-                 ptr(dy), K)
+                 ptr(slots_b), bcount, ptr(local), ptr(gamma), ptr(dgamma), ptr(dbeta),
+                 ptr(dbias), bscale, ptr(dy), K)
         else:
             call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
                  ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1),
