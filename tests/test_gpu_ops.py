@@ -584,3 +584,33 @@ def test_tappack(dtype, case, pack):
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert _rel(_nchw(y), ref_y) < 1e-5
     assert _rel(_nchw(dx), xr.grad) < tol
+
+
+# stride-2 data gradient: the four parity classes in one launch (knob cls4,
+# default) and as four launches, odd and even image sizes (classes of
+# different sizes), 8-channel dy (tap packing), against f64 torch
+@pytest.mark.parametrize('case', [(32, 64, 5, 2, 32, 64), (64, 128, 3, 2, 16, 32),
+                                  (16, 32, 3, 2, 15, 21), (48, 8, 3, 2, 18, 26),
+                                  (24, 16, 7, 1, 9, 13)])
+@pytest.mark.parametrize('cls4', [0, 1])
+def test_dgrad_stride2_classes(case, cls4):
+    from umamd import functional as U
+    from umamd._lib import PAD_ZERO, lib
+    C, K, R, N, H, W = case
+    pad = (R - 1) // 2
+    dtype = torch.bfloat16
+    g = torch.Generator().manual_seed(17)
+    w = (torch.rand(K, C, R, R, generator=g) - 0.5) * 0.2
+    P = (H + 2 * pad - R) // 2 + 1
+    Q = (W + 2 * pad - R) // 2 + 1
+    dy = torch.randn(N, K, P, Q, generator=g)
+    wq, dyq = w.to(dtype).double(), dy.to(dtype).double()
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), wq, dyq, stride=2, padding=pad)
+    _, wT = U._pack(w.to(DEV), C, dtype, wf=False)
+    old = lib().um_set_tuning(b'cls4', cls4)
+    try:
+        dx = U._conv_dgrad(_nhwc(dy).to(dtype), wT, (N, H, W, C), K, R, 2, pad, PAD_ZERO)
+        torch.cuda.synchronize()
+    finally:
+        lib().um_set_tuning(b'cls4', old)
+    assert _rel(_nchw(dx), ref) < 1e-2

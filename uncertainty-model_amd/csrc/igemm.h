@@ -54,6 +54,10 @@ long igemm_ws_bytes(int dtype, int M, int NC, int taps, int ach);
 // launch; ws may be null (then no split)
 int igemm_run(int dtype, const IgArgs& a, float* ws, long ws_bytes, hipStream_t st);
 
+// the four parity classes of a stride-2 data gradient in one launch: 1 =
+// launched, 0 = not eligible (launch them one by one), < 0 = -error code
+int igemm_run_cls4(int dtype, IgArgs (&as)[4], hipStream_t st);
+
 // reflect data gradients with more input channels than this run as one fold
 // pass, the others as a zero-pad pass + the border-list pass (knob
 // "fold_split_nc", UMAMD_FOLD_SPLIT_NC)

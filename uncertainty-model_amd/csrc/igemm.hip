@@ -364,9 +364,47 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
   }
 }
 
+// the XCD-aware tile order: blocks b, b+8, b+16... (one XCD) take
+// consecutive tiles
+__device__ __forceinline__ int xcd_tile(int t, int nb) {
+  if (nb >= 16) {
+    const int xcd = t & 7, q = nb >> 3, rr = nb & 7;
+    t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
+  }
+  return t;
+}
+
+template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT, int MODE>
+__device__ __forceinline__ void igemm_tile(const IgArgs& a, float* __restrict__ ws, int steps,
+                                           int steps_per_split, int ntn, int t, int ntiles);
+
 template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT, int MODE>
 __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict__ ws,
                                                      int steps, int steps_per_split, int ntn) {
+  igemm_tile<T, BK, BM, BN, WM, WN, SPLIT, MODE>(a, ws, steps, steps_per_split, ntn,
+                                                 xcd_tile(blockIdx.x, gridDim.x), gridDim.x);
+}
+
+// The four parity classes of a stride-2 data gradient in ONE launch: class c
+// owns tiles [start[c], start[c+1]) of the grid (same column tiling, its own
+// rows, taps and output parity), so the four short-K GEMMs fill the chip
+// together instead of four launches of one tile per CU each (+ their split-K
+// epilogues).
+template <typename T, int BK, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256) igemm_cls4_kernel(IgArgs a0, IgArgs a1, IgArgs a2, IgArgs a3,
+                                                          int4 start, int4 steps, int ntn) {
+  const int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int c = t < start.y ? 0 : (t < start.z ? 1 : (t < start.w ? 2 : 3));
+  const IgArgs* ap = c == 0 ? &a0 : (c == 1 ? &a1 : (c == 2 ? &a2 : &a3));
+  const int s0 = c == 0 ? start.x : (c == 1 ? start.y : (c == 2 ? start.z : start.w));
+  const int s1 = c == 0 ? start.y : (c == 1 ? start.z : (c == 2 ? start.w : (int)gridDim.x));
+  const int st = c == 0 ? steps.x : (c == 1 ? steps.y : (c == 2 ? steps.z : steps.w));
+  igemm_tile<T, BK, BM, BN, WM, WN, false, 1>(*ap, nullptr, st, st, ntn, t - s0, s1 - s0);
+}
+
+template <typename T, int BK, int BM, int BN, int WM, int WN, bool SPLIT, int MODE>
+__device__ __forceinline__ void igemm_tile(const IgArgs& a, float* __restrict__ ws, int steps,
+                                           int steps_per_split, int ntn, int t, int ntiles) {
   constexpr bool CLS = MODE == 1;
   using I = Img<T, BK>;
   constexpr int TM = BM / WM / 16;
@@ -388,22 +426,13 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgArgs a, float* __restrict_
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
 
-  // XCD-aware tile order: blocks b, b+8, b+16... (one XCD) take consecutive tiles
-  int t = blockIdx.x;
-  {
-    const int nb = gridDim.x;
-    if (nb >= 16) {
-      const int xcd = t & 7, q = nb >> 3, rr = nb & 7;
-      t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
-    }
-  }
   // row-major tile order (an XCD's contiguous t range shares row tiles, so
   // reads a slice of A and all of B) unless the weights outweigh the
   // gathered image (deep layers): then column-major, each XCD's L2 holds a
   // slice of B and the whole (small) A
   int bm, bn;
   if (a.colmajor) {
-    const int ntm = gridDim.x / ntn;
+    const int ntm = ntiles / ntn;
     bn = (t / ntm) * BN;
     bm = (t - (t / ntm) * ntm) * BM;
   } else {
@@ -832,6 +861,7 @@ struct Knobs {
   int glds_deep, glds_deep_blocks;
   int xcd_col;
   int tappack;
+  int cls4;
   int fold_split_nc;
   Knobs() {
     auto env = [](const char* n, int d) {
@@ -877,6 +907,8 @@ struct Knobs {
     // routes them past the halo kernel.  First conv (7x7 s2, C8) 93 -> 51 us;
     // step 711 -> 715-716 pairs/s with 1 or 3 (the heads' halo path is as fast)
     tappack = env("UMAMD_IG_TAPPACK", 1);
+    // the four parity classes of a stride-2 data gradient as one launch
+    cls4 = env("UMAMD_IG_CLS4", 1);
     // per conv (tools/conv_table.py): split form 256x512 C48 171 -> 117 us,
     // C32 K8 125 -> 85; one pass stays ahead from C = 128 up (16x32 C640:
     // 106 vs 140, 8x16 C512: 53 vs 79)
@@ -1094,6 +1126,46 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   return dispatch_tiles<float>(a, p, ws, st);
 }
 
+// the four parity classes of a stride-2 data gradient in one launch (bf16,
+// 256-row tiles); returns 1 when launched, 0 when the caller should launch
+// the classes one by one, or an error code < 0
+int igemm_run_cls4(int dtype, IgArgs (&as)[4], hipStream_t st) {
+  if (!knobs().cls4 || dtype != UM_BF16) return 0;
+  for (auto& a : as)
+    if (a.M <= 0) return 0;
+  const Plan p0 = make_plan(dtype, as[0].M, as[0].NC, as[0].R * as[0].Rx, as[0].ach, 0, false);
+  if (p0.bm != 256 || p0.bk != 32) return 0;
+  int start[5] = {0, 0, 0, 0, 0}, steps[4];
+  const int ntn = ceil_div(as[0].NC, p0.bn);
+  for (int c = 0; c < 4; ++c) {
+    IgArgs& a = as[c];
+    a.stats_rows = igemm_stats_rows(a.M, a.NC);
+    a.colmajor = 0;
+    Plan p = p0;
+    split_plan(p, a.M, a.NC, a.R * a.Rx, a.ach, 0, false);  // no workspace: no split
+    a.tappack = tappack_ok(a.ach, p.bk);
+    steps[c] = p.steps;
+    start[c + 1] = start[c] + ceil_div(a.M, 256) * ntn;
+  }
+  const dim3 grid(start[4]);
+  const int4 s4 = make_int4(start[0], start[1], start[2], start[3]);
+  const int4 k4 = make_int4(steps[0], steps[1], steps[2], steps[3]);
+#define UM_CLS4(BN_)                                                                       \
+  hipLaunchKernelGGL((igemm_cls4_kernel<bf16_t, 32, 256, BN_, 4, 1>), grid, dim3(256), 0, st, \
+                     as[0], as[1], as[2], as[3], s4, k4, ntn)
+  if (p0.bn == 16) UM_CLS4(16);
+  else if (p0.bn == 32) UM_CLS4(32);
+  else if (p0.bn == 48) UM_CLS4(48);
+  else UM_CLS4(64);
+#undef UM_CLS4
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("igemm_run_cls4: %s", hipGetErrorString(e));
+    return -UM_ERR_HIP;
+  }
+  return 1;
+}
+
 }  // namespace umamd
 
 // tuning knobs at run time (tests force code paths; sweeps): returns the old
@@ -1116,6 +1188,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "glds_deep")) f = &k.glds_deep;
   else if (!strcmp(key, "xcd_col")) f = &k.xcd_col;
   else if (!strcmp(key, "tappack")) f = &k.tappack;
+  else if (!strcmp(key, "cls4")) f = &k.cls4;
   else if (!strcmp(key, "glds_deep_blocks")) f = &k.glds_deep_blocks;
   else if (!strcmp(key, "fold_split_nc")) f = &k.fold_split_nc;
   if (!f) return -1;
