@@ -11,6 +11,8 @@
 // gate gradients reduced in-block then atomically added.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -108,63 +110,101 @@ __device__ __forceinline__ F8 src8(const CatSrc& s, long off, int cc) {
 // Vector loads for COPY/UP2 rows with ld % 8 == 0 or the 4-channel f32
 // disparity, and for PSHUF (the 32 source channels 4cc .. 4cc+31 holding
 // the group's sub-pixel values); per-element fallback otherwise.
+// the 8 channels [cc, cc+8) of source s at destination pixel (n, y, x)
+template <int OP>
+__device__ __forceinline__ void cat_vals(const CatSrc& s, int n, int y, int x, int H, int W,
+                                         int cc, float* v) {
+  const bool vec_ok = (OP == UM_CAT_PSHUF)
+                          ? ((s.ld & 7) == 0 && (s.C & 7) == 0)
+                          : ((s.ld & 7) == 0 || (s.C <= 4 && (s.ld & 3) == 0 && s.dtype == UM_F32));
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  if (!vec_ok) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (cc + e < s.C) v[e] = cat_value(s, n, y, x, H, W, cc + e);  // gate inside
+    return;
+  }
+  if (OP == UM_CAT_COPY) {
+    const F8 t = src8(s, ((long)(n * H + y) * W + x) * s.ld, cc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = t.v[e];
+  } else if (OP == UM_CAT_UP2) {
+    int y0, y1, x0, x1;
+    float ly, lx;
+    up_index(y, s.h, H, y0, y1, ly);
+    up_index(x, s.w, W, x0, x1, lx);
+    const long b = (long)n * s.h;
+    const F8 v00 = src8(s, ((b + y0) * s.w + x0) * s.ld, cc);
+    const F8 v01 = src8(s, ((b + y0) * s.w + x1) * s.ld, cc);
+    const F8 v10 = src8(s, ((b + y1) * s.w + x0) * s.ld, cc);
+    const F8 v11 = src8(s, ((b + y1) * s.w + x1) * s.ld, cc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = (1.f - ly) * ((1.f - lx) * v00.v[e] + lx * v01.v[e]) +
+             ly * ((1.f - lx) * v10.v[e] + lx * v11.v[e]);
+  } else {  // PSHUF: src [N][H/2][W/2][4C], channel 4c + (y&1)*2 + (x&1)
+    const long off = ((long)(n * s.h + (y >> 1)) * s.w + (x >> 1)) * s.ld + 4 * cc;
+    const int sub = (y & 1) * 2 + (x & 1);
+    float q[32];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ld8_any(s.ptr, off + 8 * j, s.dtype, q + 8 * j);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)  // selects, not a dynamically indexed register array
+      v[e] = sub == 0 ? q[4 * e] : sub == 1 ? q[4 * e + 1] : sub == 2 ? q[4 * e + 2] : q[4 * e + 3];
+  }
+  if (s.scale) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (cc + e < s.C) v[e] *= s.scale[n * s.C + cc + e];
+  }
+}
+
+// One launch per concat source: thread per (pixel, 8 destination channels)
+// of the source's span [coff, coff + ceil8(C)) (sources start at 8-aligned
+// offsets, so the spans tile the concat; lanes >= C are written as 0).
+// Grid (row items / 256, H, N).
 template <typename T, int OP>
 __global__ void __launch_bounds__(256) cat_src_kernel(CatSrc s, int N, int H, int W,
                                                        T* __restrict__ dst, int ld) {
   const int cg = (s.C + 7) / 8;
-  const long total = (long)N * H * W * cg;
-  const bool vec_ok = (OP == UM_CAT_PSHUF)
-                          ? ((s.ld & 7) == 0 && (s.C & 7) == 0)
-                          : ((s.ld & 7) == 0 || (s.C <= 4 && (s.ld & 3) == 0 && s.dtype == UM_F32));
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const int cc = (int)(i % cg) * 8;
-    const long pix = i / cg;
-    const int x = pix % W;
-    const int y = (pix / W) % H;
-    const int n = pix / ((long)W * H);
-    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (!vec_ok) {
+  const int y = blockIdx.y, n = blockIdx.z;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W * cg) return;
+  const int x = i / cg;
+  const int cc = (i - x * cg) * 8;
+  float v[8];
+  cat_vals<OP>(s, n, y, x, H, W, cc, v);
+  store8(dst + (((long)n * H + y) * W + x) * ld + s.coff + cc, v);
+}
+
+// ALL sources of a concat in one launch: thread per (pixel, 8-channel group
+// of the whole concat), so a pixel's Ctot channels leave as one contiguous
+// row from adjacent lanes (full cache lines, each written once) instead of
+// one partial-line pass per source.  Grid (W * Ctot/8 / 256, H, N).
+template <typename T>
+__global__ void __launch_bounds__(256) cat_all_kernel(CatArgs a, int N, int H, int W,
+                                                       T* __restrict__ dst, int ld, int ng) {
+  const int y = blockIdx.y, n = blockIdx.z;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W * ng) return;
+  const int x = i / ng;
+  const int gi = i - x * ng;
+  int k = 0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (cc + e < s.C) v[e] = cat_value(s, n, y, x, H, W, cc + e);  // gate inside
-    } else {
-      if (OP == UM_CAT_COPY) {
-        const F8 t = src8(s, ((long)(n * H + y) * W + x) * s.ld, cc);
+  for (int j = 1; j < MAX_SRC; ++j)
+    if (j < a.nsrc && a.s[j].coff <= gi * 8) k = j;
+  // constant-offset selects into the kernel arguments (no dynamic indexing)
+  const CatSrc* sp = &a.s[0];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = t.v[e];
-      } else if (OP == UM_CAT_UP2) {
-        int y0, y1, x0, x1;
-        float ly, lx;
-        up_index(y, s.h, H, y0, y1, ly);
-        up_index(x, s.w, W, x0, x1, lx);
-        const long b = (long)n * s.h;
-        const F8 v00 = src8(s, ((b + y0) * s.w + x0) * s.ld, cc);
-        const F8 v01 = src8(s, ((b + y0) * s.w + x1) * s.ld, cc);
-        const F8 v10 = src8(s, ((b + y1) * s.w + x0) * s.ld, cc);
-        const F8 v11 = src8(s, ((b + y1) * s.w + x1) * s.ld, cc);
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          v[e] = (1.f - ly) * ((1.f - lx) * v00.v[e] + lx * v01.v[e]) +
-                 ly * ((1.f - lx) * v10.v[e] + lx * v11.v[e]);
-      } else {  // PSHUF: src [N][H/2][W/2][4C], channel 4c + (y&1)*2 + (x&1)
-        const long off = ((long)(n * s.h + (y >> 1)) * s.w + (x >> 1)) * s.ld + 4 * cc;
-        const int sub = (y & 1) * 2 + (x & 1);
-        float q[32];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ld8_any(s.ptr, off + 8 * j, s.dtype, q + 8 * j);
-#pragma unroll
-        for (int e = 0; e < 8; ++e)  // selects, not a dynamically indexed register array
-          v[e] = sub == 0 ? q[4 * e] : sub == 1 ? q[4 * e + 1] : sub == 2 ? q[4 * e + 2] : q[4 * e + 3];
-      }
-      if (s.scale) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (cc + e < s.C) v[e] *= s.scale[n * s.C + cc + e];
-      }
-    }
-    store8(dst + pix * ld + s.coff + cc, v);
-  }
+  for (int j = 1; j < MAX_SRC; ++j) sp = k == j ? &a.s[j] : sp;
+  const CatSrc& s = *sp;
+  const int cc = gi * 8 - s.coff;
+  float v[8];
+  if (s.op == UM_CAT_COPY) cat_vals<UM_CAT_COPY>(s, n, y, x, H, W, cc, v);
+  else if (s.op == UM_CAT_UP2) cat_vals<UM_CAT_UP2>(s, n, y, x, H, W, cc, v);
+  else cat_vals<UM_CAT_PSHUF>(s, n, y, x, H, W, cc, v);
+  store8(dst + (((long)n * H + y) * W + x) * ld + gi * 8, v);
 }
 
 // ---- backward: RowMap blocks (channel groups x pixel lanes) over a chunk of
@@ -600,11 +640,17 @@ __global__ void __launch_bounds__(256) parts_accum_kernel(const float* __restric
   }
 }
 
-inline int grid_for(long n) {
-  long b = (n + 255) / 256;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  return (int)b;
+
+// knob UMAMD_CAT_FUSED (default 0): all sources of a concat in one launch.
+// Measured slower (decoder concats 514 -> 693 us per step, 716 -> 705
+// pairs/s): waves spanning several sources run every source's path, and the
+// per-source launches already write whole 16-byte lanes
+bool cat_fused() {
+  static const int v = [] {
+    const char* e = getenv("UMAMD_CAT_FUSED");
+    return e ? atoi(e) : 0;
+  }();
+  return v != 0;
 }
 
 }  // namespace
@@ -625,14 +671,30 @@ int um_concat_build(int dtype, int N, int H, int W, void* dst, int ld, int Ctot,
   }
   UM_CHECK_ARG(Ctot % 8 == 0 && ld % 8 == 0, "um_concat_build: Ctot/ld %% 8");
   int covered = 0;
+  if (cat_fused()) {
+    for (int i = 0; i < nsrc; ++i) {
+      UM_CHECK_ARG(a.s[i].coff == covered && a.s[i].coff % 8 == 0,
+                   "um_concat_build: source %d must start at the 8-aligned end of the previous", i);
+      covered = a.s[i].coff + (a.s[i].C + 7) / 8 * 8;
+    }
+    UM_CHECK_ARG(covered == Ctot, "um_concat_build: sources cover %d of %d channels", covered, Ctot);
+    const int ng = Ctot / 8;
+    const dim3 g(ceil_div((long)W * ng, 256), H, N);
+    if (dtype == UM_BF16)
+      hipLaunchKernelGGL(cat_all_kernel<bf16_t>, g, dim3(256), 0, st, a, N, H, W, (bf16_t*)dst, ld, ng);
+    else
+      hipLaunchKernelGGL(cat_all_kernel<float>, g, dim3(256), 0, st, a, N, H, W, (float*)dst, ld, ng);
+    UM_LAUNCH_CHECK();
+    return UM_OK;
+  }
   for (int i = 0; i < nsrc; ++i) {
     const CatSrc& s = a.s[i];
     UM_CHECK_ARG(s.coff == covered && s.coff % 8 == 0,
                  "um_concat_build: source %d must start at the 8-aligned end of the previous", i);
     covered = s.coff + (s.C + 7) / 8 * 8;
-    const int g = grid_for((long)N * H * W * ((s.C + 7) / 8));
+    const dim3 g(ceil_div((long)W * ((s.C + 7) / 8), 256), H, N);
 #define CAT_LAUNCH(T, OP) \
-  hipLaunchKernelGGL((cat_src_kernel<T, OP>), dim3(g), dim3(256), 0, st, s, N, H, W, (T*)dst, ld)
+  hipLaunchKernelGGL((cat_src_kernel<T, OP>), g, dim3(256), 0, st, s, N, H, W, (T*)dst, ld)
     if (dtype == UM_BF16) {
       if (s.op == UM_CAT_COPY) CAT_LAUNCH(bf16_t, UM_CAT_COPY);
       else if (s.op == UM_CAT_UP2) CAT_LAUNCH(bf16_t, UM_CAT_UP2);
