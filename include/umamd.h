@@ -70,6 +70,11 @@ int um_conv_stats_parts(int M, int K);
  * Passing a smaller (or null) workspace is allowed: the split shrinks. */
 long um_conv_fwd_ws(int dtype, int N, int P, int Q, int K, int R, int C);
 long um_conv_dgrad_ws(int dtype, int N, int H, int W, int C, int R, int K, int stride);
+/* as um_conv_dgrad_ws, plus the padded-input buffer of the reflect data
+ * gradient's padded form (knob "pad_dgrad"): a zero-pad transposed conv onto
+ * the (H+2p) x (W+2p) reflect-padded input, folded back onto dx */
+long um_conv_dgrad_ws_pad(int dtype, int N, int H, int W, int C, int R, int K, int stride,
+                          int pad, int pad_mode);
 
 int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                   const void* wf, const float* bias, int K, int R, int stride,

@@ -489,10 +489,13 @@ def test_dgrad_reflect(dtype, case):
     _, wT = U._pack(w.to(DEV), C, dtype, wf=False)
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     # default plan, the halo kernel wherever it applies, then the one-pass
-    # fold and the split form forced
-    for hmin, snc in ((256, 64), (1, 64), (256, 0), (256, 4096)):
+    # fold, the split form and the padded form (zero-pad transposed conv onto
+    # the padded input + reflect fold pass) forced
+    for hmin, snc, pd in ((256, 64, 1), (1, 64, 1), (256, 0, 0), (256, 4096, 1), (256, 64, 2),
+                          (1, 64, 2)):
         old = lib().um_set_tuning(b'halo_min_tiles', hmin)
         old_s = lib().um_set_tuning(b'fold_split_nc', snc)
+        old_p = lib().um_set_tuning(b'pad_dgrad', pd)
         try:
             dx = _nhwc(dx0).to(dtype).contiguous() if accumulate else None
             out = U._conv_dgrad(_nhwc(dy).to(dtype), wT, (N, H, W, C), K, R, 1, pad, PAD_REFLECT,
@@ -501,9 +504,10 @@ def test_dgrad_reflect(dtype, case):
         finally:
             lib().um_set_tuning(b'halo_min_tiles', old)
             lib().um_set_tuning(b'fold_split_nc', old_s)
+            lib().um_set_tuning(b'pad_dgrad', old_p)
         err = _rel(_nchw(out), ref)
-        print(f'dgrad_reflect {case} {dtype} halo_min_tiles={hmin} fold_split_nc={snc}: '
-              f'rel {err:.3e}')
+        print(f'dgrad_reflect {case} {dtype} halo_min_tiles={hmin} fold_split_nc={snc} '
+              f'pad_dgrad={pd}: rel {err:.3e}')
         assert err < tol, err
 
 

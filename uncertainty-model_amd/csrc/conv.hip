@@ -555,9 +555,74 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ y, in
 // out[c] (+)= sum_r p[r*stride + c]: block = cl channel lanes (cl = C up to
 // 64, power of two) x 256/cl row lanes, 8 independent accumulators per
 // thread, f64 lane combine
+// Reflect-pad data gradient, padded form: dxp[n][Y][X] (the gradient of the
+// reflect-padded input, (H+2p) x (W+2p), from a zero-pad transposed conv
+// on the fast GEMM paths) folded onto dx: x_pad[Y] = x[refl(Y - p)], so
+// dx[i] sums dxp[i + p], dxp[p - i] (1 <= i <= p) and dxp[2(H-1) + p - i]
+// (H-1-p <= i <= H-2), separably in y and x.  Thread per (pixel, 8 channels).
+template <typename T>
+__global__ void __launch_bounds__(256) reflect_fold_kernel(const T* __restrict__ dxp, int N, int H,
+                                                           int W, int C, int p, T* __restrict__ dx,
+                                                           int ldx, int accumulate) {
+  const int cg = C / 8;
+  const int y = blockIdx.y, n = blockIdx.z;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W * cg) return;
+  const int x = i / cg, c = (i - x * cg) * 8;
+  const int Hp = H + 2 * p, Wp = W + 2 * p;
+  int ys[3], xs[3], ny = 0, nx = 0;
+  ys[ny++] = y + p;
+  if (y >= 1 && y <= p) ys[ny++] = p - y;
+  if (y >= H - 1 - p && y <= H - 2) ys[ny++] = 2 * (H - 1) + p - y;
+  xs[nx++] = x + p;
+  if (x >= 1 && x <= p) xs[nx++] = p - x;
+  if (x >= W - 1 - p && x <= W - 2) xs[nx++] = 2 * (W - 1) + p - x;
+  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const T* base = dxp + (long)n * Hp * Wp * C + c;
+  for (int u = 0; u < ny; ++u)
+    for (int q = 0; q < nx; ++q) {
+      float t[8];
+      load8(base + ((long)ys[u] * Wp + xs[q]) * C, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+  T* o = dx + (((long)n * H + y) * W + x) * ldx + c;
+  if (accumulate) {
+    float t[8];
+    load8(o, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  store8(o, v);
+}
+
+// the padded form applies (knob pad_dgrad: 0 off, 1 for dx wider than
+// fold_split_nc -- the layers the one-pass fold gather served --, 2 all)
+bool pad_dgrad_applies(int C, int pad, int pad_mode, int stride, int P, int Q, int H, int W) {
+  const int kn = umamd::igemm_pad_dgrad();
+  if (kn == 0 || pad_mode != UM_PAD_REFLECT || stride != 1 || pad <= 0 || pad >= H || pad >= W) return false;
+  if (P != H || Q != W || C % 8) return false;
+  return kn == 2 || C > umamd::igemm_fold_split_nc();
+}
+
+long pad_dgrad_bytes(int dtype, int N, int H, int W, int C, int R, int K, int pad, long* gemm_off) {
+  const long Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const long esz = dtype == UM_BF16 ? 2 : 4;
+  const long buf = (N * Hp * Wp * C * esz + 255) / 256 * 256;
+  if (gemm_off) *gemm_off = buf;
+  return buf + umamd::igemm_ws_bytes(dtype, (int)(N * Hp * Wp), C, R * R, K);
+}
+
 }  // namespace
 
 extern "C" {
+
+long um_conv_dgrad_ws_pad(int dtype, int N, int H, int W, int C, int R, int K, int stride, int pad,
+                          int pad_mode) {
+  const long base = um_conv_dgrad_ws(dtype, N, H, W, C, R, K, stride);
+  if (!pad_dgrad_applies(C, pad, pad_mode, stride, H, W, H, W)) return base;
+  return std::max(base, pad_dgrad_bytes(dtype, N, H, W, C, R, K, pad, nullptr));
+}
 
 int um_conv_stats_parts(int M, int K) {
   return ceil_div(M, umamd::igemm_stats_rows(M, K));
@@ -616,6 +681,35 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
     UM_CHECK_ARG(P == H + 2 * pad - R + 1 && Q == W + 2 * pad - R + 1, "um_conv2d_dgrad: size");
     UM_CHECK_ARG(pad_mode == UM_PAD_ZERO || (P == H && Q == W && pad <= 1),
                  "um_conv2d_dgrad: reflect transpose needs a same-size conv with pad <= 1");
+    long goff = 0;
+    if (pad_dgrad_applies(C, pad, pad_mode, stride, P, Q, H, W) && ws != nullptr &&
+        ws_bytes >= pad_dgrad_bytes(dtype, N, H, W, C, R, K, pad, &goff)) {
+      // padded form: zero-pad transposed conv onto the (H+2p) x (W+2p) padded
+      // input (halo / LDS-DMA / register GEMM paths), then the reflect fold
+      const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+      umamd::IgArgs a{};
+      a.a = dy; a.ah = P; a.aw = Q; a.ach = K; a.lda = ldy;
+      a.on = N; a.oh = Hp; a.ow = Wp;
+      a.R = R; a.stride = 1; a.pad = R - 1;
+      a.Rx = R; a.padx = R - 1; a.tsign = 1; a.wR = R;
+      a.pmode = umamd::IG_PAD_ZERO; a.fold_pad = 0; a.flip = 1;
+      a.b = wT; a.ldb = (long)R * R * K;
+      a.NC = C; a.M = N * Hp * Wp;
+      a.bias = nullptr; a.out = ws; a.ld_out = C; a.out_f32 = (dtype == UM_F32);
+      a.epilogue = UM_EPI_NONE; a.accumulate = 0; a.epi_scale = 1.f;
+      a.residual = nullptr; a.ldr = 0; a.stats = nullptr;
+      int rc = umamd::igemm_run(dtype, a, reinterpret_cast<float*>((char*)ws + goff), ws_bytes - goff, st);
+      if (rc != UM_OK) return rc;
+      const dim3 g(ceil_div((long)W * (C / 8), 256), H, N);
+      if (dtype == UM_BF16)
+        hipLaunchKernelGGL(reflect_fold_kernel<bf16_t>, g, dim3(256), 0, st, (const bf16_t*)ws, N, H, W,
+                           C, pad, (bf16_t*)dx, ldx, accumulate);
+      else
+        hipLaunchKernelGGL(reflect_fold_kernel<float>, g, dim3(256), 0, st, (const float*)ws, N, H, W,
+                           C, pad, (float*)dx, ldx, accumulate);
+      UM_LAUNCH_CHECK();
+      return UM_OK;
+    }
     umamd::IgArgs a{};
     a.a = dy; a.ah = P; a.aw = Q; a.ach = K; a.lda = ldy;
     a.on = N; a.oh = H; a.ow = W;

@@ -63,6 +63,10 @@ int igemm_run_cls4(int dtype, IgArgs (&as)[4], hipStream_t st);
 // "fold_split_nc", UMAMD_FOLD_SPLIT_NC)
 int igemm_fold_split_nc();
 
+// reflect data gradients in the padded form (knob pad_dgrad): 0 off, 1 for
+// dx wider than fold_split_nc, 2 all
+int igemm_pad_dgrad();
+
 // fill the border-list fields of a (oh, ow, fold_pad set) and return the
 // number of listed pixels per image
 int igemm_border_list(IgArgs& a);

@@ -862,6 +862,7 @@ struct Knobs {
   int xcd_col;
   int tappack;
   int cls4;
+  int pad_dgrad;
   int fold_split_nc;
   Knobs() {
     auto env = [](const char* n, int d) {
@@ -909,6 +910,9 @@ struct Knobs {
     tappack = env("UMAMD_IG_TAPPACK", 1);
     // the four parity classes of a stride-2 data gradient as one launch
     cls4 = env("UMAMD_IG_CLS4", 1);
+    // reflect data gradient as a zero-pad transposed conv onto the padded
+    // input + a fold pass (0 off, 1 the wide layers, 2 all)
+    pad_dgrad = env("UMAMD_IG_PAD_DGRAD", 1);
     // per conv (tools/conv_table.py): split form 256x512 C48 171 -> 117 us,
     // C32 K8 125 -> 85; one pass stays ahead from C = 128 up (16x32 C640:
     // 106 vs 140, 8x16 C512: 53 vs 79)
@@ -1072,6 +1076,7 @@ int dispatch_tiles(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
 namespace umamd {
 
 int igemm_fold_split_nc() { return knobs().fold_split_nc; }
+int igemm_pad_dgrad() { return knobs().pad_dgrad; }
 
 int igemm_border_list(IgArgs& a) {
   const int H = a.oh, W = a.ow, p = a.fold_pad;
@@ -1189,6 +1194,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "xcd_col")) f = &k.xcd_col;
   else if (!strcmp(key, "tappack")) f = &k.tappack;
   else if (!strcmp(key, "cls4")) f = &k.cls4;
+  else if (!strcmp(key, "pad_dgrad")) f = &k.pad_dgrad;
   else if (!strcmp(key, "glds_deep_blocks")) f = &k.glds_deep_blocks;
   else if (!strcmp(key, "fold_split_nc")) f = &k.fold_split_nc;
   if (!f) return -1;

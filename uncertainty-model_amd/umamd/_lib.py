@@ -44,6 +44,7 @@ _SIG = {
                              _P, _I, _P, _L, 's']),
     'um_conv_fwd_ws': (_L, [_I, _I, _I, _I, _I, _I, _I]),
     'um_conv_dgrad_ws': (_L, [_I, _I, _I, _I, _I, _I, _I, _I]),
+    'um_conv_dgrad_ws_pad': (_L, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     'um_conv_wgrad_splits': (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     'um_conv2d_wgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I,
                              _P, _I, 's']),

@@ -103,7 +103,7 @@ def _conv_dgrad(dy, wT, x_shape, K, R, stride, pad, pad_mode, dx=None, accumulat
     _, P, Q, ldy = dy.shape
     if dx is None:
         dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
-    wsb = query('um_conv_dgrad_ws', _dt(dy), N, H, W, C, R, K, stride)
+    wsb = query('um_conv_dgrad_ws_pad', _dt(dy), N, H, W, C, R, K, stride, pad, pad_mode)
     ws = torch.empty((wsb // 4,), dtype=torch.float32, device=dy.device) if wsb else None
     call('um_conv2d_dgrad', _dt(dy), N, H, W, C, C, ptr(dx), int(accumulate), ptr(wT), K, R,
          stride, pad, pad_mode, P, Q, ptr(dy), ldy, ptr(ws), wsb,
