@@ -15,6 +15,8 @@
 // model/layers/decoder.py:82): biased variance for normalisation, unbiased
 // for running_var, eps 1e-5, momentum 0.1.  ELU alpha = 1 (nn.ELU, reference
 // model/layers/encoder.py:44, decoder.py:84).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -146,6 +148,20 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
       if (rm.lane == 0 && g < cg) store8(pool + (long)blockIdx.x * C + g * 8, ps);
     }
   }
+}
+
+// rows per backward block: the row-chunk sizing of common.h (about 512
+// blocks, 16..max rows) with the cap as a knob (UMAMD_BN_BWD_ROWS_MAX,
+// default 1024 = rows_per_part)
+static int bn_bwd_rows(long M) {
+  static const int cap = [] {
+    const char* e = getenv("UMAMD_BN_BWD_ROWS_MAX");
+    return e ? atoi(e) : 1024;
+  }();
+  const long r = (M + 511) / 512;
+  int p = 16;
+  while (p < r && p < cap) p <<= 1;
+  return p;
 }
 
 // rows per forward block: ~2048 blocks over the chip, >= 16 rows each; with
@@ -537,7 +553,7 @@ int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const 
                        fin, st);
 }
 
-int um_bn_bwd_parts(long M) { return parts_for(M); }
+int um_bn_bwd_parts(long M) { return ceil_div(M, bn_bwd_rows(M)); }
 
 static int bwd_reduce_launch(int dtype, long M, int C, long HW, const void* da, int ldda,
                              const void* y, int ldy, const float* mean, const float* invstd,
@@ -550,11 +566,11 @@ static int bwd_reduce_launch(int dtype, long M, int C, long HW, const void* da, 
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
                        (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M), fin, slots);
+                       scale, shift, add_nc, apply_elu, parts, bn_bwd_rows(M), fin, slots);
   else
     hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), shm, st,
                        (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, rows_per_part(M), fin, slots);
+                       scale, shift, add_nc, apply_elu, parts, bn_bwd_rows(M), fin, slots);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -626,12 +642,12 @@ static int bwd_apply_launch(int dtype, long M, int C, long HW, const void* da, i
     hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
                        (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
                        scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy, sum_parts,
-                       rows_per_part(M), fin);
+                       bn_bwd_rows(M), fin);
   else
     hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, dim3(blocks), dim3(256), shm, st,
                        (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
                        scale, shift, add_nc, apply_elu, k1, k2, k3, (float*)dy, lddy, sum_parts,
-                       rows_per_part(M), fin);
+                       bn_bwd_rows(M), fin);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
