@@ -48,15 +48,55 @@ def parse():
     ap.add_argument('--config', default='config.yml')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--no-loss-delta', action='store_true',
+                    help='skip the loss-delta-vs-reference leg (fp32 + bf16 10-step trajectories)')
     ap.add_argument('--no-graph', action='store_true',
                     help='eager launches instead of the captured HIP graph')
     ap.add_argument('--eager-steps', type=int, default=3,
                     help='N=1: also time this many eagerly launched steps (reported beside)')
-    ap.add_argument('--cpu-steps', type=int, default=5,
+    ap.add_argument('--cpu-steps', type=int, default=2,
                     help='CPU baseline: best of this many timed steps per shape (BASELINE.md)')
     ap.add_argument('--fp32-steps', type=int, default=5,
                     help='N=1: also time the fp32 (parity-mode) captured step, reported beside')
     return ap.parse_args()
+
+
+def spawn_ranks(n: int, cmd=None) -> int:
+    """``--gpus N`` without a launcher: start N copies of this script as
+    rank processes (one GPU each, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in
+    their environment; reference parallel_main.py:265-279 does the same with
+    mp.spawn) before this process touches the GPU, wait for all of them and
+    return the worst exit status.  Rank 0 prints the JSON line."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        argv = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+        procs.append(subprocess.Popen(argv, env=env, start_new_session=True))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in procs:  # one rank failed: the others would hang
+                        os.killpg(q.pid, signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+    return rc if rc >= 0 else 128 - rc
 
 
 def load_cfg(path, loss_type):
@@ -69,7 +109,7 @@ def load_cfg(path, loss_type):
     return cfg
 
 
-def build(cfg, dtype, device, world, dp=None):
+def build(cfg, dtype, device, world, dp=None, stream=None):
     import model as M
     from train.loss import TukraUncertaintyLoss
     from umamd.optim import Adam
@@ -79,7 +119,7 @@ def build(cfg, dtype, device, world, dp=None):
         dp = world > 1
     if dp:
         from train.parallel import data_parallel
-        m = data_parallel(m, device.index)
+        m = data_parallel(m, device.index, stream=stream)
     lf = TukraUncertaintyLoss(**cfg['loss'])
     opt = Adam(m.parameters(), 1e-4)
     return m, lf, opt
@@ -107,7 +147,10 @@ def baseline_config(a, world, cfg):
         return '5'
     if (a.height, a.width) == (128, 256):
         return '1'
-    return '2' if world == 1 else '4'
+    if world == 1:
+        return '2'
+    # C4: 8 GPUs x B=8 (global 64); N=2/4 run C4's per-GPU shape
+    return '4' if world == 8 else f'4 per-GPU shape, {world} GPUs'
 
 
 def time_eager(m, lf, opt, left, right, scale, batch, steps):
@@ -261,32 +304,43 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
 
 # --------------------------------------------------------- CPU baseline ----
 def _cpu_step_rate(cfg, H, W, batch, steps, seed=1234):
-    """best-of-``steps`` oracle train steps (1 warm-up) -> (pairs/s, s/step)"""
+    """best-of-``steps`` oracle train steps (1 warm-up) -> (pairs/s, s/step,
+    step-0 losses).  The warm-up step is step 0 from the formula weights on
+    the bench's own synthetic pair (oracle.step.bench_inputs), so its losses
+    are the oracle's side of the loss delta."""
     from oracle import model as OM, step as OS
     graphs = OM.load_stage_graphs(cfg['model']['encoder'])
     P = OS.formula_state_dict(OS.param_specs(cfg['model'], graphs))
-    g = torch.Generator().manual_seed(seed)
-    left = torch.rand(batch, 3, H, W, generator=g)
-    right = torch.rand(batch, 3, H, W, generator=g)
+    left, right = OS.bench_inputs(batch, H, W, seed)
     st = {}
-    OS.train_step(P, left, right, 0.3, cfg['model'], cfg['loss'], graphs, st)  # warm-up
+    r0 = OS.train_step(P, left, right, 0.3, cfg['model'], cfg['loss'], graphs, st)
     best = float('inf')
     for _ in range(steps):
         t0 = time.perf_counter()
         OS.train_step(P, left, right, 0.3, cfg['model'], cfg['loss'], graphs, st)
         best = min(best, time.perf_counter() - t0)
-    return batch / best, best
+    return batch / best, best, (r0['disp_loss'], r0['error_loss'])
 
 
 def cpu_baseline(config, steps):
     """The oracle's CPU train step (plain-PyTorch restatement of the
     reference, pinned to its goldens) on the host cores, BASELINE.md
-    protocol: C2 (B=8 256x512 bayesian, the GPU workload's shape; ``value``)
-    and C1 (B=2 128x256 l1), 1 warm-up + best of ``steps`` each."""
-    threads = min(os.cpu_count() or 1, 64)
+    protocol.  The thread count is swept (4..64) on C1 (B=2 128x256 l1, 1
+    warm-up + best of 2) and the best one times C2 (B=8 256x512 bayesian, the
+    GPU workload's shape: ``value``), 1 warm-up + best of ``steps``.  On the
+    GPU box os.cpu_count() shows the whole machine while a job's share is
+    smaller, so the sweep, not the core count, picks the threads."""
+    ncpu = os.cpu_count() or 1
+    counts = [t for t in (4, 8, 16, 32, 64) if t <= ncpu] or [ncpu]
+    sweep = {}
+    cfg1 = load_cfg(config, 'l1')
+    for t in counts:
+        torch.set_num_threads(t)
+        r, _, _ = _cpu_step_rate(cfg1, 128, 256, 2, 2)
+        sweep[t] = round(r, 3)
+    threads = max(sweep, key=sweep.get)
     torch.set_num_threads(threads)
-    c2, t2 = _cpu_step_rate(load_cfg(config, 'bayesian'), 256, 512, 8, steps)
-    c1, t1 = _cpu_step_rate(load_cfg(config, 'l1'), 128, 256, 2, steps)
+    c2, t2, ref0 = _cpu_step_rate(load_cfg(config, 'bayesian'), 256, 512, 8, steps)
     cpu = ''
     try:
         with open('/proc/cpuinfo') as f:
@@ -298,9 +352,70 @@ def cpu_baseline(config, steps):
         pass
     return {'value': round(c2, 3), 'unit': 'stereo-pairs/sec', 'cores': threads, 'kind': 'port',
             'sample': f'oracle fp32 train step, C2 B=8 256x512 bayesian, 1 warm-up + best of '
-                      f'{steps} ({t2:.2f} s/step); {cpu}',
-            'c1': {'value': round(c1, 3), 'unit': 'stereo-pairs/sec',
-                   'sample': f'C1 B=2 128x256 l1, best of {steps} ({t1:.3f} s/step)'}}
+                      f'{steps} ({t2:.2f} s/step) at the best thread count of a C1 sweep; {cpu}',
+            'c1_thread_sweep_pairs_per_s': sweep}, ref0
+
+
+# ------------------------------------------------------------ loss delta ----
+def _golden_traj():
+    path = os.path.join(REPO, 'tests', 'golden', 'traj_c2.npz')
+    if not os.path.exists(path):
+        return None
+    import numpy as np
+    z = np.load(path)
+    n = sum(1 for k in z.files if k.startswith('disp_loss_'))
+    return [(float(z[f'disp_loss_{i}']), float(z[f'error_loss_{i}'])) for i in range(n)]
+
+
+def loss_trajectory(cfg, dtype, device, steps):
+    """``steps`` captured train steps of a ``dtype`` model with the formula
+    weights on the bench's synthetic pair (C2: B=8 256x512 bayesian, scale
+    0.3) -> [(disp_loss, error_loss)] per step."""
+    from oracle import model as OM, step as OS
+    from train.graph import CapturedTrainStep
+    graphs = OM.load_stage_graphs(cfg['model']['encoder'])
+    sd = OS.formula_state_dict(OS.param_specs(cfg['model'], graphs))
+    left, right = OS.bench_inputs(8, 256, 512)
+    left, right = left.to(device), right.to(device)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        m, lf, opt = build(cfg, dtype, device, 1, False)
+        m.load_state_dict(sd)
+    torch.cuda.current_stream().wait_stream(st)
+    cap = CapturedTrainStep(m, lf, opt, left, right, 0.3, warmup=1, stream=st)
+    out = []
+    for _ in range(steps):
+        dl, el = cap()
+        out.append((float(dl), float(el)))
+    del cap, m, lf, opt
+    torch.cuda.synchronize()
+    return out
+
+
+def loss_delta(cfg, device, ref0):
+    """BASELINE metric's "loss delta vs ref" (SURVEY 8d): |loss - ref| / |ref|
+    of both scalars, at C2 with identical inputs and weights.  ``step0``
+    against the oracle's fp32 step 0 timed in the cpu_baseline leg (None
+    when that leg did not run); ``traj`` over the reference's own 10-step fp32
+    trajectory (tests/golden/traj_c2.npz, made by importing the reference)."""
+    gold = _golden_traj()
+    nsteps = len(gold) if gold else 1
+    res = {'config': 'C2 B=8 256x512 bayesian, formula weights, bench synthetic pair, scale 0.3'}
+    for dt in ('fp32', 'bf16'):
+        tr = loss_trajectory(cfg, dt, device, nsteps)
+        r = {'step0': {'disp': tr[0][0], 'error': tr[0][1]}}
+        if ref0 is not None:
+            r['step0_vs_oracle'] = {'disp': abs(tr[0][0] / ref0[0] - 1),
+                                    'error': abs(tr[0][1] / ref0[1] - 1)}
+        if gold:
+            dd = [abs(a[0] / b[0] - 1) for a, b in zip(tr, gold)]
+            de = [abs(a[1] / b[1] - 1) for a, b in zip(tr, gold)]
+            r['vs_reference_traj'] = {'steps': len(gold), 'step0_disp': dd[0], 'step0_error': de[0],
+                                      'max_disp': max(dd), 'max_error': max(de)}
+        res[dt] = r
+    if gold:
+        res['reference_step0'] = {'disp': gold[0][0], 'error': gold[0][1]}
+    return res
 
 
 def time_fp32(cfg, device, left, right, scale, batch, warmup, steps):
@@ -325,7 +440,12 @@ def time_fp32(cfg, device, left, right, scale, batch, warmup, steps):
 
 def main():
     a = parse()
+    if a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(spawn_ranks(a.gpus))
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if 'WORLD_SIZE' in os.environ and a.gpus not in (1, world):
+        print(f'bench: --gpus {a.gpus} but WORLD_SIZE={world}; using {world} ranks',
+              file=sys.stderr)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     # UMAMD_DIST=1 (under torchrun) runs the data-parallel path even with one
@@ -346,29 +466,53 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device('cuda', local)
     cfg = load_cfg(a.config, a.loss_type)
-    use_graph = not a.no_graph
+    backend = dist.get_backend() if dp else None
+    # a gloo collective (host-staged) cannot be captured in a HIP graph: the
+    # gloo rehearsal of the N>1 path steps eagerly
+    use_graph = not a.no_graph and backend in (None, 'nccl')
     # the graph is captured on this stream; DDP is constructed under it (it
     # keeps the parameters' AccumulateGrad nodes, which remember their stream)
     cap_stream = torch.cuda.Stream() if use_graph else torch.cuda.current_stream()
     with torch.cuda.stream(cap_stream):
-        m, lf, opt = build(cfg, a.dtype, device, world, dp)
+        m, lf, opt = build(cfg, a.dtype, device, world, dp, stream=cap_stream)
     torch.cuda.current_stream().wait_stream(cap_stream)
     g = torch.Generator(device='cpu').manual_seed(1234 + rank)
     left = torch.rand(a.batch, 3, a.height, a.width, generator=g).to(device)
     right = torch.rand(a.batch, 3, a.height, a.width, generator=g).to(device)
     scale = 0.3  # adjust_disparity(0)
 
+    launch = 'hip-graph' if use_graph else 'eager'
+    run = None
     if use_graph:
         from train.graph import CapturedTrainStep
         # the capture's own eager warm-up steps count toward W; one replay warms the graph
         # (N>1: SyncBN and the gradient all-reduce are RCCL nodes inside the graph)
-        cap = CapturedTrainStep(m, lf, opt, left, right, scale, warmup=max(1, a.warmup - 1),
-                                stream=cap_stream)
-        run = cap
-        run()
-    else:
+        err = None
+        try:
+            cap = CapturedTrainStep(m, lf, opt, left, right, scale, warmup=max(1, a.warmup - 1),
+                                    stream=cap_stream)
+            run = cap
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+            err = f'{type(e).__name__}: {e}'[:300]
+            print(f'bench rank {rank}: capture failed: {err}', file=sys.stderr)
+        if world > 1:  # every rank takes the same path, or the collectives hang
+            ok = torch.tensor([0 if run is None else 1], dtype=torch.int32, device=device)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok) == 0:
+                run = None
+                err = err or 'capture failed on another rank'
+        if run is None:
+            launch = f'eager (capture failed: {err})'
+            use_graph = False
+        else:
+            run()
+    if run is None:
+        with torch.cuda.stream(cap_stream):
+            opt.zero_grad(set_to_none=True)
+
         def run():
-            return step(m, lf, opt, left, right, scale)
+            with torch.cuda.stream(cap_stream):
+                return step(m, lf, opt, left, right, scale)
         for _ in range(a.warmup):
             run()
     torch.cuda.synchronize()
@@ -389,9 +533,9 @@ def main():
         elapsed = float(t)
     losses = (float(dl.detach()), float(el.detach()))
 
-    # the eager comparison and the roofline pass: N>1 launches on the stream
-    # DDP was built under (it keeps AccumulateGrad nodes bound to it)
-    with torch.cuda.stream(cap_stream if dp else torch.cuda.current_stream()):
+    # the eager comparison and the roofline pass run on the stream the model
+    # was built on (DDP keeps AccumulateGrad nodes bound to it)
+    with torch.cuda.stream(cap_stream):
         eager = None
         if use_graph and world == 1 and a.eager_steps > 0:
             eager = time_eager(m, lf, opt, left, right, scale, a.batch, a.eager_steps)
@@ -402,9 +546,13 @@ def main():
     fp32 = None
     if world == 1 and a.dtype == 'bf16' and a.fp32_steps > 0:
         fp32 = time_fp32(cfg, device, left, right, scale, a.batch, 2, a.fp32_steps)
-    cpu = None
+    cpu, ref0 = None, None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a.config, a.cpu_steps)
+        cpu, ref0 = cpu_baseline(a.config, a.cpu_steps)
+    delta = None
+    if rank == 0 and world == 1 and not a.no_loss_delta and \
+            (a.height, a.width, a.batch, a.loss_type) == (256, 512, 8, 'bayesian'):
+        delta = loss_delta(load_cfg(a.config, 'bayesian'), device, ref0)
 
     if rank == 0:
         total = a.batch * world * a.steps
@@ -423,12 +571,15 @@ def main():
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch,
                        'height': a.height, 'width': a.width, 'loss': a.loss_type,
                        'parallelism': f'dp{world}' + ('+syncbn' if dp else ''),
-                       'launch': 'hip-graph' if use_graph else 'eager',
+                       'process_group': ({'backend': backend, 'world_size': dist.get_world_size()}
+                                         if dp else None),
+                       'launch': launch,
                        'graph': f'{a.config} (nodes={cfg["model"]["encoder"].get("nodes")} '
                                 f'stage graphs)'},
             'eager_launch': eager,
             'fp32_line': fp32,
             'final_losses': {'disp': round(losses[0], 5), 'error': round(losses[1], 5)},
+            'loss_delta': delta,
             'roofline': roof,
             'cpu_baseline': cpu,
         }

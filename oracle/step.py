@@ -185,6 +185,34 @@ def train_step(P: Dict[str, torch.Tensor], left, right, scale, model_cfg, loss_c
     for v in trainable.values():
         v.requires_grad_(False)
     adam_update(trainable, grads, adam_state, lr)
-    return {'disp_loss': float(dl), 'error_loss': float(el),
+    return {'disp_loss': float(dl.detach()), 'error_loss': float(el.detach()),
             'terms': {k: float(v) for k, v in terms.items()},
             'grads': grads, 'disps': [d.detach() for d in disps]}
+
+
+SKETCHES = 8
+
+
+def grad_sketch(name: str, g: torch.Tensor, k: int = SKETCHES) -> torch.Tensor:
+    """k Rademacher projections <g, r_j> of one gradient tensor, r_j in
+    {-1,+1}^numel drawn from a CPU generator seeded by (crc32(name), j): a
+    direction-sensitive fingerprint (a wrong direction with the right norm
+    changes it) that goldens can store in 8 doubles per parameter.
+    ||sketch(g) - sketch(g_ref)|| / ||sketch(g_ref)|| estimates the rel-norm
+    ||g - g_ref|| / ||g_ref||."""
+    x = g.detach().to('cpu', torch.float64).reshape(-1)
+    base = zlib.crc32(name.encode())
+    out = torch.empty(k, dtype=torch.float64)
+    for j in range(k):
+        gen = torch.Generator().manual_seed(base * 16 + j)
+        r = torch.randint(0, 2, (x.numel(),), generator=gen, dtype=torch.int8)
+        out[j] = (x * (r.to(torch.float64) * 2 - 1)).sum()
+    return out
+
+
+def bench_inputs(batch: int, height: int, width: int, seed: int = 1234):
+    """the bench's synthetic pair (bench.py: U[0,1) from a CPU generator)"""
+    g = torch.Generator(device='cpu').manual_seed(seed)
+    left = torch.rand(batch, 3, height, width, generator=g)
+    right = torch.rand(batch, 3, height, width, generator=g)
+    return left, right

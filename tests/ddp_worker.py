@@ -73,12 +73,34 @@ def run_cpu(rank, world, out):
     net[1](net[0](x)).sum().backward()
     cs = CapturedTrainStep.__new__(CapturedTrainStep)
     cs.model, cs.group, cs.world = net, dist.group.WORLD, world
-    cs._flat = cs._layout = cs._raw = None
+    cs._buckets = None
     cs._reduce_grads()
+    # bucketed exchange from the backward's hooks (umamd.gradsync): 3 buckets
+    # of this net, launched in backward order as each one's gradients land
+    from umamd.gradsync import GradBuckets
+    torch.manual_seed(0)
+    net2 = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Linear(16, 4),
+                               torch.nn.Linear(4, 4))
+    gb = GradBuckets(net2.parameters(), dist.group.WORLD, world, cap_mb=80 / 2 ** 20)
+    order = []
+    orig_launch = gb._launch
+    gb._launch = lambda bi: (order.append(bi), orig_launch(bi))
+    for it in range(2):  # step 1 learns the layout (reduced in finish); step 2 from hooks
+        for p in net2.parameters():
+            p.grad = None
+        order.clear()
+        gb.arm()
+        net2[2](net2[1](net2[0](x))).sum().backward()
+        launched_in_backward = list(order)
+        gb.finish()
+    bucket_grads = [p.grad.clone() for p in net2.parameters()]
+    assert launched_in_backward == list(range(len(gb.buckets))) and len(gb.buckets) >= 3, \
+        (launched_in_backward, [len(b) for b in gb.buckets])
     flat_grads = [p.grad.clone() for p in list(net.parameters())[:4]]
     assert all(p.grad is None for p in net[2].parameters())
     assert all(p.grad.data_ptr() >= cs._flat.data_ptr() for p in list(net.parameters())[:4])
-    torch.save({'flat_grads': flat_grads,'n_sync_bn': torch.tensor(count_sync_bn(sm)),
+    torch.save({'flat_grads': flat_grads, 'bucket_grads': bucket_grads, 'x': x,
+                'n_sync_bn': torch.tensor(count_sync_bn(sm)),
                 'world_seen': torch.tensor(BNSync(bns[0]).world),
                 'stats': st,
                 'grads': [p.grad.clone() for p in dp.parameters()],

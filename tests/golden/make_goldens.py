@@ -283,8 +283,10 @@ def gen_step(ref_model, ref_loss, ref_utils, cfg, loss_type, steps=3, tag=None, 
         dl, el = lf(pyr, disps, recon, step, None)
         (dl + el).backward()
         if step == 0:
+            from oracle import step as OS  # noqa: E402
             for k, p in m.named_parameters():
                 arrays[f'gradnorm/{k}'] = p.grad.double().norm()
+                arrays[f'sketch/{k}'] = OS.grad_sketch(k, p.grad)
             for i, d in enumerate(disps):
                 if i in disp_levels:
                     arrays[f'step0_disp{i}'] = d.detach()
@@ -301,6 +303,45 @@ def gen_step(ref_model, ref_loss, ref_utils, cfg, loss_type, steps=3, tag=None, 
                     arrays[f'param_sum/{k}'] = v.double().sum()
                     arrays[f'param_abs/{k}'] = v.double().abs().sum()
     save(f'step_{tag or loss_type}.npz', **arrays)
+
+
+def gen_traj(ref_model, ref_loss, ref_utils, cfg, steps=10, b=8, h=256, w=512):
+    """BASELINE config 2 at full size: 10 fp32 steps of the reference loop
+    body (train/train.py:116-129, Adam lr 1e-4, scale 0.3) on the bench's own
+    synthetic pair (oracle.step.bench_inputs: U[0,1), seed 1234) with formula
+    weights -- the "loss delta vs ref" trajectory of the BASELINE metric,
+    plus step-0 gradient sketches and disparity sums at this size."""
+    from oracle import step as OS  # noqa: E402
+    sd, _ = _formula_weights(cfg)
+    m = _ref_model(ref_model, cfg)
+    m.load_state_dict(sd)
+    m.train()
+    lcfg = json.loads(json.dumps(cfg['loss']))
+    lcfg['error_loss_config']['loss_type'] = 'bayesian'
+    lf = ref_loss.TukraUncertaintyLoss(**lcfg)
+    opt = torch.optim.Adam(m.parameters(), 1e-4)
+    left, right = OS.bench_inputs(b, h, w)
+    arrays = {'shape': np.array([b, h, w]), 'seed': np.int64(1234), 'scale': np.float64(0.3)}
+    for step in range(steps):
+        pyr = ref_utils.scale_pyramid(torch.cat([left, right], 1), 4)
+        opt.zero_grad()
+        disps = m(left, 0.3)
+        recon = ref_utils.reconstruct_pyramid(disps, pyr)
+        dl, el = lf(pyr, disps, recon, step, None)
+        (dl + el).backward()
+        if step == 0:
+            for k, p in m.named_parameters():
+                arrays[f'gradnorm/{k}'] = p.grad.double().norm()
+                arrays[f'sketch/{k}'] = OS.grad_sketch(k, p.grad)
+            for i, d in enumerate(disps):
+                arrays[f'step0_disp{i}_sum'] = d.detach().double().sum()
+                arrays[f'step0_disp{i}_abssum'] = d.detach().double().abs().sum()
+            arrays['step0_disp3'] = disps[3].detach()
+        opt.step()
+        arrays[f'disp_loss_{step}'] = np.float64(float(dl))
+        arrays[f'error_loss_{step}'] = np.float64(float(el))
+        print(f'traj step {step}: {float(dl):.6f} {float(el):.6f}', flush=True)
+    save('traj_c2.npz', **arrays)
 
 
 def gen_nodes10(ref_model, cfg10):
@@ -463,7 +504,7 @@ def main():
     with open(os.path.join(REPO, 'config_nodes10.yml')) as f:
         cfg10 = yaml.safe_load(f)
     which = sys.argv[1:] or ['warp', 'loss', 'model', 'step', 'nodes10', 'c1', 'transforms',
-                             'sparsification', 'adversarial']
+                             'sparsification', 'adversarial', 'traj']
     if 'warp' in which:
         gen_warp(ref_utils)
     if 'loss' in which:
@@ -476,6 +517,8 @@ def main():
         gen_step(ref_model, ref_loss, ref_utils, cfg, 'l1', steps=1)
     if 'nodes10' in which:
         gen_nodes10(ref_model, cfg10)
+    if 'traj' in which:  # BASELINE config 2, full size (slow: ~1 min on 8 cores)
+        gen_traj(ref_model, ref_loss, ref_utils, cfg)
     if 'c1' in which:  # BASELINE config 1: 128x256, batch 2, l1 error loss, one step
         gen_step(ref_model, ref_loss, ref_utils, cfg, 'l1', steps=1, tag='c1_l1', b=2, h=128,
                  w=256, disp_levels=(2, 3))

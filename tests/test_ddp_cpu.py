@@ -60,3 +60,15 @@ def test_dp_wrapper_gloo_world2(tmp_path):
         # CapturedTrainStep's packed all-reduce gives DDP's average
         for a, b in zip(x['flat_grads'], g):
             assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)
+    # the bucketed, hook-launched exchange (umamd.gradsync) on a 3-layer net
+    torch.manual_seed(0)
+    ref3 = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Linear(16, 4),
+                               torch.nn.Linear(4, 4))
+    g3 = [torch.zeros_like(p) for p in ref3.parameters()]
+    for k in (1, 2):
+        ref3.zero_grad()
+        ref3(torch.ones(3, 8) * k).sum().backward()
+        g3 = [a + p.grad / 2 for a, p in zip(g3, ref3.parameters())]
+    for x in r:
+        for a, b in zip(x['bucket_grads'], g3):
+            assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)

@@ -405,15 +405,12 @@ def test_nodes10_train_step_matches_oracle():
     (dlc + elc).backward()
     assert abs(float(dl) / float(dlc) - 1) < 1e-3
     assert abs(float(el) / float(elc) - 1) < 1e-3
-    bad = []
-    for k, p in m.named_parameters():
-        if _pre_bn_bias(k) or P[k].grad is None:
-            continue
-        ref, got = float(P[k].grad.double().norm()), float(p.grad.double().norm())
-        atol = 3e-5 if k.endswith('mean_weight') else 1e-6
-        if abs(got - ref) > 2e-2 * ref + atol:
-            bad.append((k, got, ref))
-    assert not bad, bad[:8]
+    # full gradients by direction: ||g - g_ref|| <= 2e-2 ||g_ref|| (+ floor)
+    from _parity import grad_worst
+    worst = grad_worst({k: p.grad for k, p in m.named_parameters()},
+                       {k: v.grad for k, v in P.items() if v.grad is not None}, 2e-2)
+    print('nodes10 full-gradient worst', worst)
+    assert worst[0] < 1, worst
 
 
 def test_config5_nodes10_512x1024_properties():

@@ -24,11 +24,13 @@ a captured step: the disparity ``scale`` is fixed at capture (recapture when
 
 Data parallel (one process per GPU, model wrapped by train.parallel): the
 captured forward runs the wrapped module directly, so DDP's autograd hooks
-stay idle, and graph 1 ends with the gradient exchange itself -- the
-gradients are packed into one flat f32 buffer and averaged with a single
-RCCL all-reduce recorded in the graph (SyncBN's statistic all-reduces are
-recorded the same way).  ``.grad`` of each parameter is then a view of the
-reduced buffer, which is what the fused Adam's pointer table holds.  DDP
+stay idle, and the gradient exchange is recorded in graph 1 itself -- the
+gradients are packed into ~16 MB buckets of one flat f32 buffer, each
+averaged by an RCCL all-reduce launched from the backward's hooks as soon as
+its gradients exist, on a communication branch that overlaps the rest of
+the backward (umamd.gradsync; SyncBN's statistic all-reduces are recorded
+the same way).  ``.grad`` of each parameter is then a view of the reduced
+buffer, which is what the fused Adam's pointer table holds.  DDP
 construction still broadcasts rank 0's parameters, and its module keeps the
 reference's ``module.`` checkpoint keys; construct it under the capture
 stream (``stream=``).
@@ -44,6 +46,7 @@ from torch.nn.parallel import DistributedDataParallel
 
 from umamd import lossfn as LF
 from umamd import overlap
+from umamd.gradsync import GradBuckets
 
 from . import utils as u
 
@@ -68,7 +71,13 @@ class CapturedTrainStep:
             self.group = dist.group.WORLD
         if self.group is not None:
             self.world = dist.get_world_size(self.group)
-        self._flat, self._layout, self._raw = None, None, None
+        self._buckets = None
+        if self.group is not None:
+            # bucketed all-reduce overlapped with the backward (umamd.gradsync);
+            # UMAMD_GRAD_BUCKET_MB sizes the buckets, 0 = one all-reduce at the end
+            mb = float(os.environ.get('UMAMD_GRAD_BUCKET_MB', '16'))
+            self._buckets = GradBuckets(model.parameters(), self.group, self.world,
+                                        cap_mb=mb if mb > 0 else 1e9)
         snap = self._snapshot(model, optimiser) if restore_state else None
         self.model, self.loss_function, self.optimiser = model, loss_function, optimiser
         self.scale, self.scales = float(scale), scales
@@ -100,7 +109,14 @@ class CapturedTrainStep:
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb, stream=side, capture_error_mode=mode):
             self.disp_loss, self.error_loss = self._fwd_bwd()
+        # the returned losses are static graph outputs; detached, they keep no
+        # autograd graph alive (its AccumulateGrad nodes remember the capture
+        # stream, and an eager step on another stream would synchronise with it)
+        self.disp_loss, self.error_loss = self.disp_loss.detach(), self.error_loss.detach()
         optimiser.prepare()  # tables for the graph-pool gradients, outside capture
+        # the captured Adam reads these device tables by address: keep them
+        # alive even if an eager step (another batch shape) replaces them
+        self._opt_tables = list(getattr(optimiser, '_tables', {}).values())
         torch.cuda.synchronize()
         self.g_opt = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool(), stream=side,
@@ -154,46 +170,38 @@ class CapturedTrainStep:
         images = torch.cat([self.left, self.right], dim=1)
         pyramid = u.scale_pyramid(images, self.scales)
         disparities = self.model(self.left, self.scale)
-        with LF.deferred_recon():  # the loss forward writes the recon
+        from .loss import TukraUncertaintyLoss
+        if isinstance(self.loss_function, TukraUncertaintyLoss):
+            with LF.deferred_recon():  # the fused loss forward writes the recon
+                recon = u.reconstruct_pyramid(disparities, pyramid)
+        else:
             recon = u.reconstruct_pyramid(disparities, pyramid)
         disp_loss, error_loss = self.loss_function(pyramid, disparities, recon, 0, None)
         if self.overlap is None:
+            if self._buckets is not None:
+                self._buckets.arm()
             (disp_loss + error_loss).backward()
         else:
             with self.overlap:
+                if self._buckets is not None:
+                    self._buckets.arm()  # buckets launch from the backward's hooks
                 (disp_loss + error_loss).backward()
-        if self.group is not None:
+        if self._buckets is not None:
             self._reduce_grads()
         return disp_loss, error_loss
 
+    @property
+    def _flat(self):
+        return self._buckets.flat if self._buckets is not None else None
+
     def _reduce_grads(self):
-        """Average the gradients over the group: pack -> one all-reduce ->
-        ``.grad`` = views of the reduced buffer (DDP's result, one
-        collective instead of its buckets)."""
-        params = [p for p in self.model.parameters() if p.requires_grad]
-        have = tuple(p.grad is not None for p in params)
-        if self._layout is None:
-            total = sum(p.numel() for p, h in zip(params, have) if h)
-            self._flat = torch.empty(total, dtype=torch.float32, device=params[0].device)
-            self._layout = have
-        elif have != self._layout:
-            raise RuntimeError('CapturedTrainStep: the set of parameters with gradients changed')
-        used = [p for p, h in zip(params, have) if h]
-        grads = [p.grad for p in used]
-        if any(g.dtype != torch.float32 for g in grads):
-            raise TypeError('CapturedTrainStep: float32 gradients expected')
-        torch.cat([g.reshape(-1) for g in grads], out=self._flat)
-        self._raw = grads  # the backward's own gradient tensors stay allocated
-        if dist.get_backend(self.group) == 'nccl':
-            dist.all_reduce(self._flat, op=dist.ReduceOp.AVG, group=self.group)
-        else:
-            dist.all_reduce(self._flat, group=self.group)
-            self._flat.mul_(1.0 / self.world)
-        off = 0
-        for p in used:
-            n = p.numel()
-            p.grad = self._flat[off:off + n].view_as(p)
-            off += n
+        """Average the gradients over the group (DDP's result): the buckets
+        not yet launched from the backward's hooks are packed and
+        all-reduced now, the communication stream joins the launch stream
+        and ``.grad`` become views of the reduced flat buffer."""
+        if self._buckets is None:
+            self._buckets = GradBuckets(self.model.parameters(), self.group, self.world)
+        self._buckets.finish()
 
     def __call__(self, left=None, right=None):
         if left is not None:

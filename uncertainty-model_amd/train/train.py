@@ -40,18 +40,31 @@ def save_model(model: Module, save_model_to: str, disc: Optional[Module] = None,
     torch.save(state_dict, filepath)
 
 
+def _fused_loss(loss_function) -> bool:
+    """the umamd fused loss, which fills a deferred recon pyramid itself"""
+    from .loss import TukraUncertaintyLoss
+    return isinstance(loss_function, TukraUncertaintyLoss)
+
+
 def train_step(model: Module, left, right, loss_function: Module, optimiser: Optimizer,
                scale: float, scales: int = 4, batch_index: int = 0,
                disc: Optional[Module] = None, disc_clone: Optional[Module] = None,
                disc_optimiser: Optional[Optimizer] = None,
-               disc_loss_function: Optional[Module] = None):
+               disc_loss_function: Optional[Module] = None,
+               batch_size: Optional[int] = None):
     """One step of the reference loop body (train.py:114-149) without
-    logging; returns (disp_loss, error_loss, disc_loss or None) device tensors."""
+    logging; returns (disp_loss, error_loss, disc_loss or None) device tensors.
+    ``batch_size``: the loader's batch size, which the reference passes to
+    run_discriminator (train.py:140-142; on a short last batch every
+    prediction is then labelled real); default: this batch's size."""
     images = torch.cat([left, right], dim=1)
     image_pyramid = u.scale_pyramid(images, scales)
     optimiser.zero_grad()
     disparities = model(left, scale)
-    with LF.deferred_recon():  # the fused loss forward writes the recon
+    if _fused_loss(loss_function):
+        with LF.deferred_recon():  # the fused loss forward writes the recon
+            recon_pyramid = u.reconstruct_pyramid(disparities, image_pyramid)
+    else:  # any other loss reads a recon pyramid computed up front
         recon_pyramid = u.reconstruct_pyramid(disparities, image_pyramid)
     disp_loss, error_loss = loss_function(image_pyramid, disparities, recon_pyramid,
                                           batch_index, disc_clone)
@@ -61,10 +74,65 @@ def train_step(model: Module, left, right, loss_function: Module, optimiser: Opt
     if disc is not None:
         disc_optimiser.zero_grad()
         disc_loss = u.run_discriminator(image_pyramid, recon_pyramid, disc, disc_loss_function,
-                                        left.shape[0])
+                                        batch_size if batch_size is not None else left.shape[0])
         disc_loss.backward()
         disc_optimiser.step()
     return disp_loss, error_loss, disc_loss
+
+
+class _GraphSteps:
+    """The captured training step (train.graph.CapturedTrainStep) behind the
+    reference loop: one capture per (disparity scale, batch shape), replayed
+    for every full batch.  The reference loop's host-side state changes stay
+    correct: ``adjust_disparity`` moving the scale recaptures (the old graphs
+    are released), ``adjust_learning_rate`` reaches the graph through the
+    optimiser's device-side learning rate (umamd.optim.Adam.sync_lr), and a
+    batch of another shape (a ragged last batch) takes one eager step.
+
+    Used when the model's parameters are on a HIP device, the optimiser is
+    umamd.optim.Adam, the loss is the fused umamd loss and there is no
+    discriminator (the adversarial step stays eager).  A DistributedDataParallel
+    model must have been built by train.parallel.data_parallel (which builds it
+    under the capture stream, see there); a DDP built elsewhere steps eagerly.
+    UMAMD_TRAIN_GRAPH=0 turns it off."""
+
+    def __init__(self, model, loss_function, optimiser, scales):
+        self.model, self.loss_function, self.optimiser = model, loss_function, optimiser
+        self.scales = scales
+        self.key = None
+        self.cap = None
+
+    @staticmethod
+    def usable(model, loss_function, optimiser, disc) -> bool:
+        from torch.nn.parallel import DistributedDataParallel
+        if os.environ.get('UMAMD_TRAIN_GRAPH', '1') == '0' or disc is not None:
+            return False
+        if not hasattr(optimiser, 'sync_lr') or not _fused_loss(loss_function):
+            return False
+        p = next(model.parameters(), None)
+        if p is None or not p.is_cuda:
+            return False
+        if isinstance(model, DistributedDataParallel):
+            from torch import distributed as dist
+            if getattr(model, '_umamd_stream', None) is None or \
+                    dist.get_backend(model.process_group) != 'nccl':
+                return False  # a gloo all-reduce cannot be captured
+        return True
+
+    def __call__(self, left, right, scale):
+        from .graph import CapturedTrainStep
+        key = (float(scale), tuple(left.shape), tuple(right.shape), left.dtype)
+        if self.cap is not None and self.key != key and self.key[1:] != key[1:]:
+            return None  # another batch shape: the caller steps eagerly
+        self.optimiser.sync_lr()
+        if self.key != key:
+            self.cap = None  # scale changed: drop the old graphs before capturing
+            torch.cuda.synchronize()
+            stream = getattr(self.model, '_umamd_stream', None)
+            self.cap = CapturedTrainStep(self.model, self.loss_function, self.optimiser, left,
+                                         right, scale, scales=self.scales, stream=stream)
+            self.key = key
+        return self.cap(left, right)
 
 
 def train_one_epoch(model: Module, loader: DataLoader, loss_function: Module,
@@ -74,8 +142,10 @@ def train_one_epoch(model: Module, loader: DataLoader, loss_function: Module,
                     disc_loss_function: Optional[Module] = None,
                     epoch_number: Optional[int] = None, scales: int = 4,
                     perceptual_update_freq: int = 10, device: Device = 'cpu',
-                    no_pbar: bool = False, rank: int = 0) -> Tuple[float, float]:
-    """Reference train/train.py:51-170."""
+                    no_pbar: bool = False, rank: int = 0,
+                    graph_steps: Optional[_GraphSteps] = None) -> Tuple[float, float]:
+    """Reference train/train.py:51-170.  ``graph_steps`` (train_model passes
+    one): replay the captured step for full batches (see _GraphSteps)."""
     model.train()
     if disc is not None:
         disc.train()
@@ -84,14 +154,23 @@ def train_one_epoch(model: Module, loader: DataLoader, loss_function: Module,
     batch_size = loader.batch_size if loader.batch_size is not None else len(loader)
     description = f'Epoch #{epoch_number}' if epoch_number is not None else 'Epoch'
     disc_clone = deepcopy(disc) if disc is not None else None
+    graphs = None
+    if graph_steps is not None and _GraphSteps.usable(model, loss_function, model_optimiser,
+                                                      disc):
+        graphs = graph_steps
     it = tqdm.tqdm(loader, description, unit='batch', disable=(no_pbar or rank > 0)) \
         if tqdm is not None else loader
     for i, image_pair in enumerate(it):
         left = image_pair['left'].to(device)
         right = image_pair['right'].to(device)
-        disp_loss, error_loss, disc_loss = train_step(
-            model, left, right, loss_function, model_optimiser, scale, scales, i, disc,
-            disc_clone, disc_optimiser, disc_loss_function)
+        out = graphs(left, right, scale) if graphs is not None else None
+        if out is not None:
+            disp_loss, error_loss = out
+            disc_loss = None
+        else:
+            disp_loss, error_loss, disc_loss = train_step(
+                model, left, right, loss_function, model_optimiser, scale, scales, i, disc,
+                disc_clone, disc_optimiser, disc_loss_function, batch_size=loader.batch_size)
         if rank == 0:
             running_disp_loss += disp_loss.item()
             running_error_loss += error_loss.item()
@@ -135,13 +214,14 @@ def train_model(model: Module, loader: DataLoader, loss_function: Module,
     model_optimiser = Adam(model.parameters(), learning_rate)
     disc_optimiser = Adam(disc.parameters(), learning_rate) if disc is not None else None
     training_losses, validation_metrics = [], []
+    graph_steps = _GraphSteps(model, loss_function, model_optimiser, 4)
     for i in range(epochs):
         adjust_learning_rate(model_optimiser, i, learning_rate)
         scale = 1 if finetune else adjust_disparity(i)
         loss = train_one_epoch(model, loader, loss_function, model_optimiser, scale, disc,
                                disc_optimiser, disc_loss_function, epoch_number=(i + 1),
                                perceptual_update_freq=perceptual_update_freq, device=device,
-                               no_pbar=no_pbar, rank=rank)
+                               no_pbar=no_pbar, rank=rank, graph_steps=graph_steps)
         if rank == 0:
             training_losses.append(loss)
         if evaluate_every is not None and (i + 1) % evaluate_every == 0:

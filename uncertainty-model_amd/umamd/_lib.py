@@ -140,13 +140,14 @@ def lib() -> ctypes.CDLL:
         return _lib
     from . import _build
     if _build.needs_build():
-        # missing or older than its sources: build now so a compile error
-        # surfaces with hipcc's own message instead of "not found"
+        # missing or built from other sources: build now (under the build
+        # lock, so concurrent ranks neither race nor load a half-written
+        # .so) and a compile error surfaces with hipcc's own message
         if not _build.can_build():
             raise UmamdError(f'{LIB_PATH} is missing or stale and hipcc is not available to '
                              f'rebuild it (run `python uncertainty-model_amd/umamd/_build.py`)')
         try:
-            _build.build()
+            _build.ensure_built()
         except RuntimeError as e:
             raise UmamdError(f'building {LIB_PATH} failed:\n{e}') from None
     L = ctypes.CDLL(LIB_PATH)

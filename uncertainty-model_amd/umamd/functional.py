@@ -126,7 +126,7 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
     dw.record_stream(ov.stream)
     dw_ptr = ptr(dw)
     ov.defer((x, dy), lambda: _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad,
-                                             pad_mode, dw_ptr, segs))
+                                             pad_mode, dw_ptr, segs), out_ptr=dw_ptr)
     return dw
 
 

@@ -94,6 +94,16 @@ class Adam(torch.optim.Optimizer):
                 st['lr'].fill_(float(lr))
                 st['lr_host'] = float(lr)
 
+    def sync_lr(self):
+        """Copy each group's host learning rate to its device copy if it
+        changed (``adjust_learning_rate`` writes ``group['lr']``; a captured
+        step only sees the device copy)."""
+        for gi, group in enumerate(self.param_groups):
+            st = self._dev.get(gi)
+            if st is not None and st['lr_host'] != float(group['lr']):
+                st['lr'].fill_(float(group['lr']))
+                st['lr_host'] = float(group['lr'])
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None

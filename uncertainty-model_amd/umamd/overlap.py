@@ -43,6 +43,8 @@ class WgradStream:
         self.batch = batch or int(os.environ.get('UMAMD_WGRAD_BATCH', '24'))
         self._launch = None
         self._pending = []
+        self._pending_out = set()
+        self._on_flush = []
 
     def __enter__(self):
         if WgradStream._active is not None:
@@ -54,14 +56,26 @@ class WgradStream:
         WgradStream._active = self
         return self
 
-    def defer(self, tensors, launch):
+    def defer(self, tensors, launch, out_ptr=None):
         """Queue one weight gradient (``launch`` issues its kernels on the
-        current stream; ``tensors`` are the ones it touches) and flush the
-        queue onto the side stream every ``batch`` entries: one fork per
-        batch instead of one per conv."""
+        current stream; ``tensors`` are the ones it touches, ``out_ptr`` the
+        address it writes) and flush the queue onto the side stream every
+        ``batch`` entries: one fork per batch instead of one per conv."""
         self._pending.append((tensors, launch))
+        if out_ptr is not None:
+            self._pending_out.add(out_ptr)
         if len(self._pending) >= self.batch:
             self._flush()
+
+    def is_pending(self, ptrs) -> bool:
+        """True if any of these addresses is written by a queued launch
+        that has not been flushed onto the side stream yet"""
+        return any(p in self._pending_out for p in ptrs)
+
+    def on_flush(self, fn):
+        """call ``fn()`` after every flush of this context (gradsync: a
+        bucket whose gradients were queued becomes launchable)"""
+        self._on_flush.append(fn)
 
     def _flush(self):
         if not self._pending:
@@ -74,11 +88,17 @@ class WgradStream:
             for t in tensors:
                 t.record_stream(self.stream)
         self._pending = []
+        self._pending_out.clear()
+        for fn in self._on_flush:
+            fn()
 
     def __exit__(self, *exc):
         WgradStream._active = None
-        self._flush()
-        self._launch.wait_stream(self.stream)
+        try:
+            self._flush()
+        finally:
+            self._on_flush = []
+            self._launch.wait_stream(self.stream)
 
 
 def active() -> Optional[WgradStream]:
