@@ -48,6 +48,9 @@ def parse():
     ap.add_argument('--config', default='config.yml')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--loader-steps', type=int, default=20,
+                    help='N=1: also time this many steps fed by the PNG/DataLoader/GPU-augment '
+                         'input pipeline (loader_line; 0 = off)')
     ap.add_argument('--no-loss-delta', action='store_true',
                     help='skip the loss-delta-vs-reference leg (fp32 + bf16 10-step trajectories)')
     ap.add_argument('--no-graph', action='store_true',
@@ -356,6 +359,80 @@ def cpu_baseline(config, steps):
             'c1_thread_sweep_pairs_per_s': sweep}, ref0
 
 
+# ---------------------------------------------------------- loader line ----
+class _PNGPairs:
+    """The reference's DaVinciDataset.__getitem__ (loaders/davinci.py:70-90:
+    PIL open + convert('RGB') of both views, then the transform) over PNG
+    files written by ``loader_line``."""
+
+    def __init__(self, files, transform):
+        self.files, self.transform = files, transform
+
+    def __len__(self):
+        return len(self.files)
+
+    def __getitem__(self, i):
+        from PIL import Image
+        lf, rf = self.files[i]
+        return self.transform({'left': Image.open(lf).convert('RGB'),
+                               'right': Image.open(rf).convert('RGB')})
+
+
+def loader_line(run, batch, steps, warmup=3, pairs=64, src=(288, 384)):
+    """pairs/s of the captured step fed by a real input pipeline: PNG pairs
+    of the Hamlyn da Vinci frame size (288x384), decoded by DataLoader
+    workers (PIL, as the reference's loaders), augmentation draws in the
+    workers and resize / flip / ToTensor / augment on the GPU
+    (train.transforms.DeviceAugment), pinned-memory uint8 batches."""
+    import tempfile
+    import numpy as np
+    from PIL import Image
+    from torch.utils.data import DataLoader
+    import train.transforms as T
+    from umamd.imageprep import to_device
+    tmp = tempfile.mkdtemp(prefix='umamd_png_')
+    rng = np.random.default_rng(0)
+    files = []
+    base = rng.integers(0, 256, (src[0] // 8, src[1] // 8, 3), dtype=np.uint8)
+    for i in range(pairs):
+        # smooth-ish textures (PNG of pure noise would not compress like frames)
+        img = np.kron(np.roll(base, i, axis=1), np.ones((8, 8, 1), np.uint8))
+        img = (img.astype(np.int16) + rng.integers(-8, 8, img.shape)).clip(0, 255)
+        paths = []
+        for v in ('l', 'r'):
+            pth = os.path.join(tmp, f'{i:04d}_{v}.png')
+            Image.fromarray(img.astype(np.uint8)).save(pth)
+            paths.append(pth)
+        files.append(tuple(paths))
+    workers = max(1, min(8, (os.cpu_count() or 2) - 1))
+    dl = DataLoader(_PNGPairs(files, T.DeviceAugment((256, 512))), batch_size=batch,
+                    shuffle=True, num_workers=workers, pin_memory=True, drop_last=True,
+                    persistent_workers=True, prefetch_factor=4)
+    dev = torch.device('cuda', torch.cuda.current_device())
+
+    def batches():
+        while True:
+            for b in dl:
+                yield b
+    it = batches()
+    for _ in range(warmup):
+        run(*to_device(next(it), dev))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run(*to_device(next(it), dev))
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / steps
+    del dl
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+    return {'value': round(batch / t, 2), 'ms_per_step': round(t * 1e3, 3), 'steps': steps,
+            'workers': workers,
+            'source': f'{src[0]}x{src[1]} PNG pairs, PIL decode in DataLoader workers, '
+                      f'flip/augment draws in workers, resize+flip+ToTensor+augment on the GPU '
+                      f'(train.transforms.DeviceAugment), hip-graph step'}
+
+
 # ------------------------------------------------------------ loss delta ----
 def _golden_traj():
     path = os.path.join(REPO, 'tests', 'golden', 'traj_c2.npz')
@@ -533,6 +610,10 @@ def main():
         elapsed = float(t)
     losses = (float(dl.detach()), float(el.detach()))
 
+    loader = None
+    if use_graph and world == 1 and a.loader_steps > 0 and (a.height, a.width) == (256, 512):
+        loader = loader_line(run, a.batch, a.loader_steps)
+
     # the eager comparison and the roofline pass run on the stream the model
     # was built on (DDP keeps AccumulateGrad nodes bound to it)
     with torch.cuda.stream(cap_stream):
@@ -577,6 +658,7 @@ def main():
                        'graph': f'{a.config} (nodes={cfg["model"]["encoder"].get("nodes")} '
                                 f'stage graphs)'},
             'eager_launch': eager,
+            'loader_line': loader,
             'fp32_line': fp32,
             'final_losses': {'disp': round(losses[0], 5), 'error': round(losses[1], 5)},
             'loss_delta': delta,

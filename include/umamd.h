@@ -418,6 +418,25 @@ int um_adam_step_dev(const void* table, const void* chunks, int nchunks, float l
                      const float* dlr, float beta1, float beta2, float eps, float weight_decay,
                      int* dstep, hipStream_t stream);
 
+/* --------------------------------------------------- input pipeline ---
+ * The reference's training transforms (train/transforms.py:15-129 composed
+ * in main.py:78-89 / parallel_main.py:111-124: ResizeImage((256, 512)) ->
+ * RandomFlip(0.5) -> ToTensor() -> RandomAugment(0.5, ...)) for a batch of
+ * both views.  left/right: uint8 [N][Hs][Ws][3] (decoded RGB); the resize is
+ * Pillow's 8-bit bilinear resampler (host-made coefficient tables:
+ * bounds [out][2] = (first tap, taps), kk [out][ks] 22-bit fixed point),
+ * horizontal pass into `tmp` (um_stereo_prep_ws bytes), then the vertical
+ * pass, /255, the flip and the augment with per-sample params [N][8] =
+ * (flip, augment, gamma, brightness, colour[3], 0) drawn on the host in the
+ * reference's order.  out_left/out_right: f32 [N][3][Hd][Wd].
+ */
+long um_stereo_prep_ws(int N, int Hs, int Wd);
+int um_stereo_prep(int N, int Hs, int Ws, const unsigned char* left,
+                   const unsigned char* right, int Hd, int Wd, const int* bounds_h,
+                   const int* kk_h, int ks_h, const int* bounds_v, const int* kk_v, int ks_v,
+                   const float* params, unsigned char* tmp, float* out_left, float* out_right,
+                   hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,9 +15,8 @@
 Tolerances (stated per check below): fp32 build vs reference 1e-3 rel on
 disparities and loss scalars; gradients 2e-2 rel-norm (F9: the
 warp-dependent terms alone carry 4e-3 fp32-vs-fp64 noise), 0.1 for the l1
-loss's SE/merge gradients (its NLL gradient is sign(sigma - e): whole-map
-sums flip with summation order; the reference's own fp32 vs fp64 differ by
-4 %).
+loss (its NLL gradient is sign(sigma - e): the reference's own fp32 vs fp64
+differ by up to 5.5e-2 rel-norm on weights, see _l1_tol).
 """
 import os
 
@@ -32,7 +31,13 @@ pytestmark = pytest.mark.gpu
 
 
 def _l1_tol(k):
-    return 0.1 if ('excite' in k or k.endswith('mean_weight')) else 2e-2
+    """l1 error loss: its NLL gradient is sign(sigma - e), so every upstream
+    gradient inherits sign flips of near-tie pixels.  The reference's own
+    math in fp32 vs fp64 (the oracle, same inputs) differs by up to 5.5e-2
+    rel-norm on weights at config 1 (decoder.2 disp head) and 0.12 on an SE
+    weight (step_l1), so l1 directions are held to about twice that noise;
+    the bayesian loss keeps 2e-2."""
+    return 0.3 if ('excite' in k or k.endswith('mean_weight')) else 0.12
 
 
 @pytest.mark.parametrize('name,lt', [('step_bayesian.npz', 'bayesian'), ('step_l1.npz', 'l1'),

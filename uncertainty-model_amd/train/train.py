@@ -17,6 +17,7 @@ from torch.optim import Optimizer
 from torch.utils.data import DataLoader
 
 from umamd import lossfn as LF
+from umamd.imageprep import to_device
 from umamd.optim import Adam
 
 from . import utils as u
@@ -161,8 +162,8 @@ def train_one_epoch(model: Module, loader: DataLoader, loss_function: Module,
     it = tqdm.tqdm(loader, description, unit='batch', disable=(no_pbar or rank > 0)) \
         if tqdm is not None else loader
     for i, image_pair in enumerate(it):
-        left = image_pair['left'].to(device)
-        right = image_pair['right'].to(device)
+        # a DeviceAugment batch (uint8 + draws) is resized / augmented on the GPU
+        left, right = to_device(image_pair, device)
         out = graphs(left, right, scale) if graphs is not None else None
         if out is not None:
             disp_loss, error_loss = out

@@ -178,3 +178,26 @@ class Compose:
         for t in self.transforms:
             x = t(x)
         return x
+
+
+class DeviceAugment:
+    """The augmenting pipeline with its arithmetic on the GPU (umamd.imageprep):
+    a drop-in for ``Compose([ResizeImage(size), RandomFlip(0.5), ToTensor(),
+    RandomAugment(0.5, ...)])`` (reference main.py:78-89) whose workers only
+    convert the decoded PIL pair to uint8 arrays and draw the flip / augment
+    parameters in the reference's numpy order.  The batch then carries
+    uint8 images + parameters, and ``train.train`` (or
+    ``umamd.imageprep.to_device``) turns it into the f32 [N, 3, H, W] pair on
+    the device in two kernel launches.  ``augment=False`` gives the
+    no-augment pipeline (ResizeImage + ToTensor, main.py:91-93)."""
+
+    def __init__(self, size: ImageSize = (256, 512), flip_p: float = 0.5,
+                 augment_p: float = 0.5, gamma: BoundsTuple = (0.8, 1.2),
+                 brightness: BoundsTuple = (0.5, 2.0), colour: BoundsTuple = (0.8, 1.2),
+                 augment: bool = True) -> None:
+        from umamd.imageprep import StereoDraws
+        self.draws = StereoDraws(flip_p, augment_p, gamma, brightness, colour, augment, size)
+
+    def __call__(self, image_pair):
+        return self.draws({'left': np.asarray(image_pair['left']),
+                           'right': np.asarray(image_pair['right'])})

@@ -121,6 +121,9 @@ _SIG = {
     'um_spars_sort_ws': (_L, [_I, _I]),
     'um_spars_sort': (_I, [_P, _P, _I, _I, _P, _P, _P, _L, 's']),
     'um_spars_curve': (_I, [_P, _I, _I, _I, _P, _P, 's']),
+    'um_stereo_prep_ws': (_L, [_I, _I, _I]),
+    'um_stereo_prep': (_I, [_I, _I, _I, _P, _P, _I, _I, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P,
+                            's']),
     'um_adam_chunk': (_I, []),
     'um_adam_step': (_I, [_P, _P, _I, _F, _F, _F, _F, _F, _I, 's']),
     'um_adam_step_dev': (_I, [_P, _P, _I, _F, _P, _F, _F, _F, _F, _P, 's']),
