@@ -953,18 +953,17 @@ __host__ __device__ constexpr int pack_ct(int R) {  // c per workgroup: 32*ct*R*
   return R <= 1 ? 64 : (R <= 3 ? 16 : (R <= 5 ? 8 : 4));
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) pack_batch_kernel(const um_pack_desc* __restrict__ table,
-                                                         const int* __restrict__ blk2desc) {
-  __shared__ float tile[8192 + 64];
-  const um_pack_desc d = table[blk2desc[blockIdx.x]];
-  const int t = blockIdx.x - d.block0;
-  const int RR = d.R * d.R, CT = pack_ct(d.R);
+// One (32 k x CT c) tile of one weight per workgroup.  The filter size is a
+// compile-time constant (R in {1, 3, 5, 7}: every conv of the model) so the
+// (k, c, tap) index splits are multiplies and shifts, not integer divisions.
+template <typename T, int R>
+__device__ __forceinline__ void pack_tile(const um_pack_desc& d, int t, float* tile) {
+  constexpr int RR = R * R, CT = pack_ct(R);
+  constexpr int per_k = CT * RR;  // staged values per k row
+  constexpr int ldt = per_k + 1;  // odd LDS row stride
+  constexpr int n = PK * per_k;
   const int nct = (d.C + CT - 1) / CT;
   const int k0 = (t / nct) * PK, c0 = (t % nct) * CT;
-  const int per_k = CT * RR;  // staged values per k row
-  const int ldt = per_k + 1;  // odd LDS row stride
-  const int n = PK * per_k;
   for (int i = threadIdx.x; i < n; i += 256) {
     const int kk = i / per_k, rem = i - kk * per_k;
     const int cc = rem / RR, tap = rem - cc * RR;
@@ -999,6 +998,21 @@ __global__ void __launch_bounds__(256) pack_batch_kernel(const um_pack_desc* __r
       if (k < d.K && c < d.C)
         wT[((long)c * RR + tap) * d.ldT + k] = from_f32<T>(tile[kk * ldt + cc * RR + tap]);
     }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) pack_batch_kernel(const um_pack_desc* __restrict__ table,
+                                                         const int* __restrict__ blk2desc) {
+  __shared__ float tile[8192 + 64];
+  const um_pack_desc d = table[blk2desc[blockIdx.x]];
+  const int t = blockIdx.x - d.block0;
+  switch (d.R) {
+    case 1: pack_tile<T, 1>(d, t, tile); break;
+    case 3: pack_tile<T, 3>(d, t, tile); break;
+    case 5: pack_tile<T, 5>(d, t, tile); break;
+    case 7: pack_tile<T, 7>(d, t, tile); break;
+    default: break;  // rejected on the host (um_pack_batch)
+  }
 }
 
 }  // namespace

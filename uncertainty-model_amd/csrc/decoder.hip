@@ -521,8 +521,17 @@ __global__ void __launch_bounds__(256) se_mlp_fwd_kernel(
     const int c = c0 + u;
     float t = 0.f;
     if (l < L && c < C) {
+      // 8 independent partial sums: 8 loads in flight per thread (the
+      // grid is one block per image, so this loop is latency-bound)
       const float* q = parts + (long)n * nparts * C + c;
-      for (int b = l; b < nparts; b += L) t += q[(long)b * C];
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      int b = l;
+      for (; b + 7 * L < nparts; b += 8 * L) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += q[(long)(b + k * L) * C];
+      }
+      for (; b < nparts; b += L) acc[0] += q[(long)b * C];
+      t = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
     red[threadIdx.x] = t;
     __syncthreads();

@@ -160,6 +160,8 @@ class WeightPacker:
         if w32.data_ptr() != weight.data_ptr():
             # the batch reads the parameter memory directly: only f32 contiguous params
             return False
+        if R not in (1, 3, 5, 7):  # pack_batch_kernel's compile-time filter sizes
+            return False
         self.descs.append((weight, wf, wT, K, Creal, R, C, ldT, list(segs) if segs else None,
                            weight.data_ptr(), L.dtype_code(dtype)))
         self.dirty = True
