@@ -14,14 +14,17 @@
     duration, and the derived ratios
 
       mfma_busy      = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * GRBM_GUI_ACTIVE/8)
-                       (GRBM_GUI_ACTIVE is summed over the 8 XCDs)
+                       (GRBM_GUI_ACTIVE is summed over the 8 XCDs; checked on
+                       MI355X: equals 512 * MOPS_BF16 / duration / 2.5 PF within
+                       ~10 %, so it is the fraction of the dense bf16 peak)
       mfma_tflops    = 512 * SQ_INSTS_VALU_MFMA_MOPS_BF16 / duration
       valu_issue     = 2 * SQ_INSTS_VALU / (1024 * GRBM_GUI_ACTIVE/8)
                        (2 cycles per wave64 VALU op on a SIMD32 pair; a lower
                        bound of the issue time's share of the kernel)
       lds_conflict   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
-      occupancy      = SQ_ACCUM_PREV_HIRES / (GRBM_GUI_ACTIVE/8) / 256
-                       (mean resident waves per CU)
+      occupancy      = 4 * SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE/8) / 256
+                       (mean resident waves per CU; SQ_WAVE_CYCLES counts
+                       quad-cycles; SQ_ACCUM_PREV_HIRES read 0 on gfx950)
       wait_any       = SQ_WAIT_ANY / SQ_WAVE_CYCLES (share of wave time stalled)
       wait_lds       = SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES
 """
@@ -103,8 +106,11 @@ def _brackets(items):
 def parse(a):
     labels = json.load(open(a.labels))
     per_entry, per_kernel = {}, {}
+    npass = {}  # counter -> number of passes that collected it (GRBM_GUI_ACTIVE is in each)
     for d in a.dirs:
         ctr, dur = _load(d)
+        for cn in {cn for _, c in ctr.values() for cn in c}:
+            npass[cn] = npass.get(cn, 0) + 1
         # durations only from the trace-only pass (counter passes serialise
         # and slow the kernels down)
         src = ctr if ctr else {k: (v[0], {}) for k, v in dur.items()}
@@ -129,6 +135,8 @@ def parse(a):
             if any(ns is not None for _, (_, ns) in group):
                 e['launches'] += 1
     for t in list(per_entry.values()) + list(per_kernel.values()):
+        # counters collected in several passes: the per-pass mean
+        t['counters'] = {cn: v / npass.get(cn, 1) for cn, v in t['counters'].items()}
         c = t['counters']
         cyc = c.get('GRBM_GUI_ACTIVE', 0.0) / 8.0
         der = {}
@@ -140,8 +148,8 @@ def parse(a):
             der['valu_issue'] = 2.0 * c['SQ_INSTS_VALU'] / (1024.0 * cyc)
         if c.get('SQ_LDS_IDX_ACTIVE'):
             der['lds_conflict'] = c.get('SQ_LDS_BANK_CONFLICT', 0.0) / c['SQ_LDS_IDX_ACTIVE']
-        if cyc and 'SQ_ACCUM_PREV_HIRES' in c:
-            der['occupancy_waves_per_cu'] = c['SQ_ACCUM_PREV_HIRES'] / cyc / 256.0
+        if cyc and 'SQ_WAVE_CYCLES' in c:  # quad-cycles (MI355X_MICROARCH.md)
+            der['occupancy_waves_per_cu'] = 4.0 * c['SQ_WAVE_CYCLES'] / cyc / 256.0
         if c.get('SQ_WAVE_CYCLES'):
             if 'SQ_WAIT_ANY' in c:
                 der['wait_any'] = c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']
