@@ -185,6 +185,10 @@ int um_bn_coeffs(const double* stats, double count, int C, const float* gamma,
 /* pool_parts (optional, SE squeeze of decoder.py:124-136 fused in): per-block
  * channel sums of a, [um_bn_fwd_pool_parts(M, HW)][C], HW = pixels per image */
 int um_bn_fwd_pool_parts(long M, long HW);
+/* the same for a C-channel layer (the forward pass may split small layers
+ * into 64-channel slices with their own row blocking): the pool row count
+ * um_bn_elu_fwd / um_bn_elu_fwd_slots write */
+int um_bn_fwd_pool_parts_c(long M, long HW, int C);
 int um_bn_elu_fwd(int dtype, long M, int C, const void* y, int ldy, const float* scale,
                   const float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
                   hipStream_t stream);

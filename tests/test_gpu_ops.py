@@ -61,6 +61,13 @@ HALO_CASES = [
     (40, 48, 3, 1, 'reflect', 8, 32),
     (64, 16, 3, 1, 'zero', 16, 32),
     (8, 32, 3, 1, 'reflect', 8, 64),
+    # wider outputs (halo_max_nc): 96- and 128-wide 3x3 column blocks, column
+    # grids of 96 / 64 (5x5, 7x7) blocks
+    (168, 128, 3, 1, 'reflect', 8, 32),
+    (64, 96, 3, 1, 'zero', 8, 32),
+    (88, 160, 3, 1, 'zero', 8, 32),
+    (32, 88, 5, 1, 'zero', 8, 32),
+    (96, 72, 7, 1, 'zero', 8, 32),
 ]
 
 
@@ -470,6 +477,7 @@ def test_dgrad_odd_tiles(dtype, case):
     (64, 64, 3, 1, 3, 5, False),      # H = 3: rows 1 and H-2 coincide
     (32, 16, 3, 1, 2, 7, True),       # H = 2: both rows fold
     (320, 256, 3, 2, 8, 16, False),   # split-K
+    (88, 64, 3, 2, 8, 64, True),      # split form on the 96-wide halo blocks
 ])
 def test_dgrad_reflect(dtype, case):
     from umamd import functional as U

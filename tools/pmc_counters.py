@@ -64,6 +64,9 @@ def run(a):
     torch.cuda.synchronize()
     with open(a.labels, 'w') as f:
         json.dump([name for name, *_ in rec.items], f)
+    with open(a.labels + '.args.json', 'w') as f:  # per launch: entry, scalar args, FLOPs
+        json.dump([[name, [v for v in args if isinstance(v, (int, float))], work]
+                   for name, args, _, _, work in rec.items], f)
     print(json.dumps({'launches': len(rec.items)}))
 
 
@@ -158,7 +161,24 @@ def parse(a):
         t['derived'] = {k: round(v, 4) for k, v in der.items()}
         n = t.get('launches') or t.get('dispatches') or 1
         t['mean_us'] = round(t['ns'] / max(n, 1) / 1e3, 2)
-    res = {'workload': 'one eager bench step (B=8, 256x512, bf16, bayesian) after warm-up; '
+    # per-launch table from the trace-only pass: entry, shape args, kernels, us
+    launches = []
+    args_path = a.labels + '.args.json'
+    if os.path.exists(args_path):
+        largs = json.load(open(args_path))
+        for d in a.dirs:
+            ctr, dur = _load(d)
+            if ctr:
+                continue
+            items = [(dur[i][0], dur[i][1]) for i in sorted(dur)]
+            for (lab, args, work), group in zip(largs, _brackets(items)):
+                ns = sum(v for _, v in group)
+                launches.append({'entry': lab, 'args': args, 'us': round(ns / 1e3, 2),
+                                 'tflops': round(work / ns / 1e3, 1) if work and ns else None,
+                                 'kernels': [_short(n) for n, _ in group]})
+            break
+    res = {'launch_table': sorted(launches, key=lambda r: -r['us']),
+           'workload': 'one eager bench step (B=8, 256x512, bf16, bayesian) after warm-up; '
                        'entries bracketed by spin_kernel markers',
            'passes': a.dirs, 'entries': per_entry,
            'kernels': dict(sorted(per_kernel.items(), key=lambda kv: -kv[1]['ns']))}

@@ -69,19 +69,21 @@ struct FwdFin {
   float *mean, *invstd, *scale, *shift;
 };
 
-__device__ __forceinline__ void fwd_fin_coeffs(const FwdFin& f, int C, float* s_sc, float* s_sh) {
-  const bool pub = blockIdx.x == 0;
+// s_sc / s_sh hold channels [c0, c0 + n) (this block's slice) at [c - c0]
+__device__ __forceinline__ void fwd_fin_coeffs(const FwdFin& f, int C, int c0, int n, float* s_sc,
+                                               float* s_sh) {
+  const bool pub = blockIdx.x == 0;  // the first row block of every channel slice
   // count <= 0: the element count follows the slots (SyncBN: all-reduced with them)
   const double count = f.count > 0 ? f.count : f.slots[(long)UM_STAT_SLOTS * C * 2];
-  stat_slots_finish(f.slots, C, [&](int c, double s0, double s1) {
+  stat_slots_finish(f.slots, C, c0, n, [&](int c, double s0, double s1) {
     const double mean = s0 / count;
     double var = s1 / count - mean * mean;
     if (var < 0) var = 0;
     const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
     const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
     const float sc = g * invstd, sh = b - (float)mean * g * invstd;
-    s_sc[c] = sc;
-    s_sh[c] = sh;
+    s_sc[c - c0] = sc;
+    s_sh[c - c0] = sh;
     if (pub) {
       f.mean[c] = (float)mean;
       f.invstd[c] = invstd;
@@ -94,34 +96,42 @@ __device__ __forceinline__ void fwd_fin_coeffs(const FwdFin& f, int C, float* s_
       }
     }
   });
-  if (pub && threadIdx.x == 0 && f.nbt != nullptr) *f.nbt += 1;
+  if (pub && blockIdx.y == 0 && threadIdx.x == 0 && f.nbt != nullptr) *f.nbt += 1;
   __syncthreads();
 }
 
+// Channel slices (grid.y): block (x, y) owns rows [x*rows, (x+1)*rows) and
+// channels [y*cs, (y+1)*cs).  The small deep layers (M of 1k..16k rows, C of
+// 128..512) are sliced so a block finishes only its channels' statistics
+// slots (16 KB instead of up to 128 KB per block) and the grid still has a
+// few hundred blocks; wide layers keep one slice (cs = C).
 template <typename T>
 __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
     const float* __restrict__ y, int ldy, long M, int C, const float* __restrict__ scale,
     const float* __restrict__ shift, T* __restrict__ a, int lda, int apply_elu,
-    int rows_per_block, float* __restrict__ pool, FwdFin fin) {
-  extern __shared__ float red[];  // [256][8] when pooling, then [2][C] coefficients (fin)
-  const int cg = C / 8;
+    int rows_per_block, float* __restrict__ pool, FwdFin fin, int cs) {
+  extern __shared__ float red[];  // [256][8] when pooling, then [2][cs] coefficients (fin)
+  const int cb = blockIdx.y * cs;  // this block's channel slice
+  const int cg = cs / 8;
   const RowMap rm(cg);
   const long m0 = (long)blockIdx.x * rows_per_block;
   const long m1 = min(M, m0 + rows_per_block);
+  int coff = cb;  // index of channel cb in scale / shift
   if (fin.slots != nullptr) {
     float* s_sc = red + (pool ? 256 * 8 : 0);
-    fwd_fin_coeffs(fin, C, s_sc, s_sc + C);
+    fwd_fin_coeffs(fin, C, cb, cs, s_sc, s_sc + cs);
     scale = s_sc;
-    shift = s_sc + C;
+    shift = s_sc + cs;
+    coff = 0;
   }
   for (int g0 = 0; g0 < cg; g0 += rm.G) {
     const int g = g0 + rm.g;
     float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (rm.active() && g < cg) {
-      const int c = g * 8;
+      const int c = cb + g * 8;
       float sc[8], sh[8];
-      load8(scale + c, sc);
-      load8(shift + c, sh);
+      load8(scale + coff + g * 8, sc);
+      load8(shift + coff + g * 8, sh);
       auto row = [&](long m, float* v) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -145,7 +155,7 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
     }
     if (pool) {
       lane_reduce<8>(red, rm, ps);
-      if (rm.lane == 0 && g < cg) store8(pool + (long)blockIdx.x * C + g * 8, ps);
+      if (rm.lane == 0 && g < cg) store8(pool + (long)blockIdx.x * C + cb + g * 8, ps);
     }
   }
 }
@@ -280,9 +290,10 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
     long HW, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ add_nc, int apply_elu, float* __restrict__ parts,
-    int rows_per_block, BwdFin fin, double* __restrict__ slots) {
+    int rows_per_block, BwdFin fin, double* __restrict__ slots, int cs) {
   extern __shared__ float red[];  // [256][16]
-  const int cg = C / 8;
+  const int cb = blockIdx.y * cs;  // channel slice (see bn_elu_fwd_kernel)
+  const int cg = cs / 8;
   const RowMap rm(cg);
   const long m0 = (long)blockIdx.x * rows_per_block;
   const long m1 = min(M, m0 + rows_per_block);
@@ -292,7 +303,7 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
     if (rm.active() && g < cg) {
-      const int c = g * 8;
+      const int c = cb + g * 8;
       float mu[8], is[8], sc[8], sh[8];
       load8(mean + c, mu);
       load8(invstd + c, is);
@@ -326,12 +337,12 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
           red[(rm.g * 8 + e) * 2 + 1] = acc[8 + e];
         }
       __syncthreads();
-      stat_slots_add_row(slots, blockIdx.x, C, g0 * 8, min(rm.G * 8, C - g0 * 8),
+      stat_slots_add_row(slots, blockIdx.x, C, cb + g0 * 8, min(rm.G * 8, cs - g0 * 8),
                          [&](int i) { return red[i]; });
       __syncthreads();
     } else if (rm.lane == 0 && g < cg) {
       {
-        float* o = parts + ((long)blockIdx.x * C + g * 8) * 2;
+        float* o = parts + ((long)blockIdx.x * C + cb + g * 8) * 2;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           o[2 * e] = acc[e];
@@ -381,17 +392,18 @@ struct ApplyFin {
   float dbias_scale;    // SyncBN: 1/world (DDP averages the ranks' bias gradients)
 };
 
-__device__ __forceinline__ void apply_fin_coeffs(const ApplyFin& f, int C,
+// s_k1..s_k3 hold channels [c0, c0 + n) at [c - c0]
+__device__ __forceinline__ void apply_fin_coeffs(const ApplyFin& f, int C, int c0, int n,
                                                  const float* __restrict__ invstd, float* s_k1,
                                                  float* s_k2, float* s_k3) {
-  const bool pub = blockIdx.x == 0;
+  const bool pub = blockIdx.x == 0;  // the first row block of every channel slice
   const double count = f.count > 0 ? f.count : f.slots[(long)UM_STAT_SLOTS * C * 2];
-  stat_slots_finish(f.slots, C, [&](int c, double s0, double s1) {
+  stat_slots_finish(f.slots, C, c0, n, [&](int c, double s0, double s1) {
     const float g = f.gamma ? f.gamma[c] : 1.f;
     const float a1 = g * invstd[c], a2 = (float)(s0 / count);
-    s_k1[c] = a1;
-    s_k2[c] = a2;
-    s_k3[c] = (float)(s1 / count);
+    s_k1[c - c0] = a1;
+    s_k2[c - c0] = a2;
+    s_k3[c - c0] = (float)(s1 / count);
     if (pub) {
       if (f.local == nullptr) {
         if (f.dgamma) f.dgamma[c] = (float)s1;
@@ -404,7 +416,7 @@ __device__ __forceinline__ void apply_fin_coeffs(const ApplyFin& f, int C,
   });
   // parameter grads from this rank's sums, like torch SyncBatchNorm
   if (pub && f.local != nullptr)
-    stat_slots_finish(f.local, C, [&](int c, double s0, double s1) {
+    stat_slots_finish(f.local, C, c0, n, [&](int c, double s0, double s1) {
       if (f.dgamma) f.dgamma[c] = (float)s1;
       if (f.dbeta) f.dbeta[c] = (float)s0;
     });
@@ -420,33 +432,36 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ add_nc, int apply_elu, const float* __restrict__ k1,
     const float* __restrict__ k2, const float* __restrict__ k3, T* __restrict__ dy, int lddy,
-    float* __restrict__ sum_parts, int rows_per_block, ApplyFin fin) {
-  extern __shared__ float red[];  // [256][8], then [3][C] coefficients (fin)
-  const int cg = C / 8;
+    float* __restrict__ sum_parts, int rows_per_block, ApplyFin fin, int cs) {
+  extern __shared__ float red[];  // [256][8], then [3][cs] coefficients (fin)
+  const int cb = blockIdx.y * cs;  // channel slice (see bn_elu_fwd_kernel)
+  const int cg = cs / 8;
   const RowMap rm(cg);
   const long m0 = (long)blockIdx.x * rows_per_block;
   const long m1 = min(M, m0 + rows_per_block);
+  int koff = cb;  // index of channel cb in k1..k3
   if (fin.slots != nullptr) {
     float* s_k = red + 256 * 8;
-    apply_fin_coeffs(fin, C, invstd, s_k, s_k + C, s_k + 2 * C);
+    apply_fin_coeffs(fin, C, cb, cs, invstd, s_k, s_k + cs, s_k + 2 * cs);
     k1 = s_k;
-    k2 = s_k + C;
-    k3 = s_k + 2 * C;
+    k2 = s_k + cs;
+    k3 = s_k + 2 * cs;
+    koff = 0;
   }
   for (int g0 = 0; g0 < cg; g0 += rm.G) {
     const int g = g0 + rm.g;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (rm.active() && g < cg) {
-      const int c = g * 8;
+      const int c = cb + g * 8;
       // dy = A*dz + B*y + D  with A = k1, B = -k1*k3*invstd, D = -k1*k2 + k1*k3*mean*invstd
       float sc[8], sh[8], A[8], B[8], D[8];
       {
         float mu[8], is[8], a1[8], a2[8], a3[8];
         load8(mean + c, mu);
         load8(invstd + c, is);
-        load8(k1 + c, a1);
-        load8(k2 + c, a2);
-        load8(k3 + c, a3);
+        load8(k1 + koff + g * 8, a1);
+        load8(k2 + koff + g * 8, a2);
+        load8(k3 + koff + g * 8, a3);
         load8(scale + c, sc);
         load8(shift + c, sh);
 #pragma unroll
@@ -486,7 +501,7 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
     }
     if (sum_parts) {
       lane_reduce<8>(red, rm, acc);
-      if (rm.lane == 0 && g < cg) store8(sum_parts + (long)blockIdx.x * C + g * 8, acc);
+      if (rm.lane == 0 && g < cg) store8(sum_parts + (long)blockIdx.x * C + cb + g * 8, acc);
     }
   }
 }
@@ -506,8 +521,54 @@ int um_bn_coeffs(const double* stats, double count, int C, const float* gamma, c
   return UM_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Channel-slice plan of the three BN passes: small layers (M * C up to 8M
+// elements) with C >= 128 take 64-channel slices (UMAMD_BN_SLICE = 0 turns
+// it off) and rows such that the grid has ~512 blocks (>= 32 rows: the 32
+// row lanes of a 64-channel block).
+struct Slices {
+  int cs, ns;
+};
+Slices bn_slices(long M, int C) {
+  static const int on = [] {
+    const char* e = getenv("UMAMD_BN_SLICE");
+    return e ? atoi(e) : 1;
+  }();
+  if (!on || C < 128 || C % 64 || M * C > (8l << 20)) return {C, 1};
+  return {64, C / 64};
+}
+int sliced_rows(long M, long HW, int ns) {
+  const long target = (512 + ns - 1) / ns;  // row blocks
+  long r = (M + target - 1) / target;
+  int p = 32;
+  while (p < r) p <<= 1;
+  long rr = p;
+  if (HW > 0) {
+    if (rr > HW) rr = HW;
+    while (HW % rr) --rr;
+  }
+  return (int)rr;
+}
+int fwd_rows_c(long M, long HW, int C) {
+  const Slices s = bn_slices(M, C);
+  return s.ns > 1 ? sliced_rows(M, HW, s.ns) : fwd_rows(M, HW);
+}
+int bwd_rows_c(long M, int C) {
+  const Slices s = bn_slices(M, C);
+  return s.ns > 1 ? sliced_rows(M, 0, s.ns) : bn_bwd_rows(M);
+}
+}  // namespace
+
+extern "C" {
+
 int um_bn_fwd_pool_parts(long M, long HW) {
   return HW > 0 && M % HW == 0 ? (int)(M / fwd_rows(M, HW)) : 0;
+}
+
+int um_bn_fwd_pool_parts_c(long M, long HW, int C) {
+  return HW > 0 && M % HW == 0 ? (int)(M / fwd_rows_c(M, HW, C)) : 0;
 }
 
 static int bn_fwd_launch(int dtype, long M, int C, const void* y, int ldy, const float* scale,
@@ -515,16 +576,19 @@ static int bn_fwd_launch(int dtype, long M, int C, const void* y, int ldy, const
                          float* pool_parts, const FwdFin& fin, hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0 && ldy % 8 == 0 && lda % 8 == 0, "um_bn_elu_fwd: C/ld not multiple of 8");
   UM_CHECK_ARG(pool_parts == nullptr || (HW > 0 && M % HW == 0), "um_bn_elu_fwd: HW");
-  const int rows = fwd_rows(M, pool_parts ? HW : 0);
-  const int g = ceil_div(M, rows);
+  const Slices sl = bn_slices(M, C);
+  const int rows = fwd_rows_c(M, pool_parts ? HW : 0, C);
+  const dim3 g(ceil_div(M, rows), sl.ns);
   const size_t shm = (pool_parts ? 256 * 8 * sizeof(float) : 0) +
-                     (fin.slots ? 2 * (size_t)C * sizeof(float) : 0);
+                     (fin.slots ? 2 * (size_t)sl.cs * sizeof(float) : 0);
   if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, dim3(g), dim3(256), shm, st, (const float*)y,
-                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu, rows, pool_parts, fin);
+    hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, g, dim3(256), shm, st, (const float*)y,
+                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu, rows, pool_parts, fin,
+                       sl.cs);
   else
-    hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, dim3(g), dim3(256), shm, st, (const float*)y,
-                       ldy, M, C, scale, shift, (float*)a, lda, apply_elu, rows, pool_parts, fin);
+    hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, g, dim3(256), shm, st, (const float*)y,
+                       ldy, M, C, scale, shift, (float*)a, lda, apply_elu, rows, pool_parts, fin,
+                       sl.cs);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -561,16 +625,21 @@ static int bwd_reduce_launch(int dtype, long M, int C, long HW, const void* da, 
                              int apply_elu, float* parts, const BwdFin& fin, double* slots,
                              hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_reduce: C %% 8");
-  const int blocks = um_bn_bwd_parts(M);
+  // channel slices only where the statistics go to slots (the partial rows
+  // of the other paths are sized by um_bn_bwd_parts, and the fused finish
+  // counts row blocks)
+  const Slices sl = slots != nullptr ? bn_slices(M, C) : Slices{C, 1};
+  const int rows = sl.ns > 1 ? bwd_rows_c(M, C) : bn_bwd_rows(M);
+  const dim3 blocks(ceil_div(M, rows), sl.ns);
   const size_t shm = 256 * 16 * sizeof(float);
   if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
+    hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<bf16_t>, blocks, dim3(256), shm, st,
                        (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, bn_bwd_rows(M), fin, slots);
+                       scale, shift, add_nc, apply_elu, parts, rows, fin, slots, sl.cs);
   else
-    hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), shm, st,
+    hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<float>, blocks, dim3(256), shm, st,
                        (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, bn_bwd_rows(M), fin, slots);
+                       scale, shift, add_nc, apply_elu, parts, rows, fin, slots, sl.cs);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -636,18 +705,20 @@ static int bwd_apply_launch(int dtype, long M, int C, long HW, const void* da, i
                             void* dy, int lddy, float* sum_parts, const ApplyFin& fin,
                             hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_apply: C %% 8");
-  const int blocks = um_bn_bwd_parts(M);
-  const size_t shm = 256 * 8 * sizeof(float) + (fin.slots ? 3 * (size_t)C * sizeof(float) : 0);
+  const Slices sl = (fin.slots != nullptr && sum_parts == nullptr) ? bn_slices(M, C) : Slices{C, 1};
+  const int rows = sl.ns > 1 ? bwd_rows_c(M, C) : bn_bwd_rows(M);
+  const dim3 blocks(ceil_div(M, rows), sl.ns);
+  const size_t shm = 256 * 8 * sizeof(float) + (fin.slots ? 3 * (size_t)sl.cs * sizeof(float) : 0);
   if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st,
+    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, blocks, dim3(256), shm, st,
                        (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
                        scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy, sum_parts,
-                       bn_bwd_rows(M), fin);
+                       rows, fin, sl.cs);
   else
-    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, dim3(blocks), dim3(256), shm, st,
+    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, blocks, dim3(256), shm, st,
                        (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
                        scale, shift, add_nc, apply_elu, k1, k2, k3, (float*)dy, lddy, sum_parts,
-                       bn_bwd_rows(M), fin);
+                       rows, fin, sl.cs);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

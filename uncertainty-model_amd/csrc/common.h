@@ -229,18 +229,21 @@ __device__ __forceinline__ void stat_slots_count(double* slots, int C, long coun
 // shuffle tree), so a block reads the 16 x C x 16 bytes in one round trip
 // for C <= 256; the fixed order makes every block's sums identical.  Must be
 // reached by all threads of the block.
+// Channel range [c0, c0 + n) only (a block that owns a channel slice).
 template <int SPL, class F>
-__device__ __forceinline__ void stat_slots_finish_t(const double* __restrict__ slots, int C, F fin) {
+__device__ __forceinline__ void stat_slots_finish_t(const double* __restrict__ slots, int C, int c0,
+                                                    int n, F fin) {
   constexpr int PER = UM_STAT_SLOTS / SPL;
-  const int total = C * SPL;
+  const int total = n * SPL;
   for (int base = 0; base < total; base += blockDim.x) {
     const int idx = base + threadIdx.x;
-    const int c = idx / SPL, part = idx % SPL;
+    const int c = c0 + idx / SPL, part = idx % SPL;
+    const bool in = c < c0 + n;
     double2 v[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      v[k] = c < C ? *reinterpret_cast<const double2*>(slots + ((long)(part + k * SPL) * C + c) * 2)
-                   : make_double2(0.0, 0.0);
+      v[k] = in ? *reinterpret_cast<const double2*>(slots + ((long)(part + k * SPL) * C + c) * 2)
+                : make_double2(0.0, 0.0);
     double s0 = 0.0, s1 = 0.0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -252,17 +255,23 @@ __device__ __forceinline__ void stat_slots_finish_t(const double* __restrict__ s
       s0 += __shfl_xor(s0, o, 64);
       s1 += __shfl_xor(s1, o, 64);
     }
-    if (c < C && part == 0) fin(c, s0, s1);
+    if (in && part == 0) fin(c, s0, s1);
   }
 }
 
 template <class F>
-__device__ __forceinline__ void stat_slots_finish(const double* __restrict__ slots, int C, F fin) {
+__device__ __forceinline__ void stat_slots_finish(const double* __restrict__ slots, int C, int c0,
+                                                  int n, F fin) {
   const int nt = blockDim.x;
-  if (16 * C <= nt) stat_slots_finish_t<16>(slots, C, fin);
-  else if (8 * C <= nt) stat_slots_finish_t<8>(slots, C, fin);
-  else if (4 * C <= nt) stat_slots_finish_t<4>(slots, C, fin);
-  else stat_slots_finish_t<2>(slots, C, fin);
+  if (16 * n <= nt) stat_slots_finish_t<16>(slots, C, c0, n, fin);
+  else if (8 * n <= nt) stat_slots_finish_t<8>(slots, C, c0, n, fin);
+  else if (4 * n <= nt) stat_slots_finish_t<4>(slots, C, c0, n, fin);
+  else stat_slots_finish_t<2>(slots, C, c0, n, fin);
+}
+
+template <class F>
+__device__ __forceinline__ void stat_slots_finish(const double* __restrict__ slots, int C, F fin) {
+  stat_slots_finish(slots, C, 0, C, fin);
 }
 
 // rows per block of the row-chunk reductions (RowMap kernels): aim at about

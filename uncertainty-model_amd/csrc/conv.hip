@@ -598,11 +598,18 @@ __global__ void __launch_bounds__(256) reflect_fold_kernel(const T* __restrict__
 
 // the padded form applies (knob pad_dgrad: 0 off, 1 for dx wider than
 // fold_split_nc -- the layers the one-pass fold gather served --, 2 all)
-bool pad_dgrad_applies(int C, int pad, int pad_mode, int stride, int P, int Q, int H, int W) {
+// -- except where the split form's zero-pad pass runs on the halo kernel (its
+// 64..192-wide column blocks: 128x256 C88 and 64x128 C168 decoder layers)
+bool split_form(int dtype, int N, int H, int W, int C, int R) {
+  return C <= umamd::igemm_fold_split_nc() || umamd::igemm_halo_dgrad(dtype, N, H, W, C, R);
+}
+
+bool pad_dgrad_applies(int dtype, int N, int C, int R, int pad, int pad_mode, int stride, int P,
+                       int Q, int H, int W) {
   const int kn = umamd::igemm_pad_dgrad();
   if (kn == 0 || pad_mode != UM_PAD_REFLECT || stride != 1 || pad <= 0 || pad >= H || pad >= W) return false;
   if (P != H || Q != W || C % 8) return false;
-  return kn == 2 || C > umamd::igemm_fold_split_nc();
+  return kn == 2 || !split_form(dtype, N, H, W, C, R);
 }
 
 long pad_dgrad_bytes(int dtype, int N, int H, int W, int C, int R, int K, int pad, long* gemm_off) {
@@ -620,7 +627,7 @@ extern "C" {
 long um_conv_dgrad_ws_pad(int dtype, int N, int H, int W, int C, int R, int K, int stride, int pad,
                           int pad_mode) {
   const long base = um_conv_dgrad_ws(dtype, N, H, W, C, R, K, stride);
-  if (!pad_dgrad_applies(C, pad, pad_mode, stride, H, W, H, W)) return base;
+  if (!pad_dgrad_applies(dtype, N, C, R, pad, pad_mode, stride, H, W, H, W)) return base;
   return std::max(base, pad_dgrad_bytes(dtype, N, H, W, C, R, K, pad, nullptr));
 }
 
@@ -682,7 +689,7 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
     UM_CHECK_ARG(pad_mode == UM_PAD_ZERO || (P == H && Q == W && pad <= 1),
                  "um_conv2d_dgrad: reflect transpose needs a same-size conv with pad <= 1");
     long goff = 0;
-    if (pad_dgrad_applies(C, pad, pad_mode, stride, P, Q, H, W) && ws != nullptr &&
+    if (pad_dgrad_applies(dtype, N, C, R, pad, pad_mode, stride, P, Q, H, W) && ws != nullptr &&
         ws_bytes >= pad_dgrad_bytes(dtype, N, H, W, C, R, K, pad, &goff)) {
       // padded form: zero-pad transposed conv onto the (H+2p) x (W+2p) padded
       // input (halo / LDS-DMA / register GEMM paths), then the reflect fold
@@ -718,7 +725,7 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
     // reflect pad, split form (narrow dx: the zero-pad pass takes the halo /
     // 256-row tiles, 117 vs 171 us at 256x512 C48) or one fold pass (wide dx:
     // the deep layers' border list is 18-34 % of their pixels)
-    const bool fold1 = pad_mode == UM_PAD_REFLECT && pad > 0 && C > umamd::igemm_fold_split_nc();
+    const bool fold1 = pad_mode == UM_PAD_REFLECT && pad > 0 && !split_form(dtype, N, H, W, C, R);
     a.pmode = fold1 ? umamd::IG_FOLD : umamd::IG_PAD_ZERO;
     a.fold_pad = fold1 ? pad : 0; a.flip = 1;
     a.b = wT; a.ldb = (long)R * R * K;

@@ -8,7 +8,7 @@
 
 namespace umamd {
 
-bool halo_applicable(int dtype, const IgArgs& a, int min_tiles);
+bool halo_applicable(int dtype, const IgArgs& a, int min_tiles, int max_nc);
 int halo_run(const IgArgs& a, hipStream_t st);
 
 }  // namespace umamd

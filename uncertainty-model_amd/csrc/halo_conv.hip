@@ -8,7 +8,8 @@
 // channels is more than the MFMAs can consume (the 7x7 32->32 layers reached
 // ~290 TFLOP/s).  Here a workgroup owns an 8 x 32 output-pixel tile of one
 // image and up to 64 output channels, stages the (8+R-1) x (32+R-1) input
-// halo of one 32-channel chunk ONCE in LDS and runs all R*R taps from it:
+// halo of one 32-channel chunk ONCE in LDS and runs all R*R taps from it
+// (wider outputs: a grid column of such blocks per 64/96/128 channels):
 //   - A fragments (16 pixels x 32 channels) are ds_read_b128 of 16
 //     consecutive halo pixels; the 16-byte channel chunks of a pixel are
 //     XOR-swizzled by bits 2-3 of the pixel index, so any 16 consecutive
@@ -264,10 +265,24 @@ int launch_r(const IgArgs& a, hipStream_t st) {
   return UM_OK;
 }
 
+// Output-column block width: up to 64 columns one block; wider outputs (the
+// decoder's 88/128/168-channel convs and data gradients) take column blocks of
+// 64, 96 or 128 (3x3 only: the double-buffered tap-row weights of a 128-wide
+// 5x5/7x7 block would not fit LDS), whichever pads the fewest columns (ties:
+// the wider block, fewer re-reads of the halo).
 template <int R>
 int launch_bn(const IgArgs& a, hipStream_t st) {
   if (a.NC <= 16) return launch_r<R, 16>(a, st);
   if (a.NC <= 32) return launch_r<R, 32>(a, st);
+  if (a.NC <= 64) return launch_r<R, 64>(a, st);
+  if constexpr (R == 3) {
+    auto padded = [&](int bn) { return (a.NC + bn - 1) / bn * bn; };
+    int bn = 128;
+    if (padded(96) < padded(bn)) bn = 96;
+    if (padded(64) < padded(bn)) bn = 64;
+    if (bn == 128) return launch_r<R, 128>(a, st);
+    if (bn == 96) return launch_r<R, 96>(a, st);
+  }
   return launch_r<R, 64>(a, st);
 }
 
@@ -275,15 +290,17 @@ int launch_bn(const IgArgs& a, hipStream_t st) {
 
 namespace umamd {
 
-bool halo_applicable(int dtype, const IgArgs& a, int min_tiles) {
+bool halo_applicable(int dtype, const IgArgs& a, int min_tiles, int max_nc) {
   if (dtype != UM_BF16 || a.stride != 1 || a.cls) return false;
   if (a.R != 3 && a.R != 5 && a.R != 7) return false;
   if (a.pmode == IG_FOLD) return false;                         // reflect transpose: igemm
   if (a.flip && a.pmode != IG_PAD_ZERO) return false;
   if (a.oh != a.ah || a.ow != a.aw || a.pad != (a.R - 1) / 2) return false;  // "same" conv
   if (a.oh % TH || a.ow % TW) return false;
-  if (a.NC > 64 || a.ach % 8 || a.lda % 8) return false;
-  if (a.epilogue == UM_EPI_STATS && a.stats_rows != 128) return false;
+  if (a.NC > max_nc || a.ach % 8 || a.lda % 8) return false;
+  // partial-row statistics follow the GEMM's 128-row layout; the f64 slots
+  // (stat_slots) take any tiling
+  if (a.epilogue == UM_EPI_STATS && !a.stat_slots && a.stats_rows != 128) return false;
   // enough tiles to fill the chip
   return (long)a.on * (a.oh / TH) * (a.ow / TW) >= min_tiles;
 }

@@ -62,6 +62,7 @@ int igemm_run_cls4(int dtype, IgArgs (&as)[4], hipStream_t st);
 // pass, the others as a zero-pad pass + the border-list pass (knob
 // "fold_split_nc", UMAMD_FOLD_SPLIT_NC)
 int igemm_fold_split_nc();
+bool igemm_halo_dgrad(int dtype, int N, int H, int W, int C, int R);
 
 // reflect data gradients in the padded form (knob pad_dgrad): 0 off, 1 for
 // dx wider than fold_split_nc, 2 all

@@ -864,6 +864,7 @@ struct Knobs {
   int cls4;
   int pad_dgrad;
   int fold_split_nc;
+  int halo_max_nc;
   Knobs() {
     auto env = [](const char* n, int d) {
       const char* v = getenv(n);
@@ -887,6 +888,9 @@ struct Knobs {
     split_minsteps = env("UMAMD_IG_SPLIT_MINSTEPS", 4);
     halo = env("UMAMD_HALO", 1);
     halo_min_tiles = env("UMAMD_HALO_MIN_TILES", 256);
+    // widest output (columns) the halo kernel takes: 64 = one column block
+    // (round 2); up to 192 adds 96/128-wide 3x3 blocks and column grids
+    halo_max_nc = env("UMAMD_HALO_MAX_NC", 192);
     odd_bn = env("UMAMD_IG_ODD_BN", 1);
     // bit 0: 64-deep k-steps for the 64x64 tiles, bit 1: for the 128-row tiles
     bk64 = env("UMAMD_IG_BK64", 3);
@@ -1076,6 +1080,15 @@ int dispatch_tiles(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
 namespace umamd {
 
 int igemm_fold_split_nc() { return knobs().fold_split_nc; }
+
+// the zero-pad pass of a reflect data gradient in split form would run on
+// the halo kernel ("same" 3x3/5x5/7x7, 8x32 tiles, enough of them)
+bool igemm_halo_dgrad(int dtype, int N, int H, int W, int C, int R) {
+  const Knobs& k = knobs();
+  if (!k.halo || dtype != UM_BF16 || (R != 3 && R != 5 && R != 7)) return false;
+  if (H % 8 || W % 32 || C > k.halo_max_nc || C % 8) return false;
+  return (long)N * (H / 8) * (W / 32) >= k.halo_min_tiles;
+}
 int igemm_pad_dgrad() { return knobs().pad_dgrad; }
 
 int igemm_border_list(IgArgs& a) {
@@ -1120,7 +1133,8 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   // 8-channel operands take the tap-packed GEMM instead of the halo kernel
   // (which stages 32-channel chunks) unless tappack bit 1 is clear
   const bool pack_first = (knobs().tappack & 3) == 3 && a.ach == 8;
-  if (knobs().halo && !pack_first && halo_applicable(dtype, a, knobs().halo_min_tiles))
+  if (knobs().halo && !pack_first &&
+      halo_applicable(dtype, a, knobs().halo_min_tiles, knobs().halo_max_nc))
     return halo_run(a, st);
   // the LDS-DMA loop serves the bf16 64x64 tiles without the reflect fold
   Plan p = make_plan(dtype, a.M, a.NC, a.R * a.Rx, a.ach, ws ? ws_bytes : 0, false);
@@ -1197,6 +1211,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "pad_dgrad")) f = &k.pad_dgrad;
   else if (!strcmp(key, "glds_deep_blocks")) f = &k.glds_deep_blocks;
   else if (!strcmp(key, "fold_split_nc")) f = &k.fold_split_nc;
+  else if (!strcmp(key, "halo_max_nc")) f = &k.halo_max_nc;
   if (!f) return -1;
   const int old = *f;
   *f = value;

@@ -102,6 +102,19 @@ class _GraphSteps:
         self.scales = scales
         self.key = None
         self.cap = None
+        self._stream = None
+
+    @property
+    def stream(self):
+        """ONE stream for every capture and every eager fallback step of the
+        loop: autograd's AccumulateGrad nodes remember the stream they were
+        created on, and a capture whose backward meets a node of another
+        stream (e.g. one an eager ragged-batch step left alive) synchronises
+        with it and breaks (measured: segfault in hipStreamEndCapture on the
+        recapture after a ragged eager step on the null stream)."""
+        if self._stream is None:
+            self._stream = getattr(self.model, '_umamd_stream', None) or torch.cuda.Stream()
+        return self._stream
 
     @staticmethod
     def usable(model, loss_function, optimiser, disc) -> bool:
@@ -129,9 +142,8 @@ class _GraphSteps:
         if self.key != key:
             self.cap = None  # scale changed: drop the old graphs before capturing
             torch.cuda.synchronize()
-            stream = getattr(self.model, '_umamd_stream', None)
             self.cap = CapturedTrainStep(self.model, self.loss_function, self.optimiser, left,
-                                         right, scale, scales=self.scales, stream=stream)
+                                         right, scale, scales=self.scales, stream=self.stream)
             self.key = key
         return self.cap(left, right)
 
@@ -168,6 +180,16 @@ def train_one_epoch(model: Module, loader: DataLoader, loss_function: Module,
         if out is not None:
             disp_loss, error_loss = out
             disc_loss = None
+        elif graphs is not None:
+            # a batch of another shape: one eager step on the loop's capture
+            # stream (see _GraphSteps.stream)
+            cur = torch.cuda.current_stream()
+            graphs.stream.wait_stream(cur)
+            with torch.cuda.stream(graphs.stream):
+                disp_loss, error_loss, disc_loss = train_step(
+                    model, left, right, loss_function, model_optimiser, scale, scales, i, disc,
+                    disc_clone, disc_optimiser, disc_loss_function, batch_size=loader.batch_size)
+            cur.wait_stream(graphs.stream)
         else:
             disp_loss, error_loss, disc_loss = train_step(
                 model, left, right, loss_function, model_optimiser, scale, scales, i, disc,

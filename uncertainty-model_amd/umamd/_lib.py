@@ -65,6 +65,7 @@ _SIG = {
     'um_bn_bwd_stats_coeffs': (_I, [_P, _I, _I, _P, _D, _P, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_coeffs': (_I, [_P, _D, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_fwd_pool_parts': (_I, [_L, _L]),
+    'um_bn_fwd_pool_parts_c': (_I, [_L, _L, _I]),
     'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, _L, _P, 's']),
     'um_bn_elu_fwd_slots': (_I, [_I, _L, _I, _P, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P, _P, _P,
                                  _P, _P, _P, _I, _I, _L, _P, 's']),

@@ -125,8 +125,11 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
     # launch stream instead of taking it over.  dw stays alive as param.grad.
     dw.record_stream(ov.stream)
     dw_ptr = ptr(dw)
+    N, _, _, _ = x.shape
+    _, P, Q, _ = dy.shape
     ov.defer((x, dy), lambda: _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad,
-                                             pad_mode, dw_ptr, segs), out_ptr=dw_ptr)
+                                             pad_mode, dw_ptr, segs), out_ptr=dw_ptr,
+             flop=_conv_flops(N, P, Q, Kreal, R, Creal))
     return dw
 
 
@@ -391,7 +394,7 @@ class ConvBNELUFn(torch.autograd.Function):
         a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y is f32 (pre-BN)
         pool = None
         if w1 is not None and _FUSED_SE:  # the SE squeeze rides in the BN-apply pass
-            npool = query('um_bn_fwd_pool_parts', M, P * Q)
+            npool = query('um_bn_fwd_pool_parts_c', M, P * Q, K)
             pool = torch.empty((npool, K), dtype=torch.float32, device=dev)
         if slots_f is not None:
             upd = bn.track_running_stats and bn.running_mean is not None

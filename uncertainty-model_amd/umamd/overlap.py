@@ -41,6 +41,11 @@ class WgradStream:
         self.stream = torch.cuda.Stream()
         self.params = list(params)
         self.batch = batch or int(os.environ.get('UMAMD_WGRAD_BATCH', '24'))
+        # also flush once the queued weight gradients hold this much work
+        # (GFLOP; 0 = count only): a large one then starts at once instead
+        # of waiting for the batch to fill (or for the end of the backward)
+        self.flush_flop = float(os.environ.get('UMAMD_WGRAD_FLUSH_GFLOP', '0')) * 1e9
+        self._queued_flop = 0.0
         self._launch = None
         self._pending = []
         self._pending_out = set()
@@ -56,15 +61,18 @@ class WgradStream:
         WgradStream._active = self
         return self
 
-    def defer(self, tensors, launch, out_ptr=None):
+    def defer(self, tensors, launch, out_ptr=None, flop=0.0):
         """Queue one weight gradient (``launch`` issues its kernels on the
         current stream; ``tensors`` are the ones it touches, ``out_ptr`` the
-        address it writes) and flush the queue onto the side stream every
-        ``batch`` entries: one fork per batch instead of one per conv."""
+        address it writes, ``flop`` its work) and flush the queue onto the
+        side stream every ``batch`` entries (or ``flush_flop`` of work): one
+        fork per batch instead of one per conv."""
         self._pending.append((tensors, launch))
+        self._queued_flop += flop
         if out_ptr is not None:
             self._pending_out.add(out_ptr)
-        if len(self._pending) >= self.batch:
+        if len(self._pending) >= self.batch or \
+                (self.flush_flop > 0 and self._queued_flop >= self.flush_flop):
             self._flush()
 
     def is_pending(self, ptrs) -> bool:
@@ -89,6 +97,7 @@ class WgradStream:
                 t.record_stream(self.stream)
         self._pending = []
         self._pending_out.clear()
+        self._queued_flop = 0.0
         for fn in self._on_flush:
             fn()
 
