@@ -298,6 +298,10 @@ bool halo_applicable(int dtype, const IgArgs& a, int min_tiles, int max_nc) {
   if (a.oh != a.ah || a.ow != a.aw || a.pad != (a.R - 1) / 2) return false;  // "same" conv
   if (a.oh % TH || a.ow % TW) return false;
   if (a.NC > max_nc || a.ach % 8 || a.lda % 8) return false;
+  // 8-channel operands fill a quarter of each 32-channel chunk: past one
+  // 64-column block the tap-packed GEMM is faster (disp-head data gradient
+  // 64x128 C128 K8: 35 us tap-packed vs 49 us on 128-wide halo blocks)
+  if (a.ach < 32 && a.NC > 64) return false;
   // partial-row statistics follow the GEMM's 128-row layout; the f64 slots
   // (stat_slots) take any tiling
   if (a.epilogue == UM_EPI_STATS && !a.stat_slots && a.stats_rows != 128) return false;

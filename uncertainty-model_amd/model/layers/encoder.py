@@ -102,6 +102,8 @@ class GraphBlock(nn.Module):
             self.node_blocks.append(NodeBlock(node, in_channels, out_channels, kernel_size))
 
     def _fwd(self, x: Tensor) -> Tensor:
+        if U._STAGE_FN:  # the whole block as one autograd node (umamd.functional.GraphBlockFn)
+            return U.graph_block(x, self)
         results = {idx: self.node_blocks[idx]._fwd(x) for idx in self.in_nodes}
         for idx, node in enumerate(self.nodes):
             if idx in self.in_nodes:

@@ -154,20 +154,49 @@ def _colred_ws(nparts, C, nv, device):
     return torch.empty((max(n, 8) // 8,), dtype=torch.float64, device=device)
 
 
-def _reduce_rows(parts, nparts, C, out, accumulate=False):
-    call('um_reduce_rows', ptr(parts), nparts, C, C, ptr(out), int(accumulate),
+def _reduce_rows(parts, nparts, C, out, accumulate=False, out_ptr=None):
+    call('um_reduce_rows', ptr(parts), nparts, C, C, out_ptr or ptr(out), int(accumulate),
          ptr(_colred_ws(nparts, C, 1, parts.device)))
     return out
 
 
 def _colsum(y, C):
     """sum over pixels of y[..., :C] -> f32 [C]"""
+    out = torch.empty((C,), dtype=torch.float32, device=y.device)
+    _colsum_into(y, C, ptr(out))
+    return out
+
+
+def _colsum_into(y, C, out_ptr):
     M = y.numel() // y.shape[-1]
     parts_n = query('um_colsum_parts', M)
     parts = torch.empty((parts_n, C), dtype=torch.float32, device=y.device)
     call('um_colsum', _dt(y), M, C, y.shape[-1], ptr(y), ptr(parts))
+    _reduce_rows(parts, parts_n, C, None, out_ptr=out_ptr)
+
+
+def _param_grad(tensors, out, launch):
+    """Launches whose only product is a parameter gradient ``out`` (read
+    by the optimiser after the whole backward): under overlap.WgradStream
+    they are queued onto the weight-gradient side stream like the conv
+    weight gradients (off the data-gradient chain), else run now.
+    ``tensors``: what ``launch`` reads; ``launch`` must reach ``out`` by
+    address only (as _conv_wgrad: a second reference would make autograd's
+    AccumulateGrad copy the not yet written gradient instead of taking it)."""
+    ov = _overlap.active()
+    if ov is None:
+        launch()
+        return out
+    out.record_stream(ov.stream)
+    ov.defer(tensors, launch, out_ptr=out.data_ptr())
+    return out
+
+
+def _colsum_grad(y, C):
+    """a bias gradient (sum over pixels of y[..., :C]) as _param_grad"""
     out = torch.empty((C,), dtype=torch.float32, device=y.device)
-    return _reduce_rows(parts, parts_n, C, out)
+    optr = ptr(out)
+    return _param_grad((y,), out, lambda: _colsum_into(y, C, optr))
 
 
 _CONSTS = {}
@@ -338,217 +367,248 @@ class ConvSpec:
         self.elu = elu
 
 
+class _CBEState:
+    """What a conv+BN+ELU forward keeps for its backward (the autograd ctx
+    of ConvBNELUFn, or one node of a GraphBlockFn)."""
+    __slots__ = ('spec', 'sync', 'slots_b', 'has_bn', 'geom', 'se', 'saved')
+
+
+def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec):
+    """Conv2d -> BatchNorm2d -> ELU [-> SE gate] forward without autograd:
+    -> (outputs tuple, _CBEState)"""
+    ctx = _CBEState()
+    L.require_device(x)
+    N, H, W, Cp = x.shape
+    K, Creal, R, _ = weight.shape
+    bn = spec.bn
+    dev = x.device
+    wf, wT = _pack(weight, Cp, x.dtype, segs=spec.segs)
+    P = (H + 2 * spec.pad - R) // spec.stride + 1
+    Q = (W + 2 * spec.pad - R) // spec.stride + 1
+    M = N * P * Q
+    bias_f = bias.detach().float().contiguous() if bias is not None else None
+    slots_f = slots_b = None
+    if bn is not None:
+        training = bn.training
+        sync = BNSync(bn)
+    count = float(M)
+    if bn is not None and training and _ARENA is not None:
+        # statistics in f64 slots: the conv adds them atomically, the BN
+        # apply finishes them (no reduction launch).  SyncBN: the slots
+        # and this rank's element count after them are all-reduced in
+        # place (the count rides along: uneven per-rank batches)
+        if bn.track_running_stats and bn.running_mean is not None and bn.momentum is None:
+            raise NotImplementedError('BatchNorm momentum=None (cumulative average) is not supported')
+        nslot = L.STAT_SLOTS * K * 2
+        slots_f = _ARENA.take(nslot + 1)
+        slots_b = _ARENA.take(nslot + 1)
+        y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
+                      out_dtype=torch.float32, epi=L.EPI_STAT_SLOTS, stats=slots_f,
+                      creal=Creal)
+        if sync.collective:  # the conv stored this rank's count after the slots
+            sync.all_reduce(slots_f)
+            count = -1.0  # read the all-reduced count after the slots
+        mean = torch.empty(K, dtype=torch.float32, device=dev)
+        invstd = torch.empty_like(mean)
+        scale = torch.empty_like(mean)
+        shift = torch.empty_like(mean)
+    elif bn is not None:
+        nparts = query('um_conv_stats_parts', M, K)
+        parts = torch.empty((nparts, K, 2), dtype=torch.float32, device=dev)
+        y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
+                      out_dtype=torch.float32,
+                      epi=L.EPI_STATS if training else L.EPI_NONE, stats=parts, creal=Creal)
+        mean, invstd, scale, shift = _bn_forward_coeffs(parts, nparts, K, M, bn, sync,
+                                                        training, dev)
+    else:  # ConvELUBlock(batch_norm=False): identity normalisation
+        sync = None
+        training = False
+        y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
+                      out_dtype=torch.float32, creal=Creal)
+        mean = shift = _const_vec(0.0, K, dev)
+        invstd = scale = _const_vec(1.0, K, dev)
+    a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y is f32 (pre-BN)
+    pool = None
+    if w1 is not None and _FUSED_SE:  # the SE squeeze rides in the BN-apply pass
+        npool = query('um_bn_fwd_pool_parts_c', M, P * Q, K)
+        pool = torch.empty((npool, K), dtype=torch.float32, device=dev)
+    if slots_f is not None:
+        upd = bn.track_running_stats and bn.running_mean is not None
+        nbt = bn.num_batches_tracked if upd else None
+        call('um_bn_elu_fwd_slots', _dt(a), M, K, ptr(y), K, ptr(slots_f), count,
+             ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0),
+             ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
+             ptr(nbt), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K,
+             int(spec.elu), P * Q, ptr(pool))
+    else:
+        call('um_bn_elu_fwd', _dt(a), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
+             int(spec.elu), P * Q, ptr(pool))
+    inv_hw = 1.0 / (P * Q)
+    if w1 is not None and not _FUSED_SE:  # separate squeeze: the means, one row per image
+        npool, inv_hw = N, 1.0
+        pool = torch.zeros((N, K), dtype=torch.float32, device=dev)
+        call('um_channel_mean', _dt(a), N, P * Q, K, ptr(a), K, ptr(pool))
+    outs = [a]
+    se = None
+    if w1 is not None:
+        R1 = w1.shape[0]
+        pooled = torch.empty((N, K), dtype=torch.float32, device=dev)
+        z1 = torch.empty((N, R1), dtype=torch.float32, device=dev)
+        s = torch.empty((N, K), dtype=torch.float32, device=dev)
+        w1c, w2c = w1.detach().float().contiguous(), w2.detach().float().contiguous()
+        call('um_se_mlp_fwd', N, K, R1, ptr(pool), npool // N, inv_hw, ptr(pooled),
+             ptr(w1c), ptr(w2c), ptr(z1), ptr(s))
+        se = (pooled, z1, s)
+        outs.append(s)
+    ctx.spec = spec
+    ctx.sync = sync
+    ctx.slots_b = slots_b
+    ctx.has_bn = bn is not None and training
+    ctx.geom = (N, H, W, Cp, K, Creal, R, P, Q)
+    ctx.se = se
+    ctx.saved = (x, wT, y, mean, invstd, scale, shift, gamma, w1, w2)
+    return tuple(outs), ctx
+
+
+def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=False):
+    """Backward of _cbe_fwd -> (dx, dW, dbias, dgamma, dbeta, dw1, dw2).
+    ``dx``: write (or with ``dx_accumulate`` add) the input gradient into
+    this tensor instead of a new one (a GraphBlockFn predecessor's gradient
+    buffer)."""
+    x, wT, y, mean, invstd, scale, shift, gamma, w1, w2 = ctx.saved
+    N, H, W, Cp, K, Creal, R, P, Q = ctx.geom
+    spec = ctx.spec
+    M = N * P * Q
+    dev = y.device
+    adt = x.dtype
+    da = da.contiguous() if da is not None else torch.zeros(y.shape, dtype=adt, device=dev)
+    if da.dtype != adt:
+        da = da.to(adt)
+    add_nc = None
+    dw1 = dw2 = None
+    if ctx.se is not None and ds is not None:
+        pooled, z1, s = ctx.se
+        R1 = w1.shape[0]
+        dw1 = torch.empty(w1.shape, dtype=torch.float32, device=dev)
+        dw2 = torch.empty(w2.shape, dtype=torch.float32, device=dev)
+        add_nc = torch.empty((N, K), dtype=torch.float32, device=dev)
+        dz = torch.empty((N, R1), dtype=torch.float32, device=dev)
+        dsc = ds.float().contiguous()
+        w1c, w2c = w1.detach().float().contiguous(), w2.detach().float().contiguous()
+        call('um_se_mlp_bwd', N, K, R1, ptr(dsc), ptr(s), ptr(z1), ptr(pooled), ptr(w1c),
+             ptr(w2c), ptr(dw1), ptr(dw2), ptr(add_nc), ptr(dz), 1.0 / (P * Q))
+    dgamma = dbeta = dbias = None
+    slots_b = ctx.slots_b
+    if ctx.has_bn and slots_b is not None:
+        # backward sums into the slots; the apply kernel finishes them
+        if need_b:
+            dbias = torch.empty(K, dtype=torch.float32, device=dev)
+        if gamma is not None:
+            dgamma = torch.empty(K, dtype=torch.float32, device=dev)
+            dbeta = torch.empty(K, dtype=torch.float32, device=dev)
+        call('um_bn_elu_bwd_reduce_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+             ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+             ptr(slots_b))
+        local, bcount, bscale = None, float(M), 1.0
+        if ctx.sync is not None and ctx.sync.collective:
+            # dgamma/dbeta from this rank's sums (torch SyncBatchNorm),
+            # k1..k3 and the conv-bias gradient from the global ones
+            local = slots_b.clone()  # the reduce kernel stored the count after the slots
+            ctx.sync.all_reduce(slots_b)
+            bcount, bscale = -1.0, 1.0 / ctx.sync.world
+    elif ctx.has_bn:
+        k1 = torch.empty(K, dtype=torch.float32, device=dev)
+        k2 = torch.empty_like(k1)
+        k3 = torch.empty_like(k1)
+        # the conv bias feeds a training-mode BN: its gradient comes out of
+        # the coefficient kernel in closed form (no reduction of dy)
+        if need_b:
+            dbias = torch.empty(K, dtype=torch.float32, device=dev)
+        nb = query('um_bn_bwd_parts', M)
+        parts = torch.empty((nb, K, 2), dtype=torch.float32, device=dev)
+        world = ctx.sync.world if ctx.sync is not None else 1
+        if gamma is not None:
+            dgamma = torch.empty(K, dtype=torch.float32, device=dev)
+            dbeta = torch.empty(K, dtype=torch.float32, device=dev)
+        single = ctx.sync is None or not ctx.sync.collective
+        if single and _FUSED_BN_BWD:
+            # one launch: the reduce kernel's last blocks finish the coefficients
+            fin = torch.empty((query('um_bn_bwd_fin_ws', M, K) // 8,), dtype=torch.float64,
+                              device=dev)
+            call('um_bn_elu_bwd_reduce_coeffs', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+                 ptr(parts), ptr(fin), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dbias),
+                 ptr(k1), ptr(k2), ptr(k3))
+        elif single:
+            call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+                 ptr(parts))
+            call('um_bn_bwd_stats_coeffs', ptr(parts), nb, K, ptr(_colred_ws(nb, K, 2, dev)),
+                 float(M), ptr(gamma), ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(dbias),
+                 ptr(k1), ptr(k2), ptr(k3))
+        else:
+            call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+                 ptr(parts))
+            ws = _colred_ws(nb, K, 2, dev)
+            st = torch.empty((K + 1, 2), dtype=torch.float64, device=dev)
+            st[K].fill_(float(M))  # this rank's count, summed by the all-reduce
+            call('um_bn_stats_reduce', ptr(parts), nb, K, ptr(st), ptr(ws))
+            st_local = st.clone()
+            ctx.sync.all_reduce(st)
+            call('um_bn_bwd_coeffs', ptr(st), -1.0, K, ptr(gamma), ptr(invstd),
+                 ptr(st_local), ptr(dgamma), ptr(dbeta), ptr(dbias), 1.0 / world, 0,
+                 ptr(k1), ptr(k2), ptr(k3))
+    else:
+        # no batch statistics (no BN, or BN in eval mode): dy = dz * scale
+        k1 = scale
+        k2 = k3 = _const_vec(0.0, K, dev)
+        if gamma is not None and spec.bn is not None:
+            raise NotImplementedError('backward through an eval-mode BatchNorm')
+    dy = torch.empty(y.shape, dtype=adt, device=dev)
+    nbp = query('um_bn_bwd_parts', M)
+    reduce_b = need_b and dbias is None
+    bparts = torch.empty((nbp, K), dtype=torch.float32, device=dev) if reduce_b else None
+    if ctx.has_bn and slots_b is not None:
+        call('um_bn_elu_bwd_apply_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+             ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+             ptr(slots_b), bcount, ptr(local), ptr(gamma), ptr(dgamma), ptr(dbeta),
+             ptr(dbias), bscale, ptr(dy), K)
+    else:
+        call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
+             ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1),
+             ptr(k2), ptr(k3), ptr(dy), K, ptr(bparts))
+    dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode,
+                     segs=spec.segs)
+    if reduce_b:
+        dbias = torch.empty(K, dtype=torch.float32, device=dev)
+        _reduce_rows(bparts, nbp, K, dbias)
+    if need_x:
+        dx = _conv_dgrad(dy, wT, (N, H, W, Cp), K, R, spec.stride, spec.pad, spec.pad_mode,
+                         dx=dx, accumulate=dx_accumulate, creal=Creal)
+    else:
+        dx = None
+    return dx, dW, dbias, dgamma, dbeta, dw1, dw2
+
+
 class ConvBNELUFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec):
-        L.require_device(x)
-        N, H, W, Cp = x.shape
-        K, Creal, R, _ = weight.shape
-        bn = spec.bn
-        dev = x.device
-        wf, wT = _pack(weight, Cp, x.dtype, segs=spec.segs)
-        P = (H + 2 * spec.pad - R) // spec.stride + 1
-        Q = (W + 2 * spec.pad - R) // spec.stride + 1
-        M = N * P * Q
-        bias_f = bias.detach().float().contiguous() if bias is not None else None
-        slots_f = slots_b = None
-        if bn is not None:
-            training = bn.training
-            sync = BNSync(bn)
-        count = float(M)
-        if bn is not None and training and _ARENA is not None:
-            # statistics in f64 slots: the conv adds them atomically, the BN
-            # apply finishes them (no reduction launch).  SyncBN: the slots
-            # and this rank's element count after them are all-reduced in
-            # place (the count rides along: uneven per-rank batches)
-            if bn.track_running_stats and bn.running_mean is not None and bn.momentum is None:
-                raise NotImplementedError('BatchNorm momentum=None (cumulative average) is not supported')
-            nslot = L.STAT_SLOTS * K * 2
-            slots_f = _ARENA.take(nslot + 1)
-            slots_b = _ARENA.take(nslot + 1)
-            y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
-                          out_dtype=torch.float32, epi=L.EPI_STAT_SLOTS, stats=slots_f,
-                          creal=Creal)
-            if sync.collective:  # the conv stored this rank's count after the slots
-                sync.all_reduce(slots_f)
-                count = -1.0  # read the all-reduced count after the slots
-            mean = torch.empty(K, dtype=torch.float32, device=dev)
-            invstd = torch.empty_like(mean)
-            scale = torch.empty_like(mean)
-            shift = torch.empty_like(mean)
-        elif bn is not None:
-            nparts = query('um_conv_stats_parts', M, K)
-            parts = torch.empty((nparts, K, 2), dtype=torch.float32, device=dev)
-            y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
-                          out_dtype=torch.float32,
-                          epi=L.EPI_STATS if training else L.EPI_NONE, stats=parts, creal=Creal)
-            mean, invstd, scale, shift = _bn_forward_coeffs(parts, nparts, K, M, bn, sync,
-                                                            training, dev)
-        else:  # ConvELUBlock(batch_norm=False): identity normalisation
-            sync = None
-            training = False
-            y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
-                          out_dtype=torch.float32, creal=Creal)
-            mean = shift = _const_vec(0.0, K, dev)
-            invstd = scale = _const_vec(1.0, K, dev)
-        a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y is f32 (pre-BN)
-        pool = None
-        if w1 is not None and _FUSED_SE:  # the SE squeeze rides in the BN-apply pass
-            npool = query('um_bn_fwd_pool_parts_c', M, P * Q, K)
-            pool = torch.empty((npool, K), dtype=torch.float32, device=dev)
-        if slots_f is not None:
-            upd = bn.track_running_stats and bn.running_mean is not None
-            nbt = bn.num_batches_tracked if upd else None
-            call('um_bn_elu_fwd_slots', _dt(a), M, K, ptr(y), K, ptr(slots_f), count,
-                 ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0),
-                 ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
-                 ptr(nbt), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K,
-                 int(spec.elu), P * Q, ptr(pool))
-        else:
-            call('um_bn_elu_fwd', _dt(a), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
-                 int(spec.elu), P * Q, ptr(pool))
-        inv_hw = 1.0 / (P * Q)
-        if w1 is not None and not _FUSED_SE:  # separate squeeze: the means, one row per image
-            npool, inv_hw = N, 1.0
-            pool = torch.zeros((N, K), dtype=torch.float32, device=dev)
-            call('um_channel_mean', _dt(a), N, P * Q, K, ptr(a), K, ptr(pool))
-        outs = [a]
-        se = None
-        if w1 is not None:
-            R1 = w1.shape[0]
-            pooled = torch.empty((N, K), dtype=torch.float32, device=dev)
-            z1 = torch.empty((N, R1), dtype=torch.float32, device=dev)
-            s = torch.empty((N, K), dtype=torch.float32, device=dev)
-            w1c, w2c = w1.detach().float().contiguous(), w2.detach().float().contiguous()
-            call('um_se_mlp_fwd', N, K, R1, ptr(pool), npool // N, inv_hw, ptr(pooled),
-                 ptr(w1c), ptr(w2c), ptr(z1), ptr(s))
-            se = (pooled, z1, s)
-            outs.append(s)
-        ctx.spec = spec
-        ctx.sync = sync
-        ctx.slots_b = slots_b
-        ctx.has_bn = bn is not None and training
-        ctx.geom = (N, H, W, Cp, K, Creal, R, P, Q)
-        ctx.se = se
-        ctx.save_for_backward(x, wT, y, mean, invstd, scale, shift, gamma, w1, w2)
-        return tuple(outs) if len(outs) > 1 else outs[0]
+        outs, st = _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec)
+        x_, wT, y, mean, invstd, scale, shift, gamma_, w1_, w2_ = st.saved
+        st.saved = None
+        ctx.st = st
+        ctx.save_for_backward(x_, wT, y, mean, invstd, scale, shift, gamma_, w1_, w2_)
+        return outs if len(outs) > 1 else outs[0]
 
     @staticmethod
     def backward(ctx, da, ds=None):
-        x, wT, y, mean, invstd, scale, shift, gamma, w1, w2 = ctx.saved_tensors
-        N, H, W, Cp, K, Creal, R, P, Q = ctx.geom
-        spec = ctx.spec
-        M = N * P * Q
-        dev = y.device
-        adt = x.dtype
-        da = da.contiguous() if da is not None else torch.zeros(y.shape, dtype=adt, device=dev)
-        if da.dtype != adt:
-            da = da.to(adt)
-        add_nc = None
-        dw1 = dw2 = None
-        if ctx.se is not None and ds is not None:
-            pooled, z1, s = ctx.se
-            R1 = w1.shape[0]
-            dw1 = torch.empty(w1.shape, dtype=torch.float32, device=dev)
-            dw2 = torch.empty(w2.shape, dtype=torch.float32, device=dev)
-            add_nc = torch.empty((N, K), dtype=torch.float32, device=dev)
-            dz = torch.empty((N, R1), dtype=torch.float32, device=dev)
-            dsc = ds.float().contiguous()
-            w1c, w2c = w1.detach().float().contiguous(), w2.detach().float().contiguous()
-            call('um_se_mlp_bwd', N, K, R1, ptr(dsc), ptr(s), ptr(z1), ptr(pooled), ptr(w1c),
-                 ptr(w2c), ptr(dw1), ptr(dw2), ptr(add_nc), ptr(dz), 1.0 / (P * Q))
-        dgamma = dbeta = dbias = None
-        need_b = ctx.needs_input_grad[2]
-        slots_b = ctx.slots_b
-        if ctx.has_bn and slots_b is not None:
-            # backward sums into the slots; the apply kernel finishes them
-            if need_b:
-                dbias = torch.empty(K, dtype=torch.float32, device=dev)
-            if gamma is not None:
-                dgamma = torch.empty(K, dtype=torch.float32, device=dev)
-                dbeta = torch.empty(K, dtype=torch.float32, device=dev)
-            call('um_bn_elu_bwd_reduce_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
-                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
-                 ptr(slots_b))
-            local, bcount, bscale = None, float(M), 1.0
-            if ctx.sync is not None and ctx.sync.collective:
-                # dgamma/dbeta from this rank's sums (torch SyncBatchNorm),
-                # k1..k3 and the conv-bias gradient from the global ones
-                local = slots_b.clone()  # the reduce kernel stored the count after the slots
-                ctx.sync.all_reduce(slots_b)
-                bcount, bscale = -1.0, 1.0 / ctx.sync.world
-        elif ctx.has_bn:
-            k1 = torch.empty(K, dtype=torch.float32, device=dev)
-            k2 = torch.empty_like(k1)
-            k3 = torch.empty_like(k1)
-            # the conv bias feeds a training-mode BN: its gradient comes out of
-            # the coefficient kernel in closed form (no reduction of dy)
-            if need_b:
-                dbias = torch.empty(K, dtype=torch.float32, device=dev)
-            nb = query('um_bn_bwd_parts', M)
-            parts = torch.empty((nb, K, 2), dtype=torch.float32, device=dev)
-            world = ctx.sync.world if ctx.sync is not None else 1
-            if gamma is not None:
-                dgamma = torch.empty(K, dtype=torch.float32, device=dev)
-                dbeta = torch.empty(K, dtype=torch.float32, device=dev)
-            single = ctx.sync is None or not ctx.sync.collective
-            if single and _FUSED_BN_BWD:
-                # one launch: the reduce kernel's last blocks finish the coefficients
-                fin = torch.empty((query('um_bn_bwd_fin_ws', M, K) // 8,), dtype=torch.float64,
-                                  device=dev)
-                call('um_bn_elu_bwd_reduce_coeffs', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
-                     ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
-                     ptr(parts), ptr(fin), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dbias),
-                     ptr(k1), ptr(k2), ptr(k3))
-            elif single:
-                call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
-                     ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
-                     ptr(parts))
-                call('um_bn_bwd_stats_coeffs', ptr(parts), nb, K, ptr(_colred_ws(nb, K, 2, dev)),
-                     float(M), ptr(gamma), ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(dbias),
-                     ptr(k1), ptr(k2), ptr(k3))
-            else:
-                call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
-                     ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
-                     ptr(parts))
-                ws = _colred_ws(nb, K, 2, dev)
-                st = torch.empty((K + 1, 2), dtype=torch.float64, device=dev)
-                st[K].fill_(float(M))  # this rank's count, summed by the all-reduce
-                call('um_bn_stats_reduce', ptr(parts), nb, K, ptr(st), ptr(ws))
-                st_local = st.clone()
-                ctx.sync.all_reduce(st)
-                call('um_bn_bwd_coeffs', ptr(st), -1.0, K, ptr(gamma), ptr(invstd),
-                     ptr(st_local), ptr(dgamma), ptr(dbeta), ptr(dbias), 1.0 / world, 0,
-                     ptr(k1), ptr(k2), ptr(k3))
-        else:
-            # no batch statistics (no BN, or BN in eval mode): dy = dz * scale
-            k1 = scale
-            k2 = k3 = _const_vec(0.0, K, dev)
-            if gamma is not None and spec.bn is not None:
-                raise NotImplementedError('backward through an eval-mode BatchNorm')
-        dy = torch.empty(y.shape, dtype=adt, device=dev)
-        nbp = query('um_bn_bwd_parts', M)
-        reduce_b = need_b and dbias is None
-        bparts = torch.empty((nbp, K), dtype=torch.float32, device=dev) if reduce_b else None
-        if ctx.has_bn and slots_b is not None:
-            call('um_bn_elu_bwd_apply_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
-                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
-                 ptr(slots_b), bcount, ptr(local), ptr(gamma), ptr(dgamma), ptr(dbeta),
-                 ptr(dbias), bscale, ptr(dy), K)
-        else:
-            call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
-                 ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1),
-                 ptr(k2), ptr(k3), ptr(dy), K, ptr(bparts))
-        dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode,
-                         segs=spec.segs)
-        if reduce_b:
-            dbias = torch.empty(K, dtype=torch.float32, device=dev)
-            _reduce_rows(bparts, nbp, K, dbias)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = _conv_dgrad(dy, wT, (N, H, W, Cp), K, R, spec.stride, spec.pad, spec.pad_mode,
-                             creal=Creal)
-        return dx, dW, dbias, dgamma, dbeta, dw1, dw2, None
+        st = ctx.st
+        st.saved = ctx.saved_tensors
+        out = _cbe_bwd(st, da, ds, need_x=ctx.needs_input_grad[0],
+                       need_b=ctx.needs_input_grad[2])
+        st.saved = None
+        return (*out, None)
 
 
 def conv_bn_elu(x, conv, bn, pad, pad_mode, se=None, elu=True, segs=None):
@@ -603,7 +663,8 @@ class MergeFn(torch.autograd.Function):
         dw = None
         if need_w:
             dw = torch.empty_like(w, dtype=torch.float32)
-            call('um_merge_wgrad', ptr(parts), nparts, n, idx, ptr(w), ptr(dw), w.numel(), 0)
+            args = (ptr(parts), nparts, n, idx, ptr(w), ptr(dw), w.numel(), 0)
+            _param_grad((parts, w), dw, lambda: call('um_merge_wgrad', *args))
         return (dw, None, None, *dsrcs)
 
 
@@ -619,6 +680,156 @@ def merge(inputs: Sequence[torch.Tensor], w: Optional[torch.Tensor], widx: Seque
     if len(inputs) == 1 and w is None and coefs is None:
         return inputs[0]
     return MergeFn.apply(w, list(widx), list(coefs) if coefs is not None else None, *inputs)
+
+
+# -------------------------------------------------------------- graph block --
+_STAGE_FN = os.environ.get('UMAMD_STAGE_FN', '1') == '1'
+
+
+class GraphSpec:
+    """Static description of a GraphBlock (reference model/layers/encoder.py
+    :130-198) for GraphBlockFn: node order, predecessors (adjacency order,
+    F3 weight map), output nodes, one ConvSpec per node and the flat
+    parameter layout [conv.weight, conv.bias, bn.weight, bn.bias,
+    (mean_weight)] per node."""
+
+    def __init__(self, block):
+        self.nodes = [list(node.inputs) for node in block.nodes]
+        self.out_nodes = list(block.out_nodes)
+        self.specs, self.params, self.slices, self.widx = [], [], [], []
+        for nb, preds in zip(block.node_blocks, self.nodes):
+            conv, bn = nb.convolution.layers[0], nb.convolution.layers[1]
+            self.specs.append(ConvSpec(conv, bn, nb.convolution.padding[0], L.PAD_ZERO))
+            ps = [conv.weight, conv.bias, bn.weight if bn.affine else None,
+                  bn.bias if bn.affine else None]
+            if nb.mean_weight is not None:
+                ps.append(nb.mean_weight)
+            self.slices.append((len(self.params), len(ps)))
+            self.params += ps
+            self.widx.append([0] + list(range(len(preds) - 1)))
+
+
+def _merge_launch(srcs, w, widx, coefs, out):
+    n = len(srcs)
+    arr = (ctypes_p * n)(*[t.data_ptr() for t in srcs])
+    idx = (ctypes_i * n)(*widx)
+    cf = (ctypes_f * n)(*coefs) if coefs is not None else None
+    call('um_merge_fwd', _dt(out), n, arr, idx, ptr(w), cf, out.numel(), ptr(out))
+    return out
+
+
+class GraphBlockFn(torch.autograd.Function):
+    """A whole GraphBlock as one autograd node.  Forward: every node's
+    weighted predecessor merge (F3) and conv+BN+ELU in id order, the output
+    nodes averaged out of place (F4).  Backward in reverse id order, where
+    every node's gradient is complete once its (higher-id) successors are
+    done: each node's input gradient is written or ADDED straight into its
+    predecessors' gradient buffers -- the data-gradient GEMM accumulates
+    into a single predecessor, the merge backward's per-source accumulate
+    flags into several -- so no autograd gradient sums (one elementwise add
+    launch per extra consumer of a node output: 6 per K5 stage) are left."""
+
+    @staticmethod
+    def forward(ctx, gs: GraphSpec, x, *params):
+        a, states, merged = [], [], {}
+        for j, preds in enumerate(gs.nodes):
+            o, n = gs.slices[j]
+            w, b, g, be = params[o:o + 4]
+            mw = params[o + 4] if n > 4 else None
+            if not preds:
+                inp = x
+            elif len(preds) == 1:
+                inp = a[preds[0]]
+            else:
+                inp = _merge_launch([a[p] for p in preds], mw, gs.widx[j], None,
+                                    torch.empty_like(a[preds[0]]))
+            outs, st = _cbe_fwd(inp, w, b, g, be, None, None, gs.specs[j])
+            a.append(outs[0])
+            states.append(st)
+        if len(gs.out_nodes) == 1:
+            out = a[gs.out_nodes[0]]
+        else:
+            k = len(gs.out_nodes)
+            out = _merge_launch([a[o] for o in gs.out_nodes], None, [0] * k, [1.0 / k] * k,
+                                torch.empty_like(a[gs.out_nodes[0]]))
+        ctx.gs, ctx.a, ctx.states = gs, a, states
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        gs, a, states = ctx.gs, ctx.a, ctx.states
+        dout = dout.contiguous()
+        if dout.dtype != a[0].dtype:
+            dout = dout.to(a[0].dtype)
+        da = {}
+        outs = gs.out_nodes
+        if len(outs) == 1:
+            da[outs[0]] = dout
+        else:  # out = mean of the output nodes: each gets dout / k
+            k = len(outs)
+            bufs = [torch.empty_like(a[o]) for o in outs]
+            arr = (ctypes_p * k)(*[a[o].data_ptr() for o in outs])
+            darr = (ctypes_p * k)(*[t.data_ptr() for t in bufs])
+            call('um_merge_bwd', _dt(dout), k, arr, darr, (ctypes_i * k)(*([0] * k)),
+                 (ctypes_i * k)(*([0] * k)), None, (ctypes_f * k)(*([1.0 / k] * k)),
+                 dout.numel(), ptr(dout), None)
+            for o, t in zip(outs, bufs):
+                da[o] = t
+        grads = [None] * len(gs.params)
+        dx_stage = None
+        need_x = ctx.needs_input_grad[1]
+        for j in reversed(range(len(gs.nodes))):
+            preds = gs.nodes[j]
+            o, n = gs.slices[j]
+            g = da.pop(j)
+            st = states[j]
+            if not preds:
+                if need_x:
+                    dx, *pg = _cbe_bwd(st, g, None, True, True, dx=dx_stage,
+                                       dx_accumulate=dx_stage is not None)
+                    dx_stage = dx
+                else:
+                    _, *pg = _cbe_bwd(st, g, None, False, True)
+            elif len(preds) == 1:
+                p = preds[0]
+                acc = p in da
+                dx, *pg = _cbe_bwd(st, g, None, True, True, dx=da.get(p), dx_accumulate=acc)
+                da[p] = dx
+            else:
+                dm, *pg = _cbe_bwd(st, g, None, True, True)
+                k = len(preds)
+                acc = [int(p in da) for p in preds]
+                for p in preds:
+                    if p not in da:
+                        da[p] = torch.empty_like(a[p])
+                mw = gs.params[o + 4]
+                need_w = ctx.needs_input_grad[2 + o + 4]
+                nparts = query('um_merge_parts', dm.numel())
+                parts = torch.empty((nparts, k), dtype=torch.float32, device=dm.device) \
+                    if need_w else None
+                idx = (ctypes_i * k)(*gs.widx[j])
+                call('um_merge_bwd', _dt(dm), k, (ctypes_p * k)(*[a[p].data_ptr() for p in preds]),
+                     (ctypes_p * k)(*[da[p].data_ptr() for p in preds]), (ctypes_i * k)(*acc), idx,
+                     ptr(mw), None, dm.numel(), ptr(dm), ptr(parts))
+                if need_w:
+                    dmw = torch.empty(mw.shape, dtype=torch.float32, device=dm.device)
+                    grads[o + 4] = _param_grad(
+                        (parts, mw), dmw,
+                        lambda a=(ptr(parts), nparts, k, idx, ptr(mw), ptr(dmw), mw.numel()): call(
+                            'um_merge_wgrad', *a, 0))
+            dW, dbias, dgamma, dbeta = pg[0], pg[1], pg[2], pg[3]
+            grads[o], grads[o + 1], grads[o + 2], grads[o + 3] = dW, dbias, dgamma, dbeta
+            states[j] = None  # release this node's saved tensors
+        ctx.a = ctx.states = None
+        grads = [gr if p is not None else None for gr, p in zip(grads, gs.params)]
+        return (None, dx_stage, *grads)
+
+
+def graph_block(x, block):
+    """GraphBlock forward (NHWC) as one GraphBlockFn node (UMAMD_STAGE_FN=0:
+    per-node autograd functions, the round-2 path)."""
+    gs = GraphSpec(block)
+    return GraphBlockFn.apply(gs, x, *gs.params)
 
 
 # ---------------------------------------------------------------- attention --
@@ -661,7 +872,7 @@ class AttentionFn(torch.autograd.Function):
         dout = dout.contiguous()
         datt = _conv_dgrad(dout, wrT, (N, H, W, C), C, 1, 1, 0, L.PAD_ZERO)
         dwr = _conv_wgrad(att, dout, C, C, C, 1, 1, 0, L.PAD_ZERO)
-        dbr = _colsum(dout, C)
+        dbr = _colsum_grad(dout, C)
         dqkv = torch.empty((N, H, W, 3 * C), dtype=dt, device=dev)
         dks = torch.empty((N * S, C), dtype=torch.float32, device=dev)
         ws = torch.empty(query('um_attn_ws_tiles', N, S, C, heads), dtype=torch.float32,
@@ -672,7 +883,7 @@ class AttentionFn(torch.autograd.Function):
              ptr(ksum), ptr(ctxm), ptr(datt), C, ptr(dqkv), 3 * C, ptr(dks), ptr(ws), ptr(dctx),
              ptr(r))
         dwqkv = _conv_wgrad(x, dqkv, 3 * C, 3 * C, C, 1, 1, 0, L.PAD_ZERO)
-        dbqkv = _colsum(dqkv, 3 * C)
+        dbqkv = _colsum_grad(dqkv, 3 * C)
         dx = dout.clone() if dout.dtype == dt else dout.to(dt)
         _conv_dgrad(dqkv, wT, (N, H, W, C), 3 * C, 1, 1, 0, L.PAD_ZERO, dx=dx, accumulate=True)
         return (dx, dwqkv[:C], dbqkv[:C], dwqkv[C:2 * C], dbqkv[C:2 * C], dwqkv[2 * C:],
@@ -801,7 +1012,7 @@ class DispHeadFn(torch.autograd.Function):
         call('um_sigmoid_scale_bwd', _dt(dl), M, K, ptr(d), K, ptr(dd), dd.shape[-1], ctx.scale,
              ptr(dl), Kp)
         dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)
-        db = _colsum(dl, Kp)[:K]  # channels K..Kp of dl are zero
+        db = _colsum_grad(dl, Kp)[:K]  # channels K..Kp of dl are zero
         dx = _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT, creal=Creal,
                          kreal=K) \
             if ctx.needs_input_grad[0] else None
