@@ -109,6 +109,19 @@ int um_conv_wgrad_reduce(const float* slabs, int splits, int K, int Kreal, int R
 int um_conv_wgrad_reduce_seg(const float* slabs, int splits, int K, int Kreal, int R, int C,
                              int Creal, float* dw, int accumulate, int nseg, const int* src0,
                              const int* dst0, const int* len, hipStream_t stream);
+/* Several weight gradients' slab reductions (um_conv_wgrad_reduce_seg each)
+ * in ONE launch: the weight-gradient side stream reduces a whole batch of
+ * queued convs at once (reference: the dW of every nn.Conv2d in
+ * train/train.py:126's backward).  descs is a HOST array of n <= UM_WRED_MAX
+ * entries; it is passed by value to the kernel (graph-capture safe). */
+#define UM_WRED_MAX 24
+typedef struct {
+  const float* slabs;  /* [splits][K][R][R][C] f32 */
+  float* dw;           /* [Kreal][Creal][R][R] f32 */
+  int splits, K, Kreal, R, C, Creal, accumulate;
+  int nseg, src0[4], dst0[4], len[4];
+} um_wred_desc;
+int um_conv_wgrad_reduce_batch(const um_wred_desc* descs, int n, hipStream_t stream);
 int um_pack_weight_seg(int dtype, const float* w, int K, int Creal, int R, int C, void* wf,
                        void* wT, int ldT, int nseg, const int* src0, const int* dst0,
                        const int* len, hipStream_t stream);

@@ -396,6 +396,36 @@ def test_wgrad(case):
     assert err < 1e-4, err
 
 
+# the side stream's batched slab reduction (one um_conv_wgrad_reduce_batch per
+# WgradStream flush) against the per-conv reduction: same slabs, same
+# summation order -> bit-identical dW, incl. a segment-mapped (concat) input
+# and more convs than one launch takes (UM_WRED_MAX)
+def test_wgrad_reduce_batch_matches_per_conv():
+    from umamd import functional as U
+    from umamd import overlap
+    from umamd._lib import PAD_REFLECT, PAD_ZERO, WRED_MAX
+    g = torch.Generator().manual_seed(3)
+    cases = [(32, 32, 7, 1, PAD_ZERO, 12, 64, None), (64, 128, 3, 1, PAD_REFLECT, 6, 32, None),
+             (256, 512, 3, 1, PAD_ZERO, 4, 8, None), (32, 96, 1, 1, PAD_ZERO, 12, 40, None),
+             (24, 32, 3, 1, PAD_REFLECT, 8, 32, [(0, 0, 5), (5, 8, 11)])]
+    cases = (cases * ((WRED_MAX + 8) // len(cases) + 1))[:WRED_MAX + 6]
+    ins, refs = [], []
+    for C, K, R, st, pm, H, W, segs in cases:
+        N, pad = 2, (R - 1) // 2
+        x = (torch.rand(N, H, W, C, generator=g) - 0.5).to(torch.bfloat16).to(DEV)
+        dy = torch.randn(N, H, W, K, generator=g).to(torch.bfloat16).to(DEV)
+        creal = 16 if segs else C
+        ins.append((x, dy, K, creal, R, st, pad, pm, segs))
+        refs.append(U._conv_wgrad(x, dy, K, K, creal, R, st, pad, pm, segs=segs))
+    grads = [torch.empty_like(r) for r in refs]
+    with overlap.WgradStream(batch=len(cases)):
+        for (x, dy, K, creal, R, st, pad, pm, segs), dw in zip(ins, grads):
+            U._conv_wgrad(x, dy, K, K, creal, R, st, pad, pm, dw=dw, segs=segs)
+    torch.cuda.synchronize()
+    for r, got in zip(refs, grads):
+        assert torch.equal(r, got)
+
+
 # x2 bilinear (align_corners=True) upsample of a concat source: forward and
 # the adjoint (branch-free 6x6 window for low-res sides >= 4, general path
 # below), with and without an SE gate, against torch

@@ -83,6 +83,14 @@ __device__ __forceinline__ void store8(bf16_t* p, const float* v) {
   *reinterpret_cast<uint4*>(p) = u;
 }
 
+// 4-element vector stores (8 B for bf16, 16 B for f32)
+__device__ __forceinline__ void store4(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void store4(bf16_t* p, const float* v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+}
+
 // the values of v as they are stored in a T tensor (bf16 rounding)
 __device__ __forceinline__ void load8_rounded(const float* v, float* r, const float*) {
 #pragma unroll

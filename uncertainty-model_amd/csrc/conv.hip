@@ -456,12 +456,11 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 // four of them in flight per round, so a wave moves 1 KB per load instead of
 // 256 B and the reduction runs at streaming rate instead of load latency.
 // All offsets fit 32 bits (checked by the caller).
-__global__ void __launch_bounds__(256) wgrad_reduce4_kernel(const float* __restrict__ slabs,
-                                                            int splits, int K, int Kreal, int R,
-                                                            int C, int Creal,
-                                                            float* __restrict__ dw,
-                                                            int accumulate, Segs sg, int L) {
-  __shared__ float4 red[256];
+__device__ __forceinline__ void wgrad_reduce4_body(const float* __restrict__ slabs, int splits,
+                                                   int K, int Kreal, int R, int C, int Creal,
+                                                   float* __restrict__ dw, int accumulate,
+                                                   const Segs& sg, int L, int blk, int nblk,
+                                                   float4* red) {
   const int EB = 256 / L;
   const int le = threadIdx.x % EB, lane = threadIdx.x / EB;
   const int RR = R * R, RRC = RR * C;
@@ -469,7 +468,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce4_kernel(const float* __restr
   const int zs4 = K * RRC / 4;
   const int step = L * zs4;
   const float4* __restrict__ s4 = reinterpret_cast<const float4*>(slabs);
-  for (int i0 = blockIdx.x * EB; i0 < total4; i0 += gridDim.x * EB) {
+  for (int i0 = blk * EB; i0 < total4; i0 += nblk * EB) {
     const int i = i0 + le;
     float4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0, v2 = v0, v3 = v0;
     if (i < total4) {
@@ -507,6 +506,49 @@ __global__ void __launch_bounds__(256) wgrad_reduce4_kernel(const float* __restr
       }
     }
   }
+}
+
+__global__ void __launch_bounds__(256) wgrad_reduce4_kernel(const float* __restrict__ slabs,
+                                                            int splits, int K, int Kreal, int R,
+                                                            int C, int Creal,
+                                                            float* __restrict__ dw,
+                                                            int accumulate, Segs sg, int L) {
+  __shared__ float4 red[256];
+  wgrad_reduce4_body(slabs, splits, K, Kreal, R, C, Creal, dw, accumulate, sg, L, blockIdx.x,
+                     gridDim.x, red);
+}
+
+// Many weight gradients' slab reductions in ONE launch (the weight-gradient
+// side stream's batch, umamd/overlap.py): descriptor d owns workgroups
+// [first[d], first[d + 1]).  The descriptors travel as kernel arguments, so
+// a captured graph keeps them by value.
+struct WredDesc {
+  const float* slabs;
+  float* dw;
+  int splits, K, Kreal, R, C, Creal, accumulate, L;
+  Segs sg;
+};
+struct WredBatch {
+  int n;
+  int first[UM_WRED_MAX + 1];
+  WredDesc d[UM_WRED_MAX];
+};
+
+__global__ void __launch_bounds__(256) wgrad_reduce_batch_kernel(WredBatch b) {
+  __shared__ float4 red[256];
+  // the descriptor by unrolled uniform selects: a runtime index into a
+  // by-value kernel argument would copy the struct to scratch
+  WredDesc d = b.d[0];
+  int f0 = 0, f1 = b.first[1];
+#pragma unroll
+  for (int j = 1; j < UM_WRED_MAX; ++j)
+    if (j < b.n && (int)blockIdx.x >= b.first[j]) {
+      d = b.d[j];
+      f0 = b.first[j];
+      f1 = b.first[j + 1];
+    }
+  wgrad_reduce4_body(d.slabs, d.splits, d.K, d.Kreal, d.R, d.C, d.Creal, d.dw, d.accumulate, d.sg,
+                     d.L, blockIdx.x - f0, f1 - f0, red);
 }
 
 template <typename T>
@@ -903,6 +945,41 @@ int um_conv_wgrad_reduce(const float* slabs, int splits, int K, int Kreal, int R
                                   nullptr, nullptr, nullptr, st);
 }
 
+int um_conv_wgrad_reduce_batch(const um_wred_desc* descs, int n, hipStream_t st) {
+  UM_CHECK_ARG(descs != nullptr && n >= 0 && n <= UM_WRED_MAX, "um_conv_wgrad_reduce_batch: n");
+  if (n == 0) return UM_OK;
+  WredBatch b{};
+  b.n = n;
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const um_wred_desc& e = descs[i];
+    UM_CHECK_ARG(e.slabs != nullptr && e.dw != nullptr && e.splits >= 1 && e.Kreal <= e.K &&
+                     e.Creal <= e.C,
+                 "um_conv_wgrad_reduce_batch: descriptor");
+    const long RRC = (long)e.R * e.R * e.C;
+    UM_CHECK_ARG(RRC % 4 == 0 && (long)e.splits * e.K * RRC < (1l << 33),
+                 "um_conv_wgrad_reduce_batch: slab layout (R*R*C % 4, 32-bit offsets)");
+    WredDesc& d = b.d[i];
+    d.slabs = e.slabs;
+    d.dw = e.dw;
+    d.splits = e.splits; d.K = e.K; d.Kreal = e.Kreal; d.R = e.R; d.C = e.C; d.Creal = e.Creal;
+    d.accumulate = e.accumulate;
+    UM_CHECK_ARG(make_segs(d.sg, e.nseg, e.src0, e.dst0, e.len, e.Creal, e.C),
+                 "um_conv_wgrad_reduce_batch: segments");
+    const long total4 = (long)e.Kreal * RRC / 4;
+    int L = 1;  // as um_conv_wgrad_reduce_seg
+    while (L < 32 && L * 4 <= e.splits && (total4 * L) / 256 < 2048) L <<= 1;
+    d.L = L;
+    const int EB = 256 / L;
+    b.first[i] = blocks;
+    blocks += (int)std::min<long>((total4 + EB - 1) / EB, 8192);
+  }
+  b.first[n] = blocks;
+  hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3(blocks), dim3(256), 0, st, b);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
 int um_pack_weight_seg(int dtype, const float* w, int K, int Creal, int R, int C, void* wf,
                        void* wT, int ldT, int nseg, const int* src0, const int* dst0,
                        const int* len, hipStream_t st) {
@@ -989,22 +1066,39 @@ __device__ __forceinline__ void pack_tile(const um_pack_desc& d, int t, float* t
   __syncthreads();
   T* wf = reinterpret_cast<T*>(d.wf);
   T* wT = reinterpret_cast<T*>(d.wT);
+  // vector stores: wf in runs of 4 channels (C is a multiple of 8, CT of 4),
+  // wT in runs of 8 output channels (scalar where a run leaves [0, K) or ldT
+  // is not a multiple of 8).  LDS reads: consecutive lanes step by RR (wf) or
+  // ldt (wT), both odd, so they spread over the banks.
   if (wf)
-    for (int i = threadIdx.x; i < n; i += 256) {  // (kk, tap, cc): c fastest
-      const int kk = i / per_k, rem = i - kk * per_k;
-      const int tap = rem / CT, cc = rem - tap * CT;
-      const int k = k0 + kk, c = c0 + cc;
-      if (k < d.K && c < d.C)
-        wf[((long)k * RR + tap) * d.C + c] = from_f32<T>(tile[kk * ldt + cc * RR + tap]);
+    for (int i = threadIdx.x; i < n / 4; i += 256) {  // (kk, tap, c4): c fastest
+      const int kk = i / (per_k / 4), rem = i - kk * (per_k / 4);
+      const int tap = rem / (CT / 4), c4 = (rem - tap * (CT / 4)) * 4;
+      const int k = k0 + kk, c = c0 + c4;
+      if (k >= d.K || c >= d.C) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = tile[kk * ldt + (c4 + e) * RR + tap];
+      store4(wf + ((long)k * RR + tap) * d.C + c, v);
     }
-  if (wT)
-    for (int i = threadIdx.x; i < n; i += 256) {  // (cc, tap, kk): k fastest
-      const int cc = i / (RR * PK), rem = i - cc * (RR * PK);
-      const int tap = rem / PK, kk = rem - tap * PK;
-      const int k = k0 + kk, c = c0 + cc;
-      if (k < d.K && c < d.C)
-        wT[((long)c * RR + tap) * d.ldT + k] = from_f32<T>(tile[kk * ldt + cc * RR + tap]);
+  if (wT) {
+    const bool vec = (d.ldT & 7) == 0;
+    for (int i = threadIdx.x; i < n / 8; i += 256) {  // (cc, tap, k8): k fastest
+      const int cc = i / (RR * PK / 8), rem = i - cc * (RR * PK / 8);
+      const int tap = rem / (PK / 8), k8 = (rem - tap * (PK / 8)) * 8;
+      const int k = k0 + k8, c = c0 + cc;
+      if (c >= d.C || k >= d.K) continue;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tile[(k8 + e) * ldt + cc * RR + tap];
+      T* o = wT + ((long)c * RR + tap) * d.ldT + k;
+      if (vec && k + 8 <= d.K) {
+        store8(o, v);
+      } else {
+        for (int e = 0; e < 8 && k + e < d.K; ++e) o[e] = from_f32<T>(v[e]);
+      }
     }
+  }
 }
 
 template <typename T>

@@ -35,8 +35,13 @@ using umamd::IgArgs;
 
 constexpr int TH = 8, TW = 32, CK = 32;
 
-// element offset of 8-channel chunk c (0..3) of halo pixel p
-__device__ __forceinline__ int himg(int p, int c) { return p * CK + ((c ^ ((p >> 2) & 3)) << 3); }
+// element offset of 8-channel chunk c (0..3) of halo pixel p.  A fragment read
+// (ds_read_b128) takes 16 consecutive pixels from ANY start pixel p0 (tap
+// offsets), lane l -> pixel p0 + (l & 15), chunk l >> 4, serviced in the lane
+// groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32).  With chunk ^ 2*bit2(p)
+// each group covers the 64 banks exactly once for every p0 (the former
+// chunk ^ ((p >> 2) & 3) was 2-way in every group: SQ_LDS_BANK_CONFLICT 0.4)
+__device__ __forceinline__ int himg(int p, int c) { return p * CK + ((c ^ ((p >> 1) & 2)) << 3); }
 
 template <int R, int BN, bool FLIP, bool REFLECT>
 __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, int tiles_y) {

@@ -32,6 +32,16 @@ class CatSrc(ctypes.Structure):
                 ('coff', _I), ('dtype', _I), ('h', _I), ('w', _I)]
 
 
+WRED_MAX = 24  # UM_WRED_MAX
+
+
+class WredDesc(ctypes.Structure):
+    """um_wred_desc: one slab reduction of um_conv_wgrad_reduce_batch"""
+    _fields_ = [('slabs', _P), ('dw', _P), ('splits', _I), ('K', _I), ('Kreal', _I), ('R', _I),
+                ('C', _I), ('Creal', _I), ('accumulate', _I), ('nseg', _I),
+                ('src0', _I * 4), ('dst0', _I * 4), ('len', _I * 4)]
+
+
 # name -> (restype, argtypes); 's' = stream
 _SIG = {
     'um_last_error': (ctypes.c_char_p, []),
@@ -55,6 +65,7 @@ _SIG = {
     'um_pack_tiles': (_I, [_I, _I, _I]),
     'um_pack_weight_seg': (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P, 's']),
     'um_conv_wgrad_reduce_seg': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, 's']),
+    'um_conv_wgrad_reduce_batch': (_I, [_P, _I, 's']),
     'um_colsum_parts': (_I, [_I]),
     'um_colsum': (_I, [_I, _I, _I, _I, _P, _P, 's']),
     'um_reduce_rows': (_I, [_P, _I, _I, _I, _P, _I, _P, 's']),

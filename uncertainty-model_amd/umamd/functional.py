@@ -127,10 +127,46 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
     dw_ptr = ptr(dw)
     N, _, _, _ = x.shape
     _, P, Q, _ = dy.shape
-    ov.defer((x, dy), lambda: _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad,
-                                             pad_mode, dw_ptr, segs), out_ptr=dw_ptr,
-             flop=_conv_flops(N, P, Q, Kreal, R, Creal))
+    if _WRED_BATCH:  # kernel now, slab reduce batched with the flush's others
+        launch = lambda: _conv_wgrad_slabs(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode,  # noqa: E731
+                                           dw_ptr, segs)
+    else:
+        launch = lambda: _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad,  # noqa: E731
+                                        pad_mode, dw_ptr, segs)
+    ov.defer((x, dy), launch, out_ptr=dw_ptr, flop=_conv_flops(N, P, Q, Kreal, R, Creal))
     return dw
+
+
+# the side stream's slab reductions as ONE um_conv_wgrad_reduce_batch launch
+# per flush instead of one um_conv_wgrad_reduce_seg per conv
+_WRED_BATCH = os.environ.get('UMAMD_WRED_BATCH', '1') == '1'
+
+
+def _conv_wgrad_slabs(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw_ptr, segs):
+    """The weight-gradient kernel into f32 slabs -> (slabs, um_wred_desc) for
+    a batched reduction (overlap.WgradStream._flush)."""
+    N, H, W, C = x.shape
+    _, P, Q, ldy = dy.shape
+    splits = query('um_conv_wgrad_splits', _dt(x), N, H, W, C, C, K, R, stride, pad, pad_mode,
+                   P, Q, ldy)
+    slabs = torch.empty((splits, K, R * R * C), dtype=torch.float32, device=x.device)
+    call('um_conv2d_wgrad', _dt(x), N, H, W, C, C, ptr(x), K, R, stride, pad, pad_mode, P, Q,
+         ptr(dy), ldy, ptr(slabs), splits, work=_conv_flops(N, P, Q, Kreal, R, Creal))
+    d = L.WredDesc()
+    d.slabs, d.dw = slabs.data_ptr(), dw_ptr
+    d.splits, d.K, d.Kreal, d.R, d.C, d.Creal, d.accumulate = splits, K, Kreal, R, C, Creal, 0
+    d.nseg = len(segs) if segs else 0
+    for i, (a0, b0, l0) in enumerate(segs or ()):
+        d.src0[i], d.dst0[i], d.len[i] = a0, b0, l0
+    return slabs, d
+
+
+def wgrad_reduce_batch(descs):
+    """um_conv_wgrad_reduce_batch over a list of um_wred_desc, in chunks"""
+    for i in range(0, len(descs), L.WRED_MAX):
+        chunk = descs[i:i + L.WRED_MAX]
+        arr = (L.WredDesc * len(chunk))(*chunk)
+        call('um_conv_wgrad_reduce_batch', _ct.cast(arr, ctypes_p), len(chunk))
 
 
 def _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw_ptr, segs):

@@ -89,9 +89,18 @@ class WgradStream:
         if not self._pending:
             return
         self.stream.wait_stream(torch.cuda.current_stream())
+        from . import _lib as L
+        from . import functional as F
         with torch.cuda.stream(self.stream):
+            keep, descs = [], []
             for _, launch in self._pending:
-                launch()
+                r = launch()  # a weight gradient returns (slabs, um_wred_desc)
+                if isinstance(r, tuple) and len(r) == 2 and isinstance(r[1], L.WredDesc):
+                    keep.append(r[0])
+                    descs.append(r[1])
+            if descs:
+                F.wgrad_reduce_batch(descs)
+            del keep  # freed on the side stream, after the reduction
         for tensors, _ in self._pending:
             for t in tensors:
                 t.record_stream(self.stream)
