@@ -83,6 +83,17 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                   int ldr, float* stats_partials, void* ws, long ws_bytes,
                   hipStream_t stream);
 
+/* 1x1 conv forward (f32 output, zero pad, stride 1) plus the bilinear x2
+ * (align_corners=True) upsample of a low-resolution f32 map added before the
+ * epilogue's BN statistics: y = W x + bias + up2(z), z = [N][up2_h][up2_w]
+ * [up2_ld] (channels [0, K) used).  The decoder's cat(feature_map,
+ * interpolate(skip)) -> 1x1 conv (reference model/layers/decoder.py:230-238)
+ * with the skip half convolved at the skip's resolution (the 1x1 conv and
+ * the upsample commute): the full-resolution concat is never built. */
+int um_conv2d_fwd_up2(int dtype, int N, int H, int W, int C, int ldx, const void* x,
+                      const void* wf, const float* bias, int K, int P, int Q, void* y, int ldy,
+                      int epilogue, float* stats, const float* up2, int up2_h, int up2_w,
+                      int up2_ld, hipStream_t stream);
 /* data gradient: dx[N,H,W,C] (= or +=) conv^T(dy[N,P,Q,K], wT) incl. the
  * reflect-pad fold and the stride-2 scatter */
 int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx,
@@ -221,6 +232,19 @@ int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const 
                         long long* num_batches_tracked, float* mean, float* invstd, float* scale,
                         float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
                         hipStream_t stream);
+/* um_bn_elu_fwd_slots plus the NodeBlock merge of the next graph node
+ * (reference model/layers/encoder.py:115-124): merged = sum_i
+ * sigmoid(w[widx[i]]) * src_i over nsrc (2..8) sources [M][lda] of the
+ * activation dtype, where source `self` is the a this call writes (srcs[self]
+ * is ignored).  Replaces um_bn_elu_fwd_slots + um_merge_fwd when this layer
+ * is the last predecessor computed before that node. */
+int um_bn_elu_fwd_slots_merge(int dtype, long M, int C, const void* y, int ldy,
+                              const double* slots, double count, const float* gamma,
+                              const float* beta, float eps, float momentum, float* running_mean,
+                              float* running_var, long long* num_batches_tracked, float* mean,
+                              float* invstd, float* scale, float* shift, void* a, int lda,
+                              int apply_elu, int nsrc, const void* const* srcs, const int* widx,
+                              const float* w, int self, void* merged, hipStream_t stream);
 /* backward sums (sum dz, sum dz*xhat) added into zeroed f64 slots
  * [UM_STAT_SLOTS][C][2] instead of partial rows */
 int um_bn_elu_bwd_reduce_slots(int dtype, long M, int C, long HW, const void* da, int ldda,
@@ -277,6 +301,19 @@ int um_bn_elu_bwd_apply(int dtype, long M, int C, long HW, const void* da, int l
  * NodeBlock merge, reference model/layers/encoder.py:115-124 (F3 index map
  * passed in widx: input i weighted by sigmoid(w[widx[i]])).
  */
+/* Several um_merge_wgrad calls in ONE launch (one workgroup each): the
+ * weight-gradient side stream batches the merge-weight gradients of a flush.
+ * descs: HOST array of n <= UM_MWG_MAX entries, passed by value. */
+#define UM_MWG_MAX 24
+#define UM_MWG_SRC 8
+typedef struct {
+  const float* parts;  /* [nparts][nsrc] (um_merge_bwd) */
+  const float* w;
+  float* dw;
+  int nparts, nsrc, nw, accumulate;
+  int widx[UM_MWG_SRC];
+} um_mwg_desc;
+int um_merge_wgrad_batch(const um_mwg_desc* descs, int n, hipStream_t stream);
 /* coefficient of input i: sigmoid(w[widx[i]]) if w, else coefs[i] (host array), else 1 */
 int um_merge_fwd(int dtype, int nsrc, const void* const* srcs, const int* widx,
                  const float* w, const float* coefs, long count, void* dst, hipStream_t stream);

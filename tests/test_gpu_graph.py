@@ -277,3 +277,33 @@ def test_stage_fn_matches_per_node_autograd(cfgname, dtype):
             (k, d, float(g0[k].norm()))
     for k in b0:
         assert torch.allclose(b1[k], b0[k], rtol=1e-6, atol=1e-7), k
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_fused_merge_matches_separate_merge(dtype):
+    """A node's merge computed inside its last predecessor's BN apply pass
+    (um_bn_elu_fwd_slots_merge) against the separate um_merge_fwd launch:
+    same coefficients, same source order, the stored (rounded) activation of
+    the fusing layer -> bit-identical disparities and gradients."""
+    from umamd import functional as U
+    cfg = _cfg('config.yml')
+    left, _ = _uniform_pair(2, 64, 128, seed=5)
+    left = left.to(DEV)
+    res = []
+    old = U._FUSED_MERGE
+    try:
+        for flag in (True, False):
+            U._FUSED_MERGE = flag
+            m = _model(cfg, dtype).train()
+            d = m(left, 0.3)
+            (sum((t.float() ** 2).mean() for t in d)).backward()
+            torch.cuda.synchronize()
+            res.append(([t.detach().clone() for t in d],
+                        {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+    finally:
+        U._FUSED_MERGE = old
+    (d1, g1), (d0, g0) = res
+    for a, b in zip(d1, d0):
+        assert torch.equal(a, b)
+    for k in g0:
+        assert torch.equal(g1[k], g0[k]), k

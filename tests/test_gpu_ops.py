@@ -235,8 +235,13 @@ def _decoder_stage_case(cfg, N, h, w, with_gate, with_disp):
 @pytest.mark.parametrize('with_gate,with_disp,fC', [(False, False, 256), (True, True, 64),
                                                       (True, True, 3)])
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
-def test_decoder_stage(with_gate, with_disp, fC, dtype):
+@pytest.mark.parametrize('skip_conv', [True, False])
+def test_decoder_stage(with_gate, with_disp, fC, dtype, skip_conv, monkeypatch):
+    """skip_conv: the squeeze-excite 1x1 conv with the skip half at the
+    skip's resolution (SkipConvFn) or over the materialised full-size concat"""
     from oracle.model import decoder_stage
+    from umamd import functional as U
+    monkeypatch.setattr(U, '_SKIP_CONV', skip_conv)
     cfg = dict(in_channels=64, feature_in_channels=fC, skip_in_channels=64,
                upsample_channels=16, out_channels=32, skip_out_channels=32,
                concat_disp=with_disp, calculate_disp=True, disp_channels=4)

@@ -100,6 +100,21 @@ __device__ __forceinline__ void fwd_fin_coeffs(const FwdFin& f, int C, int c0, i
   __syncthreads();
 }
 
+// Optional fused NodeBlock merge of the NEXT graph node (reference
+// model/layers/encoder.py:115-124, F3 weight map): when this layer is the
+// last-computed predecessor of node s, the apply pass also writes
+// out = sum_i sigmoid(w[widx[i]]) * src_i with src_self = the a it just
+// stored (bf16-rounded as stored), reading the other predecessors' outputs
+// ([M][ld] like a) -- the separate merge launch and its re-read of a go away.
+constexpr int FMERGE_MAX = 8;
+struct MergeOut {
+  int n, self;  // n == 0: no merge
+  const void* src[FMERGE_MAX];
+  int widx[FMERGE_MAX];
+  const float* w;
+  void* out;
+};
+
 // Channel slices (grid.y): block (x, y) owns rows [x*rows, (x+1)*rows) and
 // channels [y*cs, (y+1)*cs).  The small deep layers (M of 1k..16k rows, C of
 // 128..512) are sliced so a block finishes only its channels' statistics
@@ -109,7 +124,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
     const float* __restrict__ y, int ldy, long M, int C, const float* __restrict__ scale,
     const float* __restrict__ shift, T* __restrict__ a, int lda, int apply_elu,
-    int rows_per_block, float* __restrict__ pool, FwdFin fin, int cs) {
+    int rows_per_block, float* __restrict__ pool, FwdFin fin, int cs, MergeOut mo) {
   extern __shared__ float red[];  // [256][8] when pooling, then [2][cs] coefficients (fin)
   const int cb = blockIdx.y * cs;  // this block's channel slice
   const int cg = cs / 8;
@@ -124,6 +139,9 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
     shift = s_sc + cs;
     coff = 0;
   }
+  float mc[FMERGE_MAX];  // merge coefficients (uniform; unrolled static indices)
+#pragma unroll
+  for (int i = 0; i < FMERGE_MAX; ++i) mc[i] = i < mo.n ? sigmoidf_(mo.w[mo.widx[i]]) : 0.f;
   for (int g0 = 0; g0 < cg; g0 += rm.G) {
     const int g = g0 + rm.g;
     float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -139,11 +157,33 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
           v[e] = apply_elu ? eluf_(z) : z;
         }
         store8(a + m * lda + c, v);
-        if (pool) {
+        if (pool || mo.n) {
           float r[8];
           load8_rounded(v, r, a);
+          if (pool)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) ps[e] += r[e];
+            for (int e = 0; e < 8; ++e) ps[e] += r[e];
+          if (mo.n) {  // the merge in source order, as merge_fwd_kernel
+            float acc[8], sv[8];
+#pragma unroll
+            for (int i = 0; i < FMERGE_MAX; ++i) {
+              if (i >= mo.n) break;
+              if (i == mo.self) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sv[e] = r[e];
+              } else {
+                load8(reinterpret_cast<const T*>(mo.src[i]) + m * lda + c, sv);
+              }
+              if (i == 0) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] = sv[e] * mc[0];
+              } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] += mc[i] * sv[e];
+              }
+            }
+            store8(reinterpret_cast<T*>(mo.out) + m * lda + c, acc);
+          }
         }
       };
 #pragma unroll 4
@@ -573,7 +613,8 @@ int um_bn_fwd_pool_parts_c(long M, long HW, int C) {
 
 static int bn_fwd_launch(int dtype, long M, int C, const void* y, int ldy, const float* scale,
                          const float* shift, void* a, int lda, int apply_elu, long HW,
-                         float* pool_parts, const FwdFin& fin, hipStream_t st) {
+                         float* pool_parts, const FwdFin& fin, hipStream_t st,
+                         const MergeOut& mo = MergeOut{}) {
   UM_CHECK_ARG(C % 8 == 0 && ldy % 8 == 0 && lda % 8 == 0, "um_bn_elu_fwd: C/ld not multiple of 8");
   UM_CHECK_ARG(pool_parts == nullptr || (HW > 0 && M % HW == 0), "um_bn_elu_fwd: HW");
   const Slices sl = bn_slices(M, C);
@@ -584,11 +625,11 @@ static int bn_fwd_launch(int dtype, long M, int C, const void* y, int ldy, const
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, g, dim3(256), shm, st, (const float*)y,
                        ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu, rows, pool_parts, fin,
-                       sl.cs);
+                       sl.cs, mo);
   else
     hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, g, dim3(256), shm, st, (const float*)y,
                        ldy, M, C, scale, shift, (float*)a, lda, apply_elu, rows, pool_parts, fin,
-                       sl.cs);
+                       sl.cs, mo);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -615,6 +656,37 @@ int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const 
   fin.mean = mean; fin.invstd = invstd; fin.scale = scale; fin.shift = shift;
   return bn_fwd_launch(dtype, M, C, y, ldy, nullptr, nullptr, a, lda, apply_elu, HW, pool_parts,
                        fin, st);
+}
+
+int um_bn_elu_fwd_slots_merge(int dtype, long M, int C, const void* y, int ldy,
+                              const double* slots, double count, const float* gamma,
+                              const float* beta, float eps, float momentum, float* running_mean,
+                              float* running_var, long long* num_batches_tracked, float* mean,
+                              float* invstd, float* scale, float* shift, void* a, int lda,
+                              int apply_elu, int nsrc, const void* const* srcs, const int* widx,
+                              const float* w, int self, void* merged, hipStream_t st) {
+  UM_CHECK_ARG(slots != nullptr && mean && invstd && scale && shift,
+               "um_bn_elu_fwd_slots_merge: slots / coefficient outputs");
+  UM_CHECK_ARG(nsrc >= 2 && nsrc <= FMERGE_MAX && self >= 0 && self < nsrc && srcs && widx &&
+                   w && merged,
+               "um_bn_elu_fwd_slots_merge: merge sources");
+  FwdFin fin{};
+  fin.slots = slots; fin.count = count; fin.gamma = gamma; fin.beta = beta;
+  fin.eps = eps; fin.momentum = momentum;
+  fin.running_mean = running_mean; fin.running_var = running_var; fin.nbt = num_batches_tracked;
+  fin.mean = mean; fin.invstd = invstd; fin.scale = scale; fin.shift = shift;
+  MergeOut mo{};
+  mo.n = nsrc;
+  mo.self = self;
+  for (int i = 0; i < nsrc; ++i) {
+    UM_CHECK_ARG(i == self || srcs[i] != nullptr, "um_bn_elu_fwd_slots_merge: null source");
+    mo.src[i] = srcs[i];
+    mo.widx[i] = widx[i];
+  }
+  mo.w = w;
+  mo.out = merged;
+  return bn_fwd_launch(dtype, M, C, y, ldy, nullptr, nullptr, a, lda, apply_elu, 0, nullptr, fin,
+                       st, mo);
 }
 
 int um_bn_bwd_parts(long M) { return ceil_div(M, bn_bwd_rows(M)); }

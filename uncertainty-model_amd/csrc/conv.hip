@@ -39,9 +39,13 @@ struct Segs {
   int src0[MAX_SEG], dst0[MAX_SEG], len[MAX_SEG];
 };
 __device__ __forceinline__ int seg_src(const Segs& g, int c) {  // packed -> reference, or -1
-  for (int i = 0; i < g.n; ++i)
-    if (c >= g.dst0[i] && c < g.dst0[i] + g.len[i]) return g.src0[i] + c - g.dst0[i];
-  return -1;
+  // unrolled over static indices (segments do not overlap): a runtime index
+  // would put a by-value Segs in scratch
+  int r = -1;
+#pragma unroll
+  for (int i = 0; i < MAX_SEG; ++i)
+    if (i < g.n && c >= g.dst0[i] && c < g.dst0[i] + g.len[i]) r = g.src0[i] + c - g.dst0[i];
+  return r;
 }
 constexpr int LDK = BK + 8;  // padded LDS row (elements)
 
@@ -536,19 +540,35 @@ struct WredBatch {
 
 __global__ void __launch_bounds__(256) wgrad_reduce_batch_kernel(WredBatch b) {
   __shared__ float4 red[256];
-  // the descriptor by unrolled uniform selects: a runtime index into a
-  // by-value kernel argument would copy the struct to scratch
-  WredDesc d = b.d[0];
-  int f0 = 0, f1 = b.first[1];
+  // the descriptor field by field, by unrolled uniform selects: a runtime
+  // index into the by-value kernel argument (or a struct copy of one entry)
+  // would go through scratch
+  int i = 0;
 #pragma unroll
   for (int j = 1; j < UM_WRED_MAX; ++j)
-    if (j < b.n && (int)blockIdx.x >= b.first[j]) {
-      d = b.d[j];
-      f0 = b.first[j];
-      f1 = b.first[j + 1];
-    }
-  wgrad_reduce4_body(d.slabs, d.splits, d.K, d.Kreal, d.R, d.C, d.Creal, d.dw, d.accumulate, d.sg,
-                     d.L, blockIdx.x - f0, f1 - f0, red);
+    if (j < b.n && (int)blockIdx.x >= b.first[j]) i = j;
+#define WSEL(expr)                                          \
+  ({                                                        \
+    auto v_ = b.d[0].expr;                                  \
+    _Pragma("unroll") for (int j = 1; j < UM_WRED_MAX; ++j) \
+      if (j == i) v_ = b.d[j].expr;                         \
+    v_;                                                     \
+  })
+  Segs sg;
+  sg.n = WSEL(sg.n);
+#pragma unroll
+  for (int q = 0; q < MAX_SEG; ++q) {
+    sg.src0[q] = WSEL(sg.src0[q]);
+    sg.dst0[q] = WSEL(sg.dst0[q]);
+    sg.len[q] = WSEL(sg.len[q]);
+  }
+  int f0 = 0, f1 = 0;
+#pragma unroll
+  for (int j = 0; j < UM_WRED_MAX; ++j)
+    if (j == i) { f0 = b.first[j]; f1 = b.first[j + 1]; }
+  wgrad_reduce4_body(WSEL(slabs), WSEL(splits), WSEL(K), WSEL(Kreal), WSEL(R), WSEL(C), WSEL(Creal),
+                     WSEL(dw), WSEL(accumulate), sg, WSEL(L), blockIdx.x - f0, f1 - f0, red);
+#undef WSEL
 }
 
 template <typename T>
@@ -689,11 +709,43 @@ long um_conv_dgrad_ws(int dtype, int N, int H, int W, int C, int R, int K, int s
   return b;
 }
 
+static int conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
+                      const void* wf, const float* bias, int K, int R, int stride, int pad,
+                      int pad_mode, int P, int Q, int ydtype, void* y, int ldy, int epilogue,
+                      float epi_scale, const void* residual, int ldr, float* stats, void* ws,
+                      long ws_bytes, const float* up2, int up2_h, int up2_w, int up2_ld,
+                      hipStream_t st);
+
 int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x, const void* wf,
                   const float* bias, int K, int R, int stride, int pad, int pad_mode, int P,
                   int Q, int ydtype, void* y, int ldy, int epilogue, float epi_scale,
                   const void* residual, int ldr, float* stats, void* ws, long ws_bytes,
                   hipStream_t st) {
+  return conv2d_fwd(dtype, N, H, W, C, ldx, x, wf, bias, K, R, stride, pad, pad_mode, P, Q, ydtype,
+                    y, ldy, epilogue, epi_scale, residual, ldr, stats, ws, ws_bytes, nullptr, 0, 0,
+                    0, st);
+}
+
+int um_conv2d_fwd_up2(int dtype, int N, int H, int W, int C, int ldx, const void* x,
+                      const void* wf, const float* bias, int K, int P, int Q, void* y, int ldy,
+                      int epilogue, float* stats, const float* up2, int up2_h, int up2_w,
+                      int up2_ld, hipStream_t st) {
+  UM_CHECK_ARG(up2 != nullptr && up2_h >= 1 && up2_w >= 1 && up2_ld >= K,
+               "um_conv2d_fwd_up2: low-resolution map");
+  UM_CHECK_ARG(epilogue == UM_EPI_NONE || epilogue == UM_EPI_STATS ||
+                   epilogue == UM_EPI_STAT_SLOTS,
+               "um_conv2d_fwd_up2: epilogue");
+  return conv2d_fwd(dtype, N, H, W, C, ldx, x, wf, bias, K, 1, 1, 0, UM_PAD_ZERO, P, Q, UM_F32, y,
+                    ldy, epilogue, 1.f, nullptr, 0, stats, nullptr, 0, up2, up2_h, up2_w, up2_ld,
+                    st);
+}
+
+static int conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
+                      const void* wf, const float* bias, int K, int R, int stride, int pad,
+                      int pad_mode, int P, int Q, int ydtype, void* y, int ldy, int epilogue,
+                      float epi_scale, const void* residual, int ldr, float* stats, void* ws,
+                      long ws_bytes, const float* up2, int up2_h, int up2_w, int up2_ld,
+                      hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0 && ldx % 8 == 0, "um_conv2d_fwd: C (%d) and ldx (%d) must be multiples of 8", C, ldx);
   UM_CHECK_ARG(stride == 1 || stride == 2, "um_conv2d_fwd: stride %d", stride);
   UM_CHECK_ARG(P == (H + 2 * pad - R) / stride + 1 && Q == (W + 2 * pad - R) / stride + 1,
@@ -717,6 +769,7 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
   a.stat_slots = epilogue == UM_EPI_STAT_SLOTS;
   a.accumulate = 0; a.epi_scale = epi_scale;
   a.residual = residual; a.ldr = ldr; a.stats = stats;
+  a.up2 = up2; a.up2_h = up2_h; a.up2_w = up2_w; a.up2_ld = up2_ld;
   return umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
 }
 
@@ -911,7 +964,7 @@ static int make_segs(Segs& g, int nseg, const int* src0, const int* dst0, const 
 int um_conv_wgrad_reduce_seg(const float* slabs, int splits, int K, int Kreal, int R, int C,
                              int Creal, float* dw, int accumulate, int nseg, const int* src0,
                              const int* dst0, const int* len, hipStream_t st) {
-  UM_CHECK_ARG(Kreal <= K && Creal <= C, "um_conv_wgrad_reduce: sizes");
+  UM_CHECK_ARG(Kreal <= K && (nseg > 0 || Creal <= C), "um_conv_wgrad_reduce: sizes");
   Segs g{};
   UM_CHECK_ARG(make_segs(g, nseg, src0, dst0, len, Creal, C), "um_conv_wgrad_reduce: segments");
   const long total = (long)Kreal * R * R * C;
@@ -954,7 +1007,7 @@ int um_conv_wgrad_reduce_batch(const um_wred_desc* descs, int n, hipStream_t st)
   for (int i = 0; i < n; ++i) {
     const um_wred_desc& e = descs[i];
     UM_CHECK_ARG(e.slabs != nullptr && e.dw != nullptr && e.splits >= 1 && e.Kreal <= e.K &&
-                     e.Creal <= e.C,
+                     (e.nseg > 0 || e.Creal <= e.C),
                  "um_conv_wgrad_reduce_batch: descriptor");
     const long RRC = (long)e.R * e.R * e.C;
     UM_CHECK_ARG(RRC % 4 == 0 && (long)e.splits * e.K * RRC < (1l << 33),
@@ -983,7 +1036,9 @@ int um_conv_wgrad_reduce_batch(const um_wred_desc* descs, int n, hipStream_t st)
 int um_pack_weight_seg(int dtype, const float* w, int K, int Creal, int R, int C, void* wf,
                        void* wT, int ldT, int nseg, const int* src0, const int* dst0,
                        const int* len, hipStream_t st) {
-  UM_CHECK_ARG(C >= Creal, "um_pack_weight: C < Creal");
+  // segments may place a part of the reference channels only (the decoder's
+  // skip / feature-map halves of one 1x1 weight); without them all Creal
+  UM_CHECK_ARG(nseg > 0 || C >= Creal, "um_pack_weight: C < Creal");
   Segs g{};
   UM_CHECK_ARG(make_segs(g, nseg, src0, dst0, len, Creal, C), "um_pack_weight: segments");
   const long total = (long)K * R * R * C;
@@ -1057,8 +1112,10 @@ __device__ __forceinline__ void pack_tile(const um_pack_desc& d, int t, float* t
       int cs = -1;
       if (d.nseg <= 0) cs = c < d.Creal ? c : -1;
       else
-        for (int g = 0; g < d.nseg; ++g)
-          if (c >= d.dst0[g] && c < d.dst0[g] + d.len[g]) cs = d.src0[g] + c - d.dst0[g];
+#pragma unroll
+        for (int g = 0; g < UM_PACK_MAXSEG; ++g)  // static indices: no scratch copy of d
+          if (g < d.nseg && c >= d.dst0[g] && c < d.dst0[g] + d.len[g])
+            cs = d.src0[g] + c - d.dst0[g];
       if (cs >= 0) v = d.w[((long)k * d.Creal + cs) * RR + tap];
     }
     tile[kk * ldt + cc * RR + tap] = v;

@@ -44,6 +44,11 @@ struct IgArgs {
   int stat_slots;   // UM_EPI_STAT_SLOTS: stats is double[UM_STAT_SLOTS][NC][2]
   int colmajor;     // tile order, set by igemm_run (knob xcd_col)
   int tappack;      // 4 taps x 8 channels per k-step (ach == 8), set by igemm_run
+  // optional: v += bilinear x2 (align_corners=True) of a low-resolution f32
+  // map [on][up2_h][up2_w][up2_ld] at output pixel (n, oy, ox), channel col,
+  // before the BN statistics (plain row mode, no split-K)
+  const float* up2;
+  int up2_h, up2_w, up2_ld;
 };
 
 // rows per BN partial-statistics row of a stats epilogue (M, NC of the GEMM)

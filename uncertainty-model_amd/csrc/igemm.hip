@@ -228,6 +228,34 @@ __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ sr
   to_raw(v, out);
 }
 
+// bilinear x2 (align_corners=True, torch upsample_bilinear2d) of the f32 map
+// a.up2 at output row m (plain rows), channel n: the decoder's skip half of a
+// 1x1 conv, computed at the skip's resolution (conv1x1 and the upsample
+// commute) and added here (umamd.functional.skip_conv_bn_elu)
+__device__ __forceinline__ void up2_tap(int i, int in, int out, int& i0, int& i1, float& l1) {
+  const float sc = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  const float src = sc * (float)i;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = src - (float)i0;
+}
+__device__ __forceinline__ float up2_at(const IgArgs& a, int m, int n) {
+  const int hw = a.oh * a.ow;
+  const int b = m / hw, rem = m - b * hw;
+  const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
+  int y0, y1, x0, x1;
+  float ly, lx;
+  up2_tap(oy, a.up2_h, a.oh, y0, y1, ly);
+  up2_tap(ox, a.up2_w, a.ow, x0, x1, lx);
+  const float* p = a.up2 + (long)b * a.up2_h * a.up2_w * a.up2_ld + n;
+  const float v00 = p[((long)y0 * a.up2_w + x0) * a.up2_ld];
+  const float v01 = p[((long)y0 * a.up2_w + x1) * a.up2_ld];
+  const float v10 = p[((long)y1 * a.up2_w + x0) * a.up2_ld];
+  const float v11 = p[((long)y1 * a.up2_w + x1) * a.up2_ld];
+  return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+}
+
 // Epilogue shared by the register-staged and the LDS-DMA main loops: split-K
 // partial tile, or bias / residual / sigmoid-scale / stores and the BN
 // partial statistics (sStat: WM x BN x 2 floats of LDS).
@@ -279,6 +307,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
         const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
         if (!nok || m >= a.M) continue;
         float v = acc[i][j][q] + bv;
+        if (MODE == 0 && a.up2 != nullptr) v += up2_at(a, m, n);
         const long off = out_row<MODE>(a, m) + n;
         if (a.epilogue == UM_EPI_RESIDUAL)
           v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
@@ -1114,6 +1143,10 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   if (a_in.M == 0) return UM_OK;
   IgArgs a = a_in;
   a.stats_rows = igemm_stats_rows(a.M, a.NC);
+  if (a.up2 != nullptr) {  // the up2 add lives in the one-pass epilogue only
+    ws = nullptr;
+    ws_bytes = 0;
+  }
   {
     // column-major tile order when B (NC x taps x ach) is larger than the
     // gathered image A (M x ach): knob xcd_col 0 = never, 1 = auto, 2 = always

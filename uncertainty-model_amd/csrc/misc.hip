@@ -113,6 +113,66 @@ __global__ void merge_wgrad_kernel(const float* __restrict__ parts, int nparts, 
   }
 }
 
+// Several merge-weight gradients in ONE launch (one workgroup each): the
+// weight-gradient side stream's flush batches them like the conv slab
+// reductions.  Descriptors by value; fields selected with unrolled uniform
+// selects (no scratch copy of the argument).
+struct MwDesc {
+  const float* parts;
+  const float* w;
+  float* dw;
+  int nparts, nsrc, nw, accumulate;
+  int widx[UM_MWG_SRC];
+};
+struct MwBatch {
+  int n;
+  MwDesc d[UM_MWG_MAX];
+};
+
+__global__ void __launch_bounds__(256) merge_wgrad_batch_kernel(MwBatch b) {
+  const int i = blockIdx.x;
+#define MSEL(expr)                                          \
+  ({                                                        \
+    auto v_ = b.d[0].expr;                                  \
+    _Pragma("unroll") for (int j = 1; j < UM_MWG_MAX; ++j)  \
+      if (j == i) v_ = b.d[j].expr;                         \
+    v_;                                                     \
+  })
+  const float* parts = MSEL(parts);
+  const float* w = MSEL(w);
+  float* dw = MSEL(dw);
+  const int nparts = MSEL(nparts), nsrc = MSEL(nsrc), nw = MSEL(nw), acc = MSEL(accumulate);
+  int widx[UM_MWG_SRC];
+#pragma unroll
+  for (int q = 0; q < UM_MWG_SRC; ++q) widx[q] = MSEL(widx[q]);
+#undef MSEL
+  __shared__ double tot[UM_MWG_SRC];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int s0 = 0; s0 < UM_MWG_SRC; s0 += 4) {
+    const int s = s0 + wave;
+    if (s < nsrc) {
+      double t = 0.0;
+      for (int p = lane; p < nparts; p += 64) t += parts[(long)p * nsrc + s];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (lane == 0) tot[s] = t;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // as merge_wgrad_kernel, same order
+    if (!acc)
+      for (int j = 0; j < nw; ++j) dw[j] = 0.f;
+#pragma unroll
+    for (int s = 0; s < UM_MWG_SRC; ++s) {
+      if (s < nsrc) {
+        const float sg = sigmoidf_(w[widx[s]]);
+        dw[widx[s]] += (float)(tot[s] * sg * (1.0 - sg));
+      }
+    }
+  }
+}
+
 template <typename T>
 __global__ void image_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int H, int W,
                                      int Cp, T* __restrict__ out) {
@@ -212,6 +272,25 @@ int um_merge_wgrad(const float* parts, int nparts, int nsrc, const int* widx, co
   for (int i = 0; i < nsrc; ++i) a.widx[i] = widx[i];
   hipLaunchKernelGGL(merge_wgrad_kernel, dim3(1), dim3(256), 0, st, parts, nparts, nsrc, a, w, dw,
                      nw, accumulate);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_merge_wgrad_batch(const um_mwg_desc* descs, int n, hipStream_t st) {
+  UM_CHECK_ARG(descs != nullptr && n >= 0 && n <= UM_MWG_MAX, "um_merge_wgrad_batch: n");
+  if (n == 0) return UM_OK;
+  MwBatch b{};
+  b.n = n;
+  for (int i = 0; i < n; ++i) {
+    const um_mwg_desc& e = descs[i];
+    UM_CHECK_ARG(e.parts && e.w && e.dw && e.nsrc >= 1 && e.nsrc <= UM_MWG_SRC && e.nparts >= 1,
+                 "um_merge_wgrad_batch: descriptor");
+    MwDesc& d = b.d[i];
+    d.parts = e.parts; d.w = e.w; d.dw = e.dw;
+    d.nparts = e.nparts; d.nsrc = e.nsrc; d.nw = e.nw; d.accumulate = e.accumulate;
+    for (int q = 0; q < UM_MWG_SRC; ++q) d.widx[q] = q < e.nsrc ? e.widx[q] : 0;
+  }
+  hipLaunchKernelGGL(merge_wgrad_batch_kernel, dim3(n), dim3(256), 0, st, b);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

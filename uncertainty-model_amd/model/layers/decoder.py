@@ -135,10 +135,21 @@ class DecoderStage(nn.Module):
         N, H, W, _ = feature_map.shape
         dtype = x.dtype
         skip_t, skip_g = skip if isinstance(skip, tuple) else (skip, None)
-        cat1, segs1 = U.concat([U.CatSource(feature_map, CAT_COPY, self.feature_in_channels),
-                                U.CatSource(skip_t, CAT_UP2, self.skip_in_channels, skip_g)],
-                               N, H, W, dtype)
-        u1, gate = self.squeeze_excite[0]._fwd(cat1, se=self.squeeze_excite[1], segs=segs1)
+        se_block = self.squeeze_excite[0]
+        if U._SKIP_CONV and isinstance(se_block.layers[1], nn.modules.batchnorm._BatchNorm) \
+                and se_block.layers[0].padding is None \
+                and tuple(se_block.layers[0].layers[0].kernel_size) == (1, 1):
+            # 1x1 conv of cat(feature_map, up2(skip)) with the skip half at
+            # the skip's resolution (umamd.functional.SkipConvFn)
+            u1, gate = U.skip_conv_bn_elu(feature_map, skip_t, skip_g,
+                                          se_block.layers[0].layers[0], se_block.layers[1],
+                                          self.squeeze_excite[1], self.feature_in_channels,
+                                          self.skip_in_channels)
+        else:
+            cat1, segs1 = U.concat([U.CatSource(feature_map, CAT_COPY, self.feature_in_channels),
+                                    U.CatSource(skip_t, CAT_UP2, self.skip_in_channels, skip_g)],
+                                   N, H, W, dtype)
+            u1, gate = se_block._fwd(cat1, se=self.squeeze_excite[1], segs=segs1)
         xu = self.upsample[0]._fwd(x)  # [N, H/2, W/2, 4*Cu]; pixel shuffle folded into cat2
         srcs = [U.CatSource(xu, CAT_PSHUF, self.upsample_channels),
                 U.CatSource(u1, CAT_COPY, self.skip_out_channels, gate)]

@@ -42,6 +42,15 @@ class WredDesc(ctypes.Structure):
                 ('src0', _I * 4), ('dst0', _I * 4), ('len', _I * 4)]
 
 
+MWG_MAX, MWG_SRC = 24, 8  # UM_MWG_MAX, UM_MWG_SRC
+
+
+class MwgDesc(ctypes.Structure):
+    """um_mwg_desc: one merge-weight gradient of um_merge_wgrad_batch"""
+    _fields_ = [('parts', _P), ('w', _P), ('dw', _P), ('nparts', _I), ('nsrc', _I), ('nw', _I),
+                ('accumulate', _I), ('widx', _I * 8)]
+
+
 # name -> (restype, argtypes); 's' = stream
 _SIG = {
     'um_last_error': (ctypes.c_char_p, []),
@@ -52,6 +61,8 @@ _SIG = {
                            _I, _P, _I, _I, _F, _P, _I, _P, _P, _L, 's']),
     'um_conv2d_dgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
                              _P, _I, _P, _L, 's']),
+    'um_conv2d_fwd_up2': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _I, _P,
+                               _P, _I, _I, _I, 's']),
     'um_conv_fwd_ws': (_L, [_I, _I, _I, _I, _I, _I, _I]),
     'um_conv_dgrad_ws': (_L, [_I, _I, _I, _I, _I, _I, _I, _I]),
     'um_conv_dgrad_ws_pad': (_L, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
@@ -80,6 +91,8 @@ _SIG = {
     'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, _L, _P, 's']),
     'um_bn_elu_fwd_slots': (_I, [_I, _L, _I, _P, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P, _P, _P,
                                  _P, _P, _P, _I, _I, _L, _P, 's']),
+    'um_bn_elu_fwd_slots_merge': (_I, [_I, _L, _I, _P, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P,
+                                       _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, 's']),
     'um_bn_elu_bwd_reduce_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
                                         _P, 's']),
     'um_bn_elu_bwd_apply_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
@@ -97,6 +110,7 @@ _SIG = {
     'um_merge_parts': (_I, [_L]),
     'um_merge_bwd': (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _L, _P, _P, 's']),
     'um_merge_wgrad': (_I, [_P, _I, _I, _P, _P, _P, _I, _I, 's']),
+    'um_merge_wgrad_batch': (_I, [_P, _I, 's']),
     'um_image_to_nhwc': (_I, [_I, _P, _I, _I, _I, _I, _I, _P, 's']),
     'um_axpy': (_I, [_I, _L, _F, _P, _P, 's']),
     'um_sigmoid_scale_bwd': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),

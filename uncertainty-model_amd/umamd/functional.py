@@ -161,12 +161,17 @@ def _conv_wgrad_slabs(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw_ptr, 
     return slabs, d
 
 
-def wgrad_reduce_batch(descs):
-    """um_conv_wgrad_reduce_batch over a list of um_wred_desc, in chunks"""
-    for i in range(0, len(descs), L.WRED_MAX):
-        chunk = descs[i:i + L.WRED_MAX]
-        arr = (L.WredDesc * len(chunk))(*chunk)
-        call('um_conv_wgrad_reduce_batch', _ct.cast(arr, ctypes_p), len(chunk))
+def batched_launch(descs):
+    """The batched launches of a side-stream flush: every um_wred_desc in
+    um_conv_wgrad_reduce_batch calls, every um_mwg_desc in
+    um_merge_wgrad_batch calls (in chunks of the entries' maxima)."""
+    for kind, name, cap in ((L.WredDesc, 'um_conv_wgrad_reduce_batch', L.WRED_MAX),
+                            (L.MwgDesc, 'um_merge_wgrad_batch', L.MWG_MAX)):
+        ds = [d for d in descs if isinstance(d, kind)]
+        for i in range(0, len(ds), cap):
+            chunk = ds[i:i + cap]
+            arr = (kind * len(chunk))(*chunk)
+            call(name, _ct.cast(arr, ctypes_p), len(chunk))
 
 
 def _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw_ptr, segs):
@@ -406,19 +411,24 @@ class ConvSpec:
 class _CBEState:
     """What a conv+BN+ELU forward keeps for its backward (the autograd ctx
     of ConvBNELUFn, or one node of a GraphBlockFn)."""
-    __slots__ = ('spec', 'sync', 'slots_b', 'has_bn', 'geom', 'se', 'saved')
+    __slots__ = ('spec', 'sync', 'slots_b', 'has_bn', 'geom', 'se', 'saved', 'merged')
 
 
-def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec):
+def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, yconv=None):
     """Conv2d -> BatchNorm2d -> ELU [-> SE gate] forward without autograd:
-    -> (outputs tuple, _CBEState)"""
+    -> (outputs tuple, _CBEState).  ``merge`` = (srcs with None for this
+    layer's output, widx, mean_weight): also compute that NodeBlock merge
+    (fused into the BN apply pass where the statistics slots are used), the
+    result in ``state.merged``.  ``yconv(epi, stats)`` replaces the conv
+    (it returns the f32 pre-BN output; the state then saves no packed
+    weights: its backward brings its own conv part, see skip_conv_bn_elu)."""
     ctx = _CBEState()
     L.require_device(x)
     N, H, W, Cp = x.shape
     K, Creal, R, _ = weight.shape
     bn = spec.bn
     dev = x.device
-    wf, wT = _pack(weight, Cp, x.dtype, segs=spec.segs)
+    wf, wT = _pack(weight, Cp, x.dtype, segs=spec.segs) if yconv is None else (None, None)
     P = (H + 2 * spec.pad - R) // spec.stride + 1
     Q = (W + 2 * spec.pad - R) // spec.stride + 1
     M = N * P * Q
@@ -440,7 +450,7 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec):
         slots_b = _ARENA.take(nslot + 1)
         y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
                       out_dtype=torch.float32, epi=L.EPI_STAT_SLOTS, stats=slots_f,
-                      creal=Creal)
+                      creal=Creal) if yconv is None else yconv(L.EPI_STAT_SLOTS, slots_f)
         if sync.collective:  # the conv stored this rank's count after the slots
             sync.all_reduce(slots_f)
             count = -1.0  # read the all-reduced count after the slots
@@ -451,16 +461,18 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec):
     elif bn is not None:
         nparts = query('um_conv_stats_parts', M, K)
         parts = torch.empty((nparts, K, 2), dtype=torch.float32, device=dev)
+        epi = L.EPI_STATS if training else L.EPI_NONE
         y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
-                      out_dtype=torch.float32,
-                      epi=L.EPI_STATS if training else L.EPI_NONE, stats=parts, creal=Creal)
+                      out_dtype=torch.float32, epi=epi, stats=parts, creal=Creal) \
+            if yconv is None else yconv(epi, parts)
         mean, invstd, scale, shift = _bn_forward_coeffs(parts, nparts, K, M, bn, sync,
                                                         training, dev)
     else:  # ConvELUBlock(batch_norm=False): identity normalisation
         sync = None
         training = False
         y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
-                      out_dtype=torch.float32, creal=Creal)
+                      out_dtype=torch.float32, creal=Creal) if yconv is None \
+            else yconv(L.EPI_NONE, None)
         mean = shift = _const_vec(0.0, K, dev)
         invstd = scale = _const_vec(1.0, K, dev)
     a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y is f32 (pre-BN)
@@ -468,14 +480,26 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec):
     if w1 is not None and _FUSED_SE:  # the SE squeeze rides in the BN-apply pass
         npool = query('um_bn_fwd_pool_parts_c', M, P * Q, K)
         pool = torch.empty((npool, K), dtype=torch.float32, device=dev)
+    merged = None
     if slots_f is not None:
         upd = bn.track_running_stats and bn.running_mean is not None
         nbt = bn.num_batches_tracked if upd else None
-        call('um_bn_elu_fwd_slots', _dt(a), M, K, ptr(y), K, ptr(slots_f), count,
-             ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0),
-             ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
-             ptr(nbt), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K,
-             int(spec.elu), P * Q, ptr(pool))
+        rs = (ptr(bn.running_mean) if upd else None, ptr(bn.running_var) if upd else None,
+              ptr(nbt))
+        if merge is not None and pool is None and _FUSED_MERGE:
+            msrcs, mwidx, mw = merge
+            n = len(msrcs)
+            merged = torch.empty_like(a)
+            call('um_bn_elu_fwd_slots_merge', _dt(a), M, K, ptr(y), K, ptr(slots_f), count,
+                 ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs,
+                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K, int(spec.elu), n,
+                 (ctypes_p * n)(*[t.data_ptr() if t is not None else None for t in msrcs]),
+                 (ctypes_i * n)(*mwidx), ptr(mw), msrcs.index(None), ptr(merged))
+        else:
+            call('um_bn_elu_fwd_slots', _dt(a), M, K, ptr(y), K, ptr(slots_f), count,
+                 ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs,
+                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K,
+                 int(spec.elu), P * Q, ptr(pool))
     else:
         call('um_bn_elu_fwd', _dt(a), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
              int(spec.elu), P * Q, ptr(pool))
@@ -496,6 +520,11 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec):
              ptr(w1c), ptr(w2c), ptr(z1), ptr(s))
         se = (pooled, z1, s)
         outs.append(s)
+    if merge is not None and merged is None:  # not fused: the separate merge launch
+        msrcs, mwidx, mw = merge
+        merged = _merge_launch([a if t is None else t for t in msrcs], mw, mwidx, None,
+                               torch.empty_like(a))
+    ctx.merged = merged
     ctx.spec = spec
     ctx.sync = sync
     ctx.slots_b = slots_b
@@ -506,7 +535,8 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec):
     return tuple(outs), ctx
 
 
-def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=False):
+def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=False,
+             conv_bwd=None):
     """Backward of _cbe_fwd -> (dx, dW, dbias, dgamma, dbeta, dw1, dw2).
     ``dx``: write (or with ``dx_accumulate`` add) the input gradient into
     this tensor instead of a new one (a GraphBlockFn predecessor's gradient
@@ -614,15 +644,19 @@ def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=
         call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
              ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1),
              ptr(k2), ptr(k3), ptr(dy), K, ptr(bparts))
-    dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode,
-                     segs=spec.segs)
+    if conv_bwd is not None:  # the caller's conv part (skip_conv_bn_elu): dy -> (dx, dW)
+        dx, dW = conv_bwd(dy)
+        need_x = False
+    else:
+        dW = _conv_wgrad(x, dy, K, K, Creal, R, spec.stride, spec.pad, spec.pad_mode,
+                         segs=spec.segs)
     if reduce_b:
         dbias = torch.empty(K, dtype=torch.float32, device=dev)
         _reduce_rows(bparts, nbp, K, dbias)
     if need_x:
         dx = _conv_dgrad(dy, wT, (N, H, W, Cp), K, R, spec.stride, spec.pad, spec.pad_mode,
                          dx=dx, accumulate=dx_accumulate, creal=Creal)
-    else:
+    elif conv_bwd is None:
         dx = None
     return dx, dW, dbias, dgamma, dbeta, dw1, dw2
 
@@ -658,6 +692,136 @@ def conv_bn_elu(x, conv, bn, pad, pad_mode, se=None, elu=True, segs=None):
     return ConvBNELUFn.apply(x, conv.weight, conv.bias,
                              bn.weight if affine else None, bn.bias if affine else None,
                              w1, w2, spec)
+
+
+# ------------------------------------------------ decoder skip 1x1 conv --
+class SkipConvFn(torch.autograd.Function):
+    """DecoderStage's squeeze-excite ConvELUBlock on cat(feature_map,
+    interpolate(skip, x2) * gate) (reference model/layers/decoder.py:228-238,
+    :55-87, :90-136) without the full-resolution concat: a 1x1 conv and the
+    bilinear x2 upsample are both linear and act on different axes, so
+
+        W [fm | up2(g*skip)] = W_f fm + up2(W_s (g*skip))
+
+    The skip half is convolved at the skip's (quarter) pixel count into an
+    f32 map z, and um_conv2d_fwd_up2 adds up2(z) in the epilogue of the
+    feature-map half (before the BN statistics).  Backward: t = up2^T(dy) at
+    the low resolution, dW_s = t (x) (g*skip), d(g*skip) = W_s^T t, the gate
+    adjoint as the concat's; dW_f and d fm at full resolution."""
+
+    @staticmethod
+    def forward(ctx, fm, skip, gate, weight, bias, gamma, beta, w1, w2, spec: ConvSpec,
+                fin: int, skin: int):
+        L.require_device(fm)
+        N, H, W, Cf = fm.shape
+        _, h, w, Cs = skip.shape
+        K = weight.shape[0]
+        dt = fm.dtype
+        # g * skip at the low resolution (one gated copy)
+        gs = _gated_copy(skip, gate, skin) if gate is not None else skip
+        Cg = gs.shape[-1]
+        wf_s, wT_s = _pack(weight, Cg, dt, segs=[(fin, 0, skin)])
+        wf_f, wT_f = _pack(weight, Cf, dt, segs=[(0, 0, fin)])
+        z = _conv_fwd(gs, wf_s, None, K, 1, 1, 0, L.PAD_ZERO, out_dtype=torch.float32,
+                      creal=skin)
+        bias_f = bias.detach().float().contiguous() if bias is not None else None
+
+        def yconv(epi, stats):
+            y = torch.empty((N, H, W, K), dtype=torch.float32, device=fm.device)
+            call('um_conv2d_fwd_up2', _dt(fm), N, H, W, Cf, Cf, ptr(fm), ptr(wf_f), ptr(bias_f),
+                 K, H, W, ptr(y), K, epi, ptr(stats), ptr(z), h, w, K,
+                 work=_conv_flops(N, H, W, K, 1, fin) + _conv_flops(N, h, w, K, 1, skin))
+            return y
+
+        outs, st = _cbe_fwd(fm, weight, bias, gamma, beta, w1, w2, spec, yconv=yconv)
+        x_, _, y, mean, invstd, scale, shift, gamma_, w1_, w2_ = st.saved
+        st.saved = None
+        ctx.st = st
+        ctx.geo = (N, H, W, Cf, h, w, Cg, K, fin, skin)
+        ctx.save_for_backward(fm, skip, gate, gs, wT_s, wT_f, y, mean, invstd, scale, shift,
+                              gamma_, w1_, w2_)
+        return outs if len(outs) > 1 else outs[0]
+
+    @staticmethod
+    def backward(ctx, da, ds=None):
+        (fm, skip, gate, gs, wT_s, wT_f, y, mean, invstd, scale, shift, gamma, w1,
+         w2) = ctx.saved_tensors
+        N, H, W, Cf, h, w, Cg, K, fin, skin = ctx.geo
+        st = ctx.st
+        st.saved = (fm, None, y, mean, invstd, scale, shift, gamma, w1, w2)
+        need_fm, need_skip = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_gate = gate is not None and ctx.needs_input_grad[2]
+        res = {}
+
+        def conv_bwd(dy):
+            dW = torch.empty((K, fin + skin, 1, 1), dtype=torch.float32, device=dy.device)
+            _conv_wgrad(fm, dy, K, K, fin + skin, 1, 1, 0, L.PAD_ZERO, dw=dW,
+                        segs=[(0, 0, fin)])
+            # t = up2^T(dy): the concat adjoint of an UP2 source with K channels
+            t = torch.empty((N, h, w, K), dtype=dy.dtype, device=dy.device)
+            src = L.CatSrc(t.data_ptr(), None, K, K, L.CAT_UP2, 0, _dt(t), h, w)
+            call('um_concat_bwd_src', _dt(dy), N, H, W, ptr(dy), K, _ct.byref(src), ptr(t), K,
+                 _dt(t), 0, None, None)
+            _conv_wgrad(gs, t, K, K, fin + skin, 1, 1, 0, L.PAD_ZERO, dw=dW,
+                        segs=[(fin, 0, skin)])
+            if need_skip or need_gate:
+                dgs = _conv_dgrad(t, wT_s, (N, h, w, Cg), K, 1, 1, 0, L.PAD_ZERO, creal=skin)
+                if gate is None:
+                    res['skip'] = dgs
+                else:
+                    res['skip'], res['gate'] = _gated_copy_bwd(dgs, skip, gate, skin,
+                                                               need_skip, need_gate)
+            dfm = _conv_dgrad(dy, wT_f, (N, H, W, Cf), K, 1, 1, 0, L.PAD_ZERO, creal=fin) \
+                if need_fm else None
+            return dfm, dW
+
+        dfm, dW, dbias, dgamma, dbeta, dw1, dw2 = _cbe_bwd(
+            st, da, ds, need_x=need_fm, need_b=ctx.needs_input_grad[4], conv_bwd=conv_bwd)
+        st.saved = None
+        return (dfm, res.get('skip'), res.get('gate'), dW, dbias, dgamma, dbeta, dw1, dw2,
+                None, None, None)
+
+
+def _gated_copy(skip, gate, C):
+    """g * skip (per (n, c) gate) as one concat-build launch"""
+    N, h, w, _ = skip.shape
+    src = (L.CatSrc * 1)(L.CatSrc(skip.data_ptr(), gate.data_ptr(), C, skip.shape[-1],
+                                  L.CAT_COPY, 0, _dt(skip), h, w))
+    Ct = ceil8(C)
+    out = torch.empty((N, h, w, Ct), dtype=skip.dtype, device=skip.device)
+    call('um_concat_build', _dt(out), N, h, w, ptr(out), Ct, Ct, 1, src)
+    return out
+
+
+def _gated_copy_bwd(dgs, skip, gate, C, need_skip, need_gate):
+    """adjoint of _gated_copy: (d skip, d gate)"""
+    N, h, w, Ct = dgs.shape
+    s = L.CatSrc(skip.data_ptr(), gate.data_ptr(), C, skip.shape[-1], L.CAT_COPY, 0, _dt(skip),
+                 h, w)
+    dsk = torch.empty_like(skip) if need_skip else None
+    dg = torch.zeros_like(gate) if need_gate else None
+    ws = None
+    if need_gate:
+        ws = torch.empty((query('um_concat_bwd_ws', N, h, w, C),), dtype=torch.float32,
+                         device=dgs.device)
+    call('um_concat_bwd_src', _dt(dgs), N, h, w, ptr(dgs), Ct, _ct.byref(s), ptr(dsk),
+         skip.shape[-1], _dt(skip), 0, ptr(dg), ptr(ws))
+    return dsk, dg
+
+
+_SKIP_CONV = os.environ.get('UMAMD_SKIP_CONV', '1') == '1'
+
+
+def skip_conv_bn_elu(feature_map, skip, gate, conv, bn, se, fin: int, skin: int):
+    """ConvELUBlock(1x1, BN) [+ SE] on cat(feature_map, up2(skip) * gate)
+    (see SkipConvFn); returns (a, s) with ``se`` like conv_bn_elu."""
+    spec = ConvSpec(conv, bn, 0, L.PAD_ZERO, True, None)
+    w1 = se.excite[0].weight if se is not None else None
+    w2 = se.excite[2].weight if se is not None else None
+    affine = bn is not None and bn.affine
+    return SkipConvFn.apply(feature_map, skip, gate, conv.weight, conv.bias,
+                            bn.weight if affine else None, bn.bias if affine else None, w1, w2,
+                            spec, int(fin), int(skin))
 
 
 # -------------------------------------------------------------------- merge --
@@ -720,6 +884,8 @@ def merge(inputs: Sequence[torch.Tensor], w: Optional[torch.Tensor], widx: Seque
 
 # -------------------------------------------------------------- graph block --
 _STAGE_FN = os.environ.get('UMAMD_STAGE_FN', '1') == '1'
+# a GraphBlock node's merge computed by the BN pass of its last predecessor
+_FUSED_MERGE = os.environ.get('UMAMD_FUSED_MERGE', '1') == '1'
 
 
 class GraphSpec:
@@ -743,6 +909,13 @@ class GraphSpec:
             self.slices.append((len(self.params), len(ps)))
             self.params += ps
             self.widx.append([0] + list(range(len(preds) - 1)))
+        # node p -> the first multi-input node s whose last predecessor (in
+        # id order, the evaluation order) is p: s's merge is fused into p's
+        # BN apply pass (umamd.functional._cbe_fwd, um_bn_elu_fwd_slots_merge)
+        self.merge_after = {}
+        for s, preds in enumerate(self.nodes):
+            if len(preds) > 1 and len(preds) <= 8 and max(preds) < s:
+                self.merge_after.setdefault(max(preds), s)
 
 
 def _merge_launch(srcs, w, widx, coefs, out):
@@ -776,10 +949,18 @@ class GraphBlockFn(torch.autograd.Function):
                 inp = x
             elif len(preds) == 1:
                 inp = a[preds[0]]
+            elif j in merged:  # computed by the BN pass of its last predecessor
+                inp = merged.pop(j)
             else:
                 inp = _merge_launch([a[p] for p in preds], mw, gs.widx[j], None,
                                     torch.empty_like(a[preds[0]]))
-            outs, st = _cbe_fwd(inp, w, b, g, be, None, None, gs.specs[j])
+            mg, s = None, gs.merge_after.get(j)
+            if s is not None:  # node s's merge rides in this node's BN pass
+                so = gs.slices[s][0]
+                mg = ([None if p == j else a[p] for p in gs.nodes[s]], gs.widx[s], params[so + 4])
+            outs, st = _cbe_fwd(inp, w, b, g, be, None, None, gs.specs[j], merge=mg)
+            if s is not None:
+                merged[s], st.merged = st.merged, None
             a.append(outs[0])
             states.append(st)
         if len(gs.out_nodes) == 1:
@@ -849,10 +1030,20 @@ class GraphBlockFn(torch.autograd.Function):
                      ptr(mw), None, dm.numel(), ptr(dm), ptr(parts))
                 if need_w:
                     dmw = torch.empty(mw.shape, dtype=torch.float32, device=dm.device)
-                    grads[o + 4] = _param_grad(
-                        (parts, mw), dmw,
-                        lambda a=(ptr(parts), nparts, k, idx, ptr(mw), ptr(dmw), mw.numel()): call(
-                            'um_merge_wgrad', *a, 0))
+                    if _WRED_BATCH and _overlap.active() is not None and k <= L.MWG_SRC:
+                        # one um_merge_wgrad_batch launch per side-stream flush
+                        d = L.MwgDesc()
+                        d.parts, d.w, d.dw = parts.data_ptr(), mw.data_ptr(), dmw.data_ptr()
+                        d.nparts, d.nsrc, d.nw, d.accumulate = nparts, k, mw.numel(), 0
+                        for q, wi in enumerate(gs.widx[j]):
+                            d.widx[q] = wi
+                        grads[o + 4] = _param_grad((parts, mw), dmw,
+                                                   lambda d=d, keep=parts: (keep, d))
+                    else:
+                        grads[o + 4] = _param_grad(
+                            (parts, mw), dmw,
+                            lambda a=(ptr(parts), nparts, k, idx, ptr(mw), ptr(dmw), mw.numel()):
+                            call('um_merge_wgrad', *a, 0))
             dW, dbias, dgamma, dbeta = pg[0], pg[1], pg[2], pg[3]
             grads[o], grads[o + 1], grads[o + 2], grads[o + 3] = dW, dbias, dgamma, dbeta
             states[j] = None  # release this node's saved tensors

@@ -94,13 +94,17 @@ class WgradStream:
         with torch.cuda.stream(self.stream):
             keep, descs = [], []
             for _, launch in self._pending:
-                r = launch()  # a weight gradient returns (slabs, um_wred_desc)
-                if isinstance(r, tuple) and len(r) == 2 and isinstance(r[1], L.WredDesc):
+                # a batched piece returns (what it must keep alive, descriptor):
+                # conv weight gradients (slabs, um_wred_desc), merge weights
+                # (partial sums, um_mwg_desc)
+                r = launch()
+                if isinstance(r, tuple) and len(r) == 2 and \
+                        isinstance(r[1], (L.WredDesc, L.MwgDesc)):
                     keep.append(r[0])
                     descs.append(r[1])
             if descs:
-                F.wgrad_reduce_batch(descs)
-            del keep  # freed on the side stream, after the reduction
+                F.batched_launch(descs)
+            del keep  # freed on the side stream, after the batched launches
         for tensors, _ in self._pending:
             for t in tensors:
                 t.record_stream(self.stream)
