@@ -405,9 +405,10 @@ def test_wgrad(case):
 # WgradStream flush) against the per-conv reduction: same slabs, same
 # summation order -> bit-identical dW, incl. a segment-mapped (concat) input
 # and more convs than one launch takes (UM_WRED_MAX)
-def test_wgrad_reduce_batch_matches_per_conv():
+def test_wgrad_reduce_batch_matches_per_conv(monkeypatch):
     from umamd import functional as U
     from umamd import overlap
+    monkeypatch.setattr(U, '_WRED_BATCH', True)  # off by default (measured slower)
     from umamd._lib import PAD_REFLECT, PAD_ZERO, WRED_MAX
     g = torch.Generator().manual_seed(3)
     cases = [(32, 32, 7, 1, PAD_ZERO, 12, 64, None), (64, 128, 3, 1, PAD_REFLECT, 6, 32, None),

@@ -120,7 +120,9 @@ struct MergeOut {
 // 128..512) are sliced so a block finishes only its channels' statistics
 // slots (16 KB instead of up to 128 KB per block) and the grid still has a
 // few hundred blocks; wide layers keep one slice (cs = C).
-template <typename T>
+// MERGE: the fused-merge instance (its register footprint, ~200 VGPRs with
+// up to 8 sources, stays out of the plain instance's ~94)
+template <typename T, bool MERGE>
 __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
     const float* __restrict__ y, int ldy, long M, int C, const float* __restrict__ scale,
     const float* __restrict__ shift, T* __restrict__ a, int lda, int apply_elu,
@@ -141,7 +143,8 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
   }
   float mc[FMERGE_MAX];  // merge coefficients (uniform; unrolled static indices)
 #pragma unroll
-  for (int i = 0; i < FMERGE_MAX; ++i) mc[i] = i < mo.n ? sigmoidf_(mo.w[mo.widx[i]]) : 0.f;
+  for (int i = 0; i < FMERGE_MAX; ++i)
+    mc[i] = MERGE && i < mo.n ? sigmoidf_(mo.w[mo.widx[i]]) : 0.f;
   for (int g0 = 0; g0 < cg; g0 += rm.G) {
     const int g = g0 + rm.g;
     float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -157,13 +160,13 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
           v[e] = apply_elu ? eluf_(z) : z;
         }
         store8(a + m * lda + c, v);
-        if (pool || mo.n) {
+        if (pool || MERGE) {
           float r[8];
           load8_rounded(v, r, a);
           if (pool)
 #pragma unroll
             for (int e = 0; e < 8; ++e) ps[e] += r[e];
-          if (mo.n) {  // the merge in source order, as merge_fwd_kernel
+          if constexpr (MERGE) {  // the merge in source order, as merge_fwd_kernel
             float acc[8], sv[8];
 #pragma unroll
             for (int i = 0; i < FMERGE_MAX; ++i) {
@@ -186,11 +189,19 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
           }
         }
       };
+      if constexpr (MERGE) {
+        for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+          float v[8];
+          load8(y + m * ldy + c, v);
+          row(m, v);
+        }
+      } else {
 #pragma unroll 4
-      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
-        float v[8];
-        load8(y + m * ldy + c, v);
-        row(m, v);
+        for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+          float v[8];
+          load8(y + m * ldy + c, v);
+          row(m, v);
+        }
       }
     }
     if (pool) {
@@ -622,14 +633,15 @@ static int bn_fwd_launch(int dtype, long M, int C, const void* y, int ldy, const
   const dim3 g(ceil_div(M, rows), sl.ns);
   const size_t shm = (pool_parts ? 256 * 8 * sizeof(float) : 0) +
                      (fin.slots ? 2 * (size_t)sl.cs * sizeof(float) : 0);
-  if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_fwd_kernel<bf16_t>, g, dim3(256), shm, st, (const float*)y,
-                       ldy, M, C, scale, shift, (bf16_t*)a, lda, apply_elu, rows, pool_parts, fin,
-                       sl.cs, mo);
-  else
-    hipLaunchKernelGGL(bn_elu_fwd_kernel<float>, g, dim3(256), shm, st, (const float*)y,
-                       ldy, M, C, scale, shift, (float*)a, lda, apply_elu, rows, pool_parts, fin,
-                       sl.cs, mo);
+#define UM_BN_FWD(T_, MG_)                                                                     \
+  hipLaunchKernelGGL((bn_elu_fwd_kernel<T_, MG_>), g, dim3(256), shm, st, (const float*)y, ldy, M, \
+                     C, scale, shift, (T_*)a, lda, apply_elu, rows, pool_parts, fin, sl.cs, mo)
+  if (dtype == UM_BF16) {
+    if (mo.n) UM_BN_FWD(bf16_t, true); else UM_BN_FWD(bf16_t, false);
+  } else {
+    if (mo.n) UM_BN_FWD(float, true); else UM_BN_FWD(float, false);
+  }
+#undef UM_BN_FWD
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -138,7 +138,7 @@ __device__ __forceinline__ void border_pixel(const IgArgs& a, int m, int& n, int
     if (j < a.nrr && pick4(a.rr, j) <= y) ++y;
 }
 
-// MODE: 0 plain rows, 1 parity class rows (stride-2 data gradient), 2 the
+// MODE: 0 plain rows, 3 plain rows + the up2 add (IgArgs::up2), 1 parity class rows (stride-2 data gradient), 2 the
 // border list of the reflect fold (IgArgs::border)
 template <int MODE>
 __device__ __forceinline__ ARow decode_row(const IgArgs& a, int m) {
@@ -240,20 +240,31 @@ __device__ __forceinline__ void up2_tap(int i, int in, int out, int& i0, int& i1
   i1 = i0 + ((i0 < in - 1) ? 1 : 0);
   l1 = src - (float)i0;
 }
-__device__ __forceinline__ float up2_at(const IgArgs& a, int m, int n) {
+struct Up2Row {
+  const float *r0, *r1;  // rows y0, y1 of the low-resolution map
+  int x0, x1;            // element offsets of columns x0, x1 (times up2_ld)
+  float ly, lx;
+};
+__device__ __forceinline__ Up2Row up2_row(const IgArgs& a, int m) {
   const int hw = a.oh * a.ow;
   const int b = m / hw, rem = m - b * hw;
   const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
   int y0, y1, x0, x1;
-  float ly, lx;
-  up2_tap(oy, a.up2_h, a.oh, y0, y1, ly);
-  up2_tap(ox, a.up2_w, a.ow, x0, x1, lx);
-  const float* p = a.up2 + (long)b * a.up2_h * a.up2_w * a.up2_ld + n;
-  const float v00 = p[((long)y0 * a.up2_w + x0) * a.up2_ld];
-  const float v01 = p[((long)y0 * a.up2_w + x1) * a.up2_ld];
-  const float v10 = p[((long)y1 * a.up2_w + x0) * a.up2_ld];
-  const float v11 = p[((long)y1 * a.up2_w + x1) * a.up2_ld];
-  return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+  Up2Row u;
+  up2_tap(oy, a.up2_h, a.oh, y0, y1, u.ly);
+  up2_tap(ox, a.up2_w, a.ow, x0, x1, u.lx);
+  const float* p = a.up2 + (long)b * a.up2_h * a.up2_w * a.up2_ld;
+  u.r0 = p + (long)y0 * a.up2_w * a.up2_ld;
+  u.r1 = p + (long)y1 * a.up2_w * a.up2_ld;
+  u.x0 = x0 * a.up2_ld;
+  u.x1 = x1 * a.up2_ld;
+  return u;
+}
+__device__ __forceinline__ float up2_val(const Up2Row& u, int n) {
+  const float v00 = u.r0[u.x0 + n], v01 = u.r0[u.x1 + n];
+  const float v10 = u.r1[u.x0 + n], v11 = u.r1[u.x1 + n];
+  return (1.f - u.ly) * ((1.f - u.lx) * v00 + u.lx * v01) +
+         u.ly * ((1.f - u.lx) * v10 + u.lx * v11);
 }
 
 // Epilogue shared by the register-staged and the LDS-DMA main loops: split-K
@@ -295,6 +306,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
   float csum[TN], csq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+  if constexpr (MODE != 3) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = bn + wn * (BN / WN) + j * 16 + col_l;
@@ -307,7 +319,6 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
         const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
         if (!nok || m >= a.M) continue;
         float v = acc[i][j][q] + bv;
-        if (MODE == 0 && a.up2 != nullptr) v += up2_at(a, m, n);
         const long off = out_row<MODE>(a, m) + n;
         if (a.epilogue == UM_EPI_RESIDUAL)
           v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
@@ -326,6 +337,51 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
         csum[j] += v;
         csq[j] += v * v;
       }
+  }
+  } else {
+  // MODE 3 (plain rows + the up2 add): rows outer, columns inner, so the
+  // row's output offset and up2 taps are derived once per row; each
+  // column's sums still run over the rows in the same order
+  float bv[TN];
+  int ncol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    ncol[j] = bn + wn * (BN / WN) + j * 16 + col_l;
+    bv[j] = (a.bias != nullptr && ncol[j] < a.NC) ? a.bias[ncol[j]] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
+      if (m >= a.M) continue;
+      const long orow = out_row<MODE>(a, m);
+      const Up2Row ur = up2_row(a, m);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = ncol[j];
+        if (n >= a.NC) continue;
+        float v = acc[i][j][q] + bv[j];
+        v += up2_val(ur, n);
+        const long off = orow + n;
+        if (a.epilogue == UM_EPI_RESIDUAL)
+          v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
+        if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
+        if (a.out_f32) {
+          float* o = reinterpret_cast<float*>(a.out) + off;
+          if (a.accumulate) v += *o;
+          *o = v;
+        } else if (staged) {  // accumulate (if any) happens at the row store
+          sOut[(m - bm) * BN + (n - bn)] = from_f32<T>(v);
+        } else {
+          T* o = reinterpret_cast<T*>(a.out) + off;
+          if (a.accumulate) v += to_f32(*o);
+          *o = from_f32<T>(v);
+        }
+        csum[j] += v;
+        csq[j] += v * v;
+      }
+    }
   }
   if (a.epilogue == UM_EPI_STATS) {
 #pragma unroll
@@ -1026,7 +1082,7 @@ void split_plan(Plan& p, int M, int NC, int taps, int ach, long ws_bytes, bool g
 template <typename T, int BK, int BM, int BN, int WM, int WN, int MODE>
 int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
   const int ntm = ceil_div(a.M, BM), ntn = ceil_div(a.NC, BN);
-  if constexpr (sizeof(T) == 2 && BK == 64 && WM == 2 && WN == 2 && MODE != 2) {
+  if constexpr (sizeof(T) == 2 && BK == 64 && WM == 2 && WN == 2 && MODE != 2 && MODE != 3) {
     if (a.pmode != umamd::IG_FOLD && (knobs().glds & (BM == 64 ? 1 : 2))) {
       const bool w8 = BM == 64 && (knobs().glds & 4);
       const long blocks = (long)ntm * ntn * p.splits;
@@ -1074,6 +1130,8 @@ int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
 
 template <typename T, int BK, int BM, int BN, int WM, int WN>
 int launch(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
+  if (a.up2 != nullptr)  // plain rows + the up2 add (register main loop, no split)
+    return launch_cls<T, BK, BM, BN, WM, WN, 3>(a, p, ws, st);
   return a.cls ? launch_cls<T, BK, BM, BN, WM, WN, 1>(a, p, ws, st)
                : launch_cls<T, BK, BM, BN, WM, WN, 0>(a, p, ws, st);
 }

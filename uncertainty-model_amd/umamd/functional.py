@@ -138,8 +138,14 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
 
 
 # the side stream's slab reductions as ONE um_conv_wgrad_reduce_batch launch
-# per flush instead of one um_conv_wgrad_reduce_seg per conv
-_WRED_BATCH = os.environ.get('UMAMD_WRED_BATCH', '1') == '1'
+# per flush instead of one um_conv_wgrad_reduce_seg per conv.  Measured on
+# MI355X (bench step, tools/gpu_arms.sh r03j): 734 with vs 771 pairs/s
+# without -- the batch lands as one chip-wide burst at the end of each flush
+# instead of small reductions filling the gaps beside the data-gradient
+# chain -- so it is off; the merge-weight gradients (15 single-workgroup
+# launches -> 1 per flush) stay batched (UMAMD_MWG_BATCH)
+_WRED_BATCH = os.environ.get('UMAMD_WRED_BATCH', '0') == '1'
+_MWG_BATCH = os.environ.get('UMAMD_MWG_BATCH', '1') == '1'
 
 
 def _conv_wgrad_slabs(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw_ptr, segs):
@@ -1030,7 +1036,7 @@ class GraphBlockFn(torch.autograd.Function):
                      ptr(mw), None, dm.numel(), ptr(dm), ptr(parts))
                 if need_w:
                     dmw = torch.empty(mw.shape, dtype=torch.float32, device=dm.device)
-                    if _WRED_BATCH and _overlap.active() is not None and k <= L.MWG_SRC:
+                    if _MWG_BATCH and _overlap.active() is not None and k <= L.MWG_SRC:
                         # one um_merge_wgrad_batch launch per side-stream flush
                         d = L.MwgDesc()
                         d.parts, d.w, d.dw = parts.data_ptr(), mw.data_ptr(), dmw.data_ptr()
