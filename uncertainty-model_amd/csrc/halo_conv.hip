@@ -193,9 +193,14 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int ty = 2 * wave + (i >> 1);
-      const long mrow = ((long)nimg * a.oh + ty0 + ty) * a.ow + tx0 + (i & 1) * 16 + row_g;
+      const int oxb = tx0 + (i & 1) * 16 + row_g;
+      // partial tiles at the bottom / right edge (output sizes not multiples
+      // of the 8 x 32 tile: the padded-domain reflect data gradient)
+      const bool yok = ty0 + ty < a.oh;
+      const long mrow = ((long)nimg * a.oh + ty0 + ty) * a.ow + oxb;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        if (!yok || oxb + q >= a.ow) continue;
         const long m = mrow + q;
         float v = acc[i][j][q] + bv;
         const long off = m * a.ld_out + n;
@@ -255,7 +260,7 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
 
 template <int R, int BN>
 int launch_r(const IgArgs& a, hipStream_t st) {
-  const int tiles_x = a.ow / TW, tiles_y = a.oh / TH;
+  const int tiles_x = (a.ow + TW - 1) / TW, tiles_y = (a.oh + TH - 1) / TH;
   dim3 grid(a.on * tiles_y * tiles_x, (a.NC + BN - 1) / BN);
   if (a.flip)
     hipLaunchKernelGGL((halo_conv_kernel<R, BN, true, false>), grid, dim3(256), 0, st, a, tiles_x,
@@ -300,8 +305,15 @@ bool halo_applicable(int dtype, const IgArgs& a, int min_tiles, int max_nc) {
   if (a.R != 3 && a.R != 5 && a.R != 7) return false;
   if (a.pmode == IG_FOLD) return false;                         // reflect transpose: igemm
   if (a.flip && a.pmode != IG_PAD_ZERO) return false;
-  if (a.oh != a.ah || a.ow != a.aw || a.pad != (a.R - 1) / 2) return false;  // "same" conv
-  if (a.oh % TH || a.ow % TW) return false;
+  // "same" conv, or the zero-pad transposed conv onto the reflect-padded
+  // input (output (H+2p) x (W+2p) from a P x Q dy with pad R-1: the padded
+  // form of the reflect data gradient, umamd::pad_dgrad in conv.hip);
+  // partial edge tiles are masked in the epilogue
+  const bool same = a.oh == a.ah && a.ow == a.aw && a.pad == (a.R - 1) / 2;
+  const bool grown = a.flip && a.pad == a.R - 1 && a.oh == a.ah + a.R - 1 && a.ow == a.aw + a.R - 1;
+  if (!same && !grown) return false;
+  if (!same && (a.epilogue == UM_EPI_STATS)) return false;
+  if (a.ow < TW / 2) return false;  // mostly-empty column tiles: the GEMM
   if (a.NC > max_nc || a.ach % 8 || a.lda % 8) return false;
   // 8-channel operands fill a quarter of each 32-channel chunk: past one
   // 64-column block the tap-packed GEMM is faster (disp-head data gradient
@@ -311,7 +323,7 @@ bool halo_applicable(int dtype, const IgArgs& a, int min_tiles, int max_nc) {
   // (stat_slots) take any tiling
   if (a.epilogue == UM_EPI_STATS && !a.stat_slots && a.stats_rows != 128) return false;
   // enough tiles to fill the chip
-  return (long)a.on * (a.oh / TH) * (a.ow / TW) >= min_tiles;
+  return (long)a.on * ((a.oh + TH - 1) / TH) * ((a.ow + TW - 1) / TW) >= min_tiles;
 }
 
 int halo_run(const IgArgs& a, hipStream_t st) {

@@ -736,7 +736,7 @@ class SkipConvFn(torch.autograd.Function):
             y = torch.empty((N, H, W, K), dtype=torch.float32, device=fm.device)
             call('um_conv2d_fwd_up2', _dt(fm), N, H, W, Cf, Cf, ptr(fm), ptr(wf_f), ptr(bias_f),
                  K, H, W, ptr(y), K, epi, ptr(stats), ptr(z), h, w, K,
-                 work=_conv_flops(N, H, W, K, 1, fin) + _conv_flops(N, h, w, K, 1, skin))
+                 work=_conv_flops(N, H, W, K, 1, fin))  # the z conv is its own launch
             return y
 
         outs, st = _cbe_fwd(fm, weight, bias, gamma, beta, w1, w2, spec, yconv=yconv)
