@@ -32,6 +32,11 @@ extern "C" {
 
 enum { UM_OK = 0, UM_ERR_ARG = 1, UM_ERR_HIP = 2 };
 enum { UM_F32 = 0, UM_BF16 = 1 };
+/* OR'ed into the dtype of the um_bn_elu_* entries (and um_conv2d_fwd_up2's): the pre-BN conv output y is stored in the activation
+ * dtype instead of f32 (the bf16 build's default, as a bf16 autocast conv
+ * feeding BatchNorm2d; statistics are still taken in f32 in the conv
+ * epilogue).  um_conv2d_fwd_up2: y and the low-resolution map up2. */
+enum { UM_Y_ACT = 0x100 };
 enum { UM_PAD_ZERO = 0, UM_PAD_REFLECT = 1 };
 enum {
   UM_EPI_NONE = 0,           /* y = acc (+ bias)                               */
@@ -92,7 +97,7 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
  * the upsample commute): the full-resolution concat is never built. */
 int um_conv2d_fwd_up2(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                       const void* wf, const float* bias, int K, int P, int Q, void* y, int ldy,
-                      int epilogue, float* stats, const float* up2, int up2_h, int up2_w,
+                      int epilogue, float* stats, const void* up2, int up2_h, int up2_w,
                       int up2_ld, hipStream_t stream);
 /* data gradient: dx[N,H,W,C] (= or +=) conv^T(dy[N,P,Q,K], wT) incl. the
  * reflect-pad fold and the stride-2 scatter */
@@ -163,6 +168,21 @@ int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C,
                    void* wf, void* wT, int ldT, hipStream_t stream);
 
 /* per-channel column sums of y[M][C] (pixel stride ld) -> partial rows [parts][C] */
+/* Several bias gradients (um_colsum + um_reduce_rows each) in two launches:
+ * the weight-gradient side stream batches the bias reductions of a flush
+ * (the attention's K/Q/V/reprojection and the disparity heads' conv biases,
+ * reference model/layers/attention.py:24-33, decoder.py:244-247).  descs:
+ * HOST array of n <= UM_CSUM_MAX entries (passed by value); out[c] =
+ * sum_m y[m][c] for c < creal, parts = a [nparts][C] f32 workspace with
+ * nparts = um_colsum_parts(M); one dtype for all entries. */
+#define UM_CSUM_MAX 24
+typedef struct {
+  const void* y;
+  float* parts;
+  float* out;
+  int M, C, ld, nparts, creal;
+} um_csum_desc;
+int um_colsum_batch(int dtype, const um_csum_desc* descs, int n, hipStream_t stream);
 int um_colsum_parts(int M);
 int um_colsum(int dtype, int M, int C, int ld, const void* y, float* partials,
               hipStream_t stream);
@@ -357,7 +377,8 @@ typedef struct {
 } um_cat_src;
 int um_concat_build(int dtype, int N, int H, int W, void* dst, int ld, int Ctot, int nsrc,
                     const um_cat_src* srcs, hipStream_t stream);
-/* dscale (+=) needs ws: um_concat_bwd_ws(N, src.h, src.w, src.C) floats */
+/* dscale (+=) needs ws: um_concat_bwd_ws(N, src.h, src.w, src.C) floats.
+ * accumulate: bit 0 = dsrc (+=), bit 1 = dscale written (=) instead of (+=) */
 long um_concat_bwd_ws(int N, int h, int w, int C);
 int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
                       const um_cat_src* src, void* dsrc, int ldd, int dsrc_dtype,

@@ -307,3 +307,47 @@ def test_fused_merge_matches_separate_merge(dtype):
         assert torch.equal(a, b)
     for k in g0:
         assert torch.equal(g1[k], g0[k]), k
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_grad_slots_match_autograd_sums(dtype):
+    """Fan-out input gradients accumulated into one shared buffer by the
+    registered consumers (umamd.functional.GradSlots) against autograd
+    summing each consumer's own gradient: same losses; gradients equal up to
+    the summation order of the fan-out sums (fp32 1e-5, bf16 5e-2 rel-norm on
+    the conv weights, as test_stage_fn_matches_per_node_autograd)."""
+    import train.utils as u
+    from train.loss import TukraUncertaintyLoss
+    from umamd import functional as U
+    from _parity import atol_of, pre_bn_bias
+    cfg = _cfg('config.yml')
+    cfg['loss']['error_loss_config']['loss_type'] = 'bayesian'
+    left, right = _uniform_pair(2, 64, 128, seed=9)
+    left, right = left.to(DEV), right.to(DEV)
+    pyr = u.scale_pyramid(torch.cat([left, right], 1), 4)
+    res = []
+    old = U._GRAD_SLOTS
+    try:
+        for flag in (True, False):
+            U._GRAD_SLOTS = flag
+            m = _model(cfg, dtype).train()
+            lf = TukraUncertaintyLoss(**cfg['loss'])
+            d = m(left, 0.3)
+            dl, el = lf(pyr, d, u.reconstruct_pyramid(d, pyr), 0, None)
+            (dl + el).backward()
+            torch.cuda.synchronize()
+            res.append((float(dl), float(el),
+                        {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+    finally:
+        U._GRAD_SLOTS = old
+    (dl1, el1, g1), (dl0, el0, g0) = res
+    assert dl1 == dl0 and el1 == el0
+    tol = 1e-5 if dtype == 'fp32' else 5e-2
+    for k in g0:
+        if pre_bn_bias(k) or (dtype == 'bf16' and not k.endswith('.weight')):
+            continue
+        d = float((g1[k] - g0[k]).norm())
+        # + the per-element floor of whole-map sums with heavy cancellation
+        # (merge weights: ~1e-5 true value, summation-order noise of the same size)
+        assert d <= tol * float(g0[k].norm()) + g0[k].numel() ** 0.5 * atol_of(k), \
+            (k, d, float(g0[k].norm()))

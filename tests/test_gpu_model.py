@@ -283,11 +283,17 @@ def test_batched_weight_pack_matches_per_site_pack(dtype):
         m(x, 0.3)
         assert pk.batched and not pk.dirty
         torch.cuda.synchronize()
-        checked = 0
-        for key, (f, t) in pk.entries.items():
+        checked = biases = 0
+        params = {p.data_ptr(): p for p in m.parameters()}
+        for key, e in pk.entries.items():
+            if key[0] == 'bias':  # the attention's fused QKV bias (f32, batch-refreshed)
+                assert torch.equal(e, torch.cat([params[q] for q in key[1]])), key
+                biases += 1
+                continue
             if key[0] != 'w':
                 continue
-            w = next(p for p in m.parameters() if p.data_ptr() == key[1])
+            f, t = e
+            w = params[key[1]]
             Cp, dt, ldT, segs = key[3], key[4], key[5], key[6]
             f2 = torch.empty_like(f) if f is not None else None
             t2 = torch.zeros_like(t) if t is not None else None
@@ -297,7 +303,7 @@ def test_batched_weight_pack_matches_per_site_pack(dtype):
             if t is not None:
                 assert torch.equal(t, t2), key
             checked += 1
-        assert checked >= 40
+        assert checked >= 40 and biases == 5
 
 
 def test_train_step_config1_l1():

@@ -72,13 +72,18 @@ HALO_CASES = [
 
 
 @pytest.mark.parametrize('case', HALO_CASES)
-def test_conv_bn_elu_halo(case):
+@pytest.mark.parametrize('pf2', [0, 1])
+def test_conv_bn_elu_halo(case, pf2):
+    """the halo kernel forced on; pf2: weight tap rows loaded two rows ahead
+    (knob halo_pf2), forward and data gradient"""
     from umamd._lib import lib
     old = lib().um_set_tuning(b'halo_min_tiles', 1)
+    old_p = lib().um_set_tuning(b'halo_pf2', pf2)
     try:
         test_conv_bn_elu(case, torch.bfloat16)
     finally:
         lib().um_set_tuning(b'halo_min_tiles', old)
+        lib().um_set_tuning(b'halo_pf2', old_p)
 
 
 @pytest.mark.parametrize('case', CONV_CASES)
@@ -430,6 +435,24 @@ def test_wgrad_reduce_batch_matches_per_conv(monkeypatch):
     torch.cuda.synchronize()
     for r, got in zip(refs, grads):
         assert torch.equal(r, got)
+
+
+# the side stream's batched bias gradients (um_colsum_batch: one partial-row
+# pass + one f64 finish per flush) against the per-bias reduction
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_colsum_batch_matches_per_bias(dtype):
+    from umamd import functional as U
+    from umamd import overlap
+    g = torch.Generator().manual_seed(11)
+    shapes = [(2, 64, 128, 32), (2, 16, 32, 768), (1, 8, 16, 1536), (2, 128, 256, 8),
+              (3, 5, 7, 64)] * 6
+    ys = [torch.randn(*sh, generator=g).to(dtype).to(DEV) for sh in shapes]
+    refs = [y.double().sum(dim=(0, 1, 2)).float() for y in ys]
+    with overlap.WgradStream(batch=len(ys)):
+        outs = [U._colsum_grad(y, y.shape[-1]) for y in ys]
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert torch.allclose(o, r, rtol=1e-5, atol=1e-4), float((o - r).abs().max())
 
 
 # x2 bilinear (align_corners=True) upsample of a concat source: forward and

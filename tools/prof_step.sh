@@ -11,4 +11,6 @@ trace=$(find gpurun_out/$OUT/prof -name '*kernel_trace.csv' | head -1)
 stats=$(find gpurun_out/$OUT/prof -name '*kernel_stats.csv' | head -1)
 cp $stats gpurun_out/$OUT/kernel_stats.csv
 python3 tools/step_stats.py $trace 200 > gpurun_out/$OUT/step_kernels.txt
+python3 tools/step_launches.py $trace > gpurun_out/$OUT/step_launches.txt 2>&1 || true
+python3 tools/trace_gaps.py $trace 25 > gpurun_out/$OUT/gaps.txt 2>&1 || true
 rm -f $trace

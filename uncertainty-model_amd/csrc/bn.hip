@@ -122,9 +122,9 @@ struct MergeOut {
 // few hundred blocks; wide layers keep one slice (cs = C).
 // MERGE: the fused-merge instance (its register footprint, ~200 VGPRs with
 // up to 8 sources, stays out of the plain instance's ~94)
-template <typename T, bool MERGE>
+template <typename T, bool MERGE, typename TY>
 __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
-    const float* __restrict__ y, int ldy, long M, int C, const float* __restrict__ scale,
+    const TY* __restrict__ y, int ldy, long M, int C, const float* __restrict__ scale,
     const float* __restrict__ shift, T* __restrict__ a, int lda, int apply_elu,
     int rows_per_block, float* __restrict__ pool, FwdFin fin, int cs, MergeOut mo) {
   extern __shared__ float red[];  // [256][8] when pooling, then [2][cs] coefficients (fin)
@@ -335,9 +335,9 @@ __device__ void bwd_finish(const float* __restrict__ parts, int nb, int C, const
 
 // Backward reduce: dz = (da + add[n][c]) * ELU'(z), z = y*scale + shift,
 // xhat = (y - mean) * invstd; partial sums per block [blk][C][2].
-template <typename T>
+template <typename T, typename TY>
 __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
-    const T* __restrict__ da, int ldda, const float* __restrict__ y, int ldy, long M, int C,
+    const T* __restrict__ da, int ldda, const TY* __restrict__ y, int ldy, long M, int C,
     long HW, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ add_nc, int apply_elu, float* __restrict__ parts,
@@ -476,9 +476,9 @@ __device__ __forceinline__ void apply_fin_coeffs(const ApplyFin& f, int C, int c
 
 // dy = k1*(dz - k2 - xhat*k3); optional per-block partial sums of dy
 // ([blk][C], the conv-bias gradient) written to sum_parts.
-template <typename T>
+template <typename T, typename TY>
 __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
-    const T* __restrict__ da, int ldda, const float* __restrict__ y, int ldy, long M, int C,
+    const T* __restrict__ da, int ldda, const TY* __restrict__ y, int ldy, long M, int C,
     long HW, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ add_nc, int apply_elu, const float* __restrict__ k1,
@@ -633,13 +633,18 @@ static int bn_fwd_launch(int dtype, long M, int C, const void* y, int ldy, const
   const dim3 g(ceil_div(M, rows), sl.ns);
   const size_t shm = (pool_parts ? 256 * 8 * sizeof(float) : 0) +
                      (fin.slots ? 2 * (size_t)sl.cs * sizeof(float) : 0);
-#define UM_BN_FWD(T_, MG_)                                                                     \
-  hipLaunchKernelGGL((bn_elu_fwd_kernel<T_, MG_>), g, dim3(256), shm, st, (const float*)y, ldy, M, \
-                     C, scale, shift, (T_*)a, lda, apply_elu, rows, pool_parts, fin, sl.cs, mo)
-  if (dtype == UM_BF16) {
-    if (mo.n) UM_BN_FWD(bf16_t, true); else UM_BN_FWD(bf16_t, false);
+  const bool yact = dtype & UM_Y_ACT;
+  dtype &= ~UM_Y_ACT;
+#define UM_BN_FWD(T_, MG_, TY_)                                                            \
+  hipLaunchKernelGGL((bn_elu_fwd_kernel<T_, MG_, TY_>), g, dim3(256), shm, st, (const TY_*)y, \
+                     ldy, M, C, scale, shift, (T_*)a, lda, apply_elu, rows, pool_parts, fin,   \
+                     sl.cs, mo)
+  if (dtype == UM_BF16 && yact) {
+    if (mo.n) UM_BN_FWD(bf16_t, true, bf16_t); else UM_BN_FWD(bf16_t, false, bf16_t);
+  } else if (dtype == UM_BF16) {
+    if (mo.n) UM_BN_FWD(bf16_t, true, float); else UM_BN_FWD(bf16_t, false, float);
   } else {
-    if (mo.n) UM_BN_FWD(float, true); else UM_BN_FWD(float, false);
+    if (mo.n) UM_BN_FWD(float, true, float); else UM_BN_FWD(float, false, float);
   }
 #undef UM_BN_FWD
   UM_LAUNCH_CHECK();
@@ -716,14 +721,14 @@ static int bwd_reduce_launch(int dtype, long M, int C, long HW, const void* da, 
   const int rows = sl.ns > 1 ? bwd_rows_c(M, C) : bn_bwd_rows(M);
   const dim3 blocks(ceil_div(M, rows), sl.ns);
   const size_t shm = 256 * 16 * sizeof(float);
-  if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<bf16_t>, blocks, dim3(256), shm, st,
-                       (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, rows, fin, slots, sl.cs);
-  else
-    hipLaunchKernelGGL(bn_elu_bwd_reduce_kernel<float>, blocks, dim3(256), shm, st,
-                       (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, parts, rows, fin, slots, sl.cs);
+#define UM_BN_RED(T_, TY_)                                                                   \
+  hipLaunchKernelGGL((bn_elu_bwd_reduce_kernel<T_, TY_>), blocks, dim3(256), shm, st,        \
+                     (const T_*)da, ldda, (const TY_*)y, ldy, M, C, HW, mean, invstd, scale, \
+                     shift, add_nc, apply_elu, parts, rows, fin, slots, sl.cs)
+  if (dtype == (UM_BF16 | UM_Y_ACT)) UM_BN_RED(bf16_t, bf16_t);
+  else if (dtype == UM_BF16) UM_BN_RED(bf16_t, float);
+  else UM_BN_RED(float, float);
+#undef UM_BN_RED
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -793,16 +798,15 @@ static int bwd_apply_launch(int dtype, long M, int C, long HW, const void* da, i
   const int rows = sl.ns > 1 ? bwd_rows_c(M, C) : bn_bwd_rows(M);
   const dim3 blocks(ceil_div(M, rows), sl.ns);
   const size_t shm = 256 * 8 * sizeof(float) + (fin.slots ? 3 * (size_t)sl.cs * sizeof(float) : 0);
-  if (dtype == UM_BF16)
-    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<bf16_t>, blocks, dim3(256), shm, st,
-                       (const bf16_t*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, k1, k2, k3, (bf16_t*)dy, lddy, sum_parts,
-                       rows, fin, sl.cs);
-  else
-    hipLaunchKernelGGL(bn_elu_bwd_apply_kernel<float>, blocks, dim3(256), shm, st,
-                       (const float*)da, ldda, (const float*)y, ldy, M, C, HW, mean, invstd,
-                       scale, shift, add_nc, apply_elu, k1, k2, k3, (float*)dy, lddy, sum_parts,
-                       rows, fin, sl.cs);
+#define UM_BN_APPLY(T_, TY_)                                                                 \
+  hipLaunchKernelGGL((bn_elu_bwd_apply_kernel<T_, TY_>), blocks, dim3(256), shm, st,         \
+                     (const T_*)da, ldda, (const TY_*)y, ldy, M, C, HW, mean, invstd, scale, \
+                     shift, add_nc, apply_elu, k1, k2, k3, (T_*)dy, lddy, sum_parts, rows, fin, \
+                     sl.cs)
+  if (dtype == (UM_BF16 | UM_Y_ACT)) UM_BN_APPLY(bf16_t, bf16_t);
+  else if (dtype == UM_BF16) UM_BN_APPLY(bf16_t, float);
+  else UM_BN_APPLY(float, float);
+#undef UM_BN_APPLY
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -614,6 +614,99 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ y, in
   }
 }
 
+// Several bias gradients (column sums) in two launches: the weight-gradient
+// side stream's flush batches them (umamd.functional._colsum_grad).  Phase 1:
+// descriptor d owns workgroups [first[d], first[d+1]), each one row chunk of
+// y -> its partial row parts[blk][C] (as colsum_kernel); phase 2: one
+// workgroup per (descriptor, 64 columns) sums the partial rows in f64.
+struct CsDesc {
+  const void* y;
+  float* parts;
+  float* out;
+  int M, C, ld, nparts, rows, creal;
+};
+struct CsBatch {
+  int n, dtype;
+  int first[UM_CSUM_MAX + 1];
+  CsDesc d[UM_CSUM_MAX];
+};
+
+#define CSEL(expr)                                          \
+  ({                                                        \
+    auto v_ = b.d[0].expr;                                  \
+    _Pragma("unroll") for (int j = 1; j < UM_CSUM_MAX; ++j) \
+      if (j == i) v_ = b.d[j].expr;                         \
+    v_;                                                     \
+  })
+
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_batch_kernel(CsBatch b) {
+  __shared__ float red[256 * 8];
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < UM_CSUM_MAX; ++j)
+    if (j < b.n && (int)blockIdx.x >= b.first[j]) i = j;
+  int f0 = 0;
+#pragma unroll
+  for (int j = 0; j < UM_CSUM_MAX; ++j)
+    if (j == i) f0 = b.first[j];
+  const T* __restrict__ y = reinterpret_cast<const T*>(CSEL(y));
+  float* __restrict__ parts = CSEL(parts);
+  const int M = CSEL(M), C = CSEL(C), ld = CSEL(ld), rows = CSEL(rows);
+  const int blk = blockIdx.x - f0;
+  const int cg = C / 8;
+  const RowMap rm(cg);
+  const long m0 = (long)blk * rows;
+  const long m1 = min((long)M, m0 + rows);
+  for (int g0 = 0; g0 < cg; g0 += rm.G) {
+    const int g = g0 + rm.g;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (rm.active() && g < cg)
+      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+        float v[8];
+        load8(y + m * ld + g * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+    lane_reduce<8>(red, rm, acc);
+    if (rm.lane == 0 && g < cg) store8(parts + (long)blk * C + g * 8, acc);
+  }
+}
+
+// grid (descriptors, column chunks of 32): 32 columns x 8 row lanes, each
+// lane with 4 independent f64 accumulators (the partial rows are up to ~2k
+// deep: one dependent load chain per lane was 42 us per launch)
+__global__ void __launch_bounds__(256) colsum_fin_batch_kernel(CsBatch b) {
+  const int i = blockIdx.x;
+  if (i >= b.n) return;
+  const float* __restrict__ parts = CSEL(parts);
+  float* __restrict__ out = CSEL(out);
+  const int C = CSEL(C), np = CSEL(nparts), creal = CSEL(creal);
+  __shared__ double red[8][32];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c = blockIdx.y * 32 + cl;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (c < C) {
+    int r = rl;
+    for (; r + 24 < np; r += 32) {
+      s0 += parts[(long)r * C + c];
+      s1 += parts[(long)(r + 8) * C + c];
+      s2 += parts[(long)(r + 16) * C + c];
+      s3 += parts[(long)(r + 24) * C + c];
+    }
+    for (; r < np; r += 8) s0 += parts[(long)r * C + c];
+  }
+  red[rl][cl] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (rl == 0 && c < creal) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][cl];
+    out[c] = (float)t;
+  }
+}
+#undef CSEL
+
 // out[c] (+)= sum_r p[r*stride + c]: block = cl channel lanes (cl = C up to
 // 64, power of two) x 256/cl row lanes, 8 independent accumulators per
 // thread, f64 lane combine
@@ -713,8 +806,7 @@ static int conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void
                       const void* wf, const float* bias, int K, int R, int stride, int pad,
                       int pad_mode, int P, int Q, int ydtype, void* y, int ldy, int epilogue,
                       float epi_scale, const void* residual, int ldr, float* stats, void* ws,
-                      long ws_bytes, const float* up2, int up2_h, int up2_w, int up2_ld,
-                      hipStream_t st);
+                      long ws_bytes, int accumulate, hipStream_t st);
 
 int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x, const void* wf,
                   const float* bias, int K, int R, int stride, int pad, int pad_mode, int P,
@@ -722,30 +814,41 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                   const void* residual, int ldr, float* stats, void* ws, long ws_bytes,
                   hipStream_t st) {
   return conv2d_fwd(dtype, N, H, W, C, ldx, x, wf, bias, K, R, stride, pad, pad_mode, P, Q, ydtype,
-                    y, ldy, epilogue, epi_scale, residual, ldr, stats, ws, ws_bytes, nullptr, 0, 0,
-                    0, st);
+                    y, ldy, epilogue, epi_scale, residual, ldr, stats, ws, ws_bytes, 0, st);
 }
 
 int um_conv2d_fwd_up2(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                       const void* wf, const float* bias, int K, int P, int Q, void* y, int ldy,
-                      int epilogue, float* stats, const float* up2, int up2_h, int up2_w,
+                      int epilogue, float* stats, const void* up2, int up2_h, int up2_w,
                       int up2_ld, hipStream_t st) {
+  // UM_Y_ACT: y and up2 in the activation dtype, else f32
+  const int ydt = (dtype & UM_Y_ACT) ? (dtype & ~UM_Y_ACT) : UM_F32;
+  dtype &= ~UM_Y_ACT;
   UM_CHECK_ARG(up2 != nullptr && up2_h >= 1 && up2_w >= 1 && up2_ld >= K,
                "um_conv2d_fwd_up2: low-resolution map");
   UM_CHECK_ARG(epilogue == UM_EPI_NONE || epilogue == UM_EPI_STATS ||
                    epilogue == UM_EPI_STAT_SLOTS,
                "um_conv2d_fwd_up2: epilogue");
-  return conv2d_fwd(dtype, N, H, W, C, ldx, x, wf, bias, K, 1, 1, 0, UM_PAD_ZERO, P, Q, UM_F32, y,
-                    ldy, epilogue, 1.f, nullptr, 0, stats, nullptr, 0, up2, up2_h, up2_w, up2_ld,
-                    st);
+  UM_CHECK_ARG(K % 8 == 0 && ldy % 8 == 0 && up2_ld % 8 == 0 && P == H && Q == W,
+               "um_conv2d_fwd_up2: K / strides must be multiples of 8, 1x1 same-size conv");
+  // y = up2(z) by one vectorised upsample pass (the concat kernel with one
+  // UP2 source), then the GEMM ADDS W x + bias into y, with the BN
+  // statistics taken on the sum in its epilogue (an in-epilogue gather of the
+  // 4 taps per element measured 142 us for the 256x512 stage vs ~60 here)
+  um_cat_src src{};
+  src.ptr = up2; src.scale = nullptr; src.C = K; src.ld = up2_ld; src.op = UM_CAT_UP2;
+  src.coff = 0; src.dtype = ydt; src.h = up2_h; src.w = up2_w;
+  const int rc = um_concat_build(ydt, N, H, W, y, ldy, K, 1, &src, st);
+  if (rc != UM_OK) return rc;
+  return conv2d_fwd(dtype, N, H, W, C, ldx, x, wf, bias, K, 1, 1, 0, UM_PAD_ZERO, P, Q, ydt, y,
+                    ldy, epilogue, 1.f, nullptr, 0, stats, nullptr, 0, 1, st);
 }
 
 static int conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                       const void* wf, const float* bias, int K, int R, int stride, int pad,
                       int pad_mode, int P, int Q, int ydtype, void* y, int ldy, int epilogue,
                       float epi_scale, const void* residual, int ldr, float* stats, void* ws,
-                      long ws_bytes, const float* up2, int up2_h, int up2_w, int up2_ld,
-                      hipStream_t st) {
+                      long ws_bytes, int accumulate, hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0 && ldx % 8 == 0, "um_conv2d_fwd: C (%d) and ldx (%d) must be multiples of 8", C, ldx);
   UM_CHECK_ARG(stride == 1 || stride == 2, "um_conv2d_fwd: stride %d", stride);
   UM_CHECK_ARG(P == (H + 2 * pad - R) / stride + 1 && Q == (W + 2 * pad - R) / stride + 1,
@@ -767,9 +870,8 @@ static int conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void
   a.bias = bias; a.out = y; a.ld_out = ldy; a.out_f32 = (ydtype == UM_F32);
   a.epilogue = epilogue == UM_EPI_STAT_SLOTS ? UM_EPI_STATS : epilogue;
   a.stat_slots = epilogue == UM_EPI_STAT_SLOTS;
-  a.accumulate = 0; a.epi_scale = epi_scale;
+  a.accumulate = accumulate; a.epi_scale = epi_scale;
   a.residual = residual; a.ldr = ldr; a.stats = stats;
-  a.up2 = up2; a.up2_h = up2_h; a.up2_w = up2_w; a.up2_ld = up2_ld;
   return umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
 }
 
@@ -1057,6 +1159,36 @@ int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C, vo
                    int ldT, hipStream_t st) {
   return um_pack_weight_seg(dtype, w, K, Creal, R, C, wf, wT, ldT, 0, nullptr, nullptr, nullptr,
                             st);
+}
+
+int um_colsum_batch(int dtype, const um_csum_desc* descs, int n, hipStream_t st) {
+  UM_CHECK_ARG(descs != nullptr && n >= 0 && n <= UM_CSUM_MAX, "um_colsum_batch: n");
+  if (n == 0) return UM_OK;
+  CsBatch b{};
+  b.n = n;
+  b.dtype = dtype;
+  int blocks = 0, maxc = 0;
+  for (int i = 0; i < n; ++i) {
+    const um_csum_desc& e = descs[i];
+    UM_CHECK_ARG(e.y && e.parts && e.out && e.M > 0 && e.C % 8 == 0 && e.ld % 8 == 0 &&
+                     e.creal <= e.C && e.nparts == parts_for(e.M),
+                 "um_colsum_batch: descriptor %d", i);
+    CsDesc& d = b.d[i];
+    d.y = e.y; d.parts = e.parts; d.out = e.out;
+    d.M = e.M; d.C = e.C; d.ld = e.ld; d.nparts = e.nparts; d.rows = rows_per_part(e.M);
+    d.creal = e.creal;
+    b.first[i] = blocks;
+    blocks += e.nparts;
+    maxc = std::max(maxc, e.C);
+  }
+  b.first[n] = blocks;
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL(colsum_batch_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, b);
+  else
+    hipLaunchKernelGGL(colsum_batch_kernel<float>, dim3(blocks), dim3(256), 0, st, b);
+  hipLaunchKernelGGL(colsum_fin_batch_kernel, dim3(n, ceil_div(maxc, 32)), dim3(256), 0, st, b);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
 }
 
 int um_colsum_parts(int M) { return parts_for(M); }

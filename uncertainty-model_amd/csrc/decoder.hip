@@ -621,10 +621,11 @@ __global__ void __launch_bounds__(256) se_wgrad_kernel(int N, int C, int R, cons
   }
 }
 
-// dscale[n][c] += sum_b parts[n][b][c]: block = (cl channels) x (256/cl
+// dscale[n][c] (+)= sum_b parts[n][b][c]: block = (cl channels) x (256/cl
 // b-lanes), grid (ceil(C/cl), N)
 __global__ void __launch_bounds__(256) parts_accum_kernel(const float* __restrict__ parts, int B,
-                                                          int C, float* __restrict__ out, int cl) {
+                                                          int C, float* __restrict__ out, int cl,
+                                                          int store) {
   __shared__ float red[256];
   const int lanes = 256 / cl;
   const int n = blockIdx.y;
@@ -645,7 +646,7 @@ __global__ void __launch_bounds__(256) parts_accum_kernel(const float* __restric
   __syncthreads();
   if (lane == 0 && c < C) {
     for (int q = 1; q < lanes; ++q) t += red[q * cl + (threadIdx.x % cl)];
-    out[n * C + c] += t;
+    out[n * C + c] = store ? t : out[n * C + c] + t;
   }
 }
 
@@ -728,6 +729,10 @@ long um_concat_bwd_ws(int N, int h, int w, int C) {
 int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
                       const um_cat_src* src, void* dsrc, int ldd, int dsrc_dtype, int accumulate,
                       float* dscale, float* ws, hipStream_t st) {
+  // accumulate bit 0: dsrc (+=); bit 1: dscale is WRITTEN (=) instead of added
+  // to (no zero fill of the gate gradient beforehand)
+  const int store_scale = (accumulate >> 1) & 1;
+  accumulate &= 1;
   const um_cat_src& s0 = *src;
   CatSrc s{s0.ptr, s0.scale, s0.C, s0.ld, s0.op, s0.coff, s0.dtype, s0.h, s0.w};
   UM_CHECK_ARG(ldg % 8 == 0, "um_concat_bwd_src: ldg %% 8");
@@ -788,7 +793,7 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
     int cl = 1;
     while (cl < s.C && cl < 64) cl <<= 1;
     hipLaunchKernelGGL(parts_accum_kernel, dim3(ceil_div(s.C, cl), N), dim3(256), 0, st, parts,
-                       nblk, s.C, dscale, cl);
+                       nblk, s.C, dscale, cl, store_scale);
   }
   UM_LAUNCH_CHECK();
   return UM_OK;

@@ -26,6 +26,8 @@
 // Replaces nn.Conv2d forward / input-gradient of reference
 // model/layers/encoder.py:36-42 (7x7, 5x5, 3x3 zero padded) and
 // model/layers/decoder.py:30-52 (3x3 reflection padded, forward).
+#include <cstdlib>
+
 #include "common.h"
 #include "halo_conv.h"
 
@@ -43,7 +45,10 @@ constexpr int TH = 8, TW = 32, CK = 32;
 // chunk ^ ((p >> 2) & 3) was 2-way in every group: SQ_LDS_BANK_CONFLICT 0.4)
 __device__ __forceinline__ int himg(int p, int c) { return p * CK + ((c ^ ((p >> 1) & 2)) << 3); }
 
-template <int R, int BN, bool FLIP, bool REFLECT>
+// PF2: weight tap rows are loaded two rows ahead into two register sets
+// (rows r+1 and r+2 in flight while row r computes) instead of one: a tap
+// row of MFMAs (~0.4-0.8 us) is shorter than an L2 round trip under load
+template <int R, int BN, bool FLIP, bool REFLECT, bool PF2>
 __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, int tiles_y) {
   constexpr int HH = TH + R - 1, HWd = TW + R - 1, HP = HH * HWd;
   constexpr int PIECES = HP * 4;                 // 16-byte pieces per chunk
@@ -104,32 +109,34 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
   // weight tap row r of chunk c0 -> registers: piece i = (s, n, c) of tap (r, s),
   // output channel bn + n, reduction channels c0 + 8c .. + 8
   const int ncol = lane & 15, kq = lane >> 4;
-  uint4 wv[NW];
-  auto load_wrow = [&](int r, int c0) {
+  uint4 wv[NW], wv2[NW];
+  auto load_wset = [&](uint4 (&w)[NW], int r, int c0) {
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
       const int i = tid + k * 256;
-      wv[k] = make_uint4(0, 0, 0, 0);
+      w[k] = make_uint4(0, 0, 0, 0);
       if (i < WP) {
         const int c = i & 3, nn = (i >> 2) % BN, ss = (i >> 2) / BN;
         const int n = bn + nn, ch = c0 + c * 8;
         const int tap = r * R + ss;
         const int btap = FLIP ? RR - 1 - tap : tap;
         if (n < a.NC && ch < a.ach)
-          wv[k] = *reinterpret_cast<const uint4*>(wsrc + (long)n * a.ldb + (long)btap * a.ach + ch);
+          w[k] = *reinterpret_cast<const uint4*>(wsrc + (long)n * a.ldb + (long)btap * a.ach + ch);
       }
     }
   };
-  auto store_wrow = [&](int buf) {
+  auto store_wset = [&](const uint4 (&w)[NW], int buf) {
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
       const int i = tid + k * 256;
       if (i < WP) {
         const int c = i & 3, row = i >> 2;  // row = ss * BN + nn
-        *reinterpret_cast<uint4*>(&sW[buf][himg(row, c)]) = wv[k];
+        *reinterpret_cast<uint4*>(&sW[buf][himg(row, c)]) = w[k];
       }
     }
   };
+  auto load_wrow = [&](int r, int c0) { load_wset(wv, r, c0); };
+  auto store_wrow = [&](int buf) { store_wset(wv, buf); };
   bool nok[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) nok[j] = bn + j * 16 + ncol < a.NC;
@@ -146,7 +153,51 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
   for (int i = 0; i < TM; ++i) pbase[i] = (2 * wave + (i >> 1)) * HWd + (i & 1) * 16 + ncol;
 
   const int nchunk = (a.ach + CK - 1) / CK;
+  // the R taps of tap row r from LDS weight buffer buf
+  auto taps = [&](int r, int buf) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8_t*>(&sH[himg(pbase[i] + r * HWd + s, kq)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8_t*>(&sW[buf][himg(s * BN + j * 16 + ncol, kq)]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
   load_halo(0);
+  if constexpr (PF2) {
+    for (int ch = 0; ch < nchunk; ++ch) {
+      const int c0 = ch * CK;
+      load_wset(wv, 0, c0);
+      if (R > 1) load_wset(wv2, 1, c0);
+      __syncthreads();  // the previous chunk's fragment reads are done
+      store_halo();
+      if (ch + 1 < nchunk) load_halo(c0 + CK);
+      store_wset(wv, 0);
+      __syncthreads();
+      // row r: set `nxt` holds row r+1 (loaded a row ago), `fre` is free and
+      // takes row r+2; the sets alternate, so the pair loop keeps every
+      // register-array index static
+      auto row = [&](int r, uint4 (&nxt)[NW], uint4 (&fre)[NW]) {
+        if (r + 2 < R) load_wset(fre, r + 2, c0);
+        taps(r, r & 1);
+        if (r + 1 < R) store_wset(nxt, (r + 1) & 1);  // that buffer was last read in row r-1
+        __syncthreads();
+      };
+#pragma unroll 1
+      for (int r = 0; r < R; r += 2) {
+        row(r, wv2, wv);
+        if (r + 1 < R) row(r + 1, wv, wv2);
+      }
+    }
+  } else
   for (int ch = 0; ch < nchunk; ++ch) {
     const int c0 = ch * CK;
     __syncthreads();  // the previous chunk's fragment reads are done
@@ -160,21 +211,7 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
     for (int r = 0; r < R; ++r) {
       const int buf = r & 1;
       if (r + 1 < R) load_wrow(r + 1, c0);
-#pragma unroll
-      for (int s = 0; s < R; ++s) {
-        bf16x8_t fa[TM], fb[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          fa[i] = *reinterpret_cast<const bf16x8_t*>(&sH[himg(pbase[i] + r * HWd + s, kq)]);
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fb[j] = *reinterpret_cast<const bf16x8_t*>(&sW[buf][himg(s * BN + j * 16 + ncol, kq)]);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      }
+      taps(r, buf);
       if (r + 1 < R) store_wrow(buf ^ 1);  // that buffer was last read in row r-1
       __syncthreads();
     }
@@ -258,19 +295,32 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
   }
 }
 
+template <int R, int BN, bool PF2>
+void launch_rp(const IgArgs& a, dim3 grid, int tiles_x, int tiles_y, hipStream_t st) {
+  if (a.flip)
+    hipLaunchKernelGGL((halo_conv_kernel<R, BN, true, false, PF2>), grid, dim3(256), 0, st, a,
+                       tiles_x, tiles_y);
+  else if (a.pmode == umamd::IG_PAD_REFLECT)
+    hipLaunchKernelGGL((halo_conv_kernel<R, BN, false, true, PF2>), grid, dim3(256), 0, st, a,
+                       tiles_x, tiles_y);
+  else
+    hipLaunchKernelGGL((halo_conv_kernel<R, BN, false, false, PF2>), grid, dim3(256), 0, st, a,
+                       tiles_x, tiles_y);
+}
+
 template <int R, int BN>
 int launch_r(const IgArgs& a, hipStream_t st) {
   const int tiles_x = (a.ow + TW - 1) / TW, tiles_y = (a.oh + TH - 1) / TH;
   dim3 grid(a.on * tiles_y * tiles_x, (a.NC + BN - 1) / BN);
-  if (a.flip)
-    hipLaunchKernelGGL((halo_conv_kernel<R, BN, true, false>), grid, dim3(256), 0, st, a, tiles_x,
-                       tiles_y);
-  else if (a.pmode == umamd::IG_PAD_REFLECT)
-    hipLaunchKernelGGL((halo_conv_kernel<R, BN, false, true>), grid, dim3(256), 0, st, a, tiles_x,
-                       tiles_y);
-  else
-    hipLaunchKernelGGL((halo_conv_kernel<R, BN, false, false>), grid, dim3(256), 0, st, a,
-                       tiles_x, tiles_y);
+  // PF2 only where the second register set keeps the instance <= 256 VGPRs
+  // (2 waves per SIMD): BN 16/32, and BN 64 at R = 3 (R = 5, 7 at BN 64 would
+  // reach 270-320 VGPRs and one wave per SIMD)
+  if constexpr (BN <= 32 || (R == 3 && BN <= 64)) {
+    if (umamd::igemm_halo_pf2()) launch_rp<R, BN, true>(a, grid, tiles_x, tiles_y, st);
+    else launch_rp<R, BN, false>(a, grid, tiles_x, tiles_y, st);
+  } else {
+    launch_rp<R, BN, false>(a, grid, tiles_x, tiles_y, st);
+  }
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -44,11 +44,6 @@ struct IgArgs {
   int stat_slots;   // UM_EPI_STAT_SLOTS: stats is double[UM_STAT_SLOTS][NC][2]
   int colmajor;     // tile order, set by igemm_run (knob xcd_col)
   int tappack;      // 4 taps x 8 channels per k-step (ach == 8), set by igemm_run
-  // optional: v += bilinear x2 (align_corners=True) of a low-resolution f32
-  // map [on][up2_h][up2_w][up2_ld] at output pixel (n, oy, ox), channel col,
-  // before the BN statistics (plain row mode, no split-K)
-  const float* up2;
-  int up2_h, up2_w, up2_ld;
 };
 
 // rows per BN partial-statistics row of a stats epilogue (M, NC of the GEMM)
@@ -72,6 +67,9 @@ bool igemm_halo_dgrad(int dtype, int N, int H, int W, int C, int R);
 // reflect data gradients in the padded form (knob pad_dgrad): 0 off, 1 for
 // dx wider than fold_split_nc, 2 all
 int igemm_pad_dgrad();
+
+// halo conv weight rows two rows ahead (knob "halo_pf2", UMAMD_HALO_PF2)
+int igemm_halo_pf2();
 
 // fill the border-list fields of a (oh, ow, fold_pad set) and return the
 // number of listed pixels per image

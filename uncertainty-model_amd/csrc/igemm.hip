@@ -138,7 +138,7 @@ __device__ __forceinline__ void border_pixel(const IgArgs& a, int m, int& n, int
     if (j < a.nrr && pick4(a.rr, j) <= y) ++y;
 }
 
-// MODE: 0 plain rows, 3 plain rows + the up2 add (IgArgs::up2), 1 parity class rows (stride-2 data gradient), 2 the
+// MODE: 0 plain rows, 1 parity class rows (stride-2 data gradient), 2 the
 // border list of the reflect fold (IgArgs::border)
 template <int MODE>
 __device__ __forceinline__ ARow decode_row(const IgArgs& a, int m) {
@@ -228,45 +228,6 @@ __device__ __forceinline__ void gather(const IgArgs& a, const T* __restrict__ sr
   to_raw(v, out);
 }
 
-// bilinear x2 (align_corners=True, torch upsample_bilinear2d) of the f32 map
-// a.up2 at output row m (plain rows), channel n: the decoder's skip half of a
-// 1x1 conv, computed at the skip's resolution (conv1x1 and the upsample
-// commute) and added here (umamd.functional.skip_conv_bn_elu)
-__device__ __forceinline__ void up2_tap(int i, int in, int out, int& i0, int& i1, float& l1) {
-  const float sc = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
-  const float src = sc * (float)i;
-  i0 = (int)src;
-  if (i0 > in - 1) i0 = in - 1;
-  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
-  l1 = src - (float)i0;
-}
-struct Up2Row {
-  const float *r0, *r1;  // rows y0, y1 of the low-resolution map
-  int x0, x1;            // element offsets of columns x0, x1 (times up2_ld)
-  float ly, lx;
-};
-__device__ __forceinline__ Up2Row up2_row(const IgArgs& a, int m) {
-  const int hw = a.oh * a.ow;
-  const int b = m / hw, rem = m - b * hw;
-  const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
-  int y0, y1, x0, x1;
-  Up2Row u;
-  up2_tap(oy, a.up2_h, a.oh, y0, y1, u.ly);
-  up2_tap(ox, a.up2_w, a.ow, x0, x1, u.lx);
-  const float* p = a.up2 + (long)b * a.up2_h * a.up2_w * a.up2_ld;
-  u.r0 = p + (long)y0 * a.up2_w * a.up2_ld;
-  u.r1 = p + (long)y1 * a.up2_w * a.up2_ld;
-  u.x0 = x0 * a.up2_ld;
-  u.x1 = x1 * a.up2_ld;
-  return u;
-}
-__device__ __forceinline__ float up2_val(const Up2Row& u, int n) {
-  const float v00 = u.r0[u.x0 + n], v01 = u.r0[u.x1 + n];
-  const float v10 = u.r1[u.x0 + n], v11 = u.r1[u.x1 + n];
-  return (1.f - u.ly) * ((1.f - u.lx) * v00 + u.lx * v01) +
-         u.ly * ((1.f - u.lx) * v10 + u.lx * v11);
-}
-
 // Epilogue shared by the register-staged and the LDS-DMA main loops: split-K
 // partial tile, or bias / residual / sigmoid-scale / stores and the BN
 // partial statistics (sStat: WM x BN x 2 floats of LDS).
@@ -306,7 +267,6 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
   float csum[TN], csq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
-  if constexpr (MODE != 3) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = bn + wn * (BN / WN) + j * 16 + col_l;
@@ -337,51 +297,6 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
         csum[j] += v;
         csq[j] += v * v;
       }
-  }
-  } else {
-  // MODE 3 (plain rows + the up2 add): rows outer, columns inner, so the
-  // row's output offset and up2 taps are derived once per row; each
-  // column's sums still run over the rows in the same order
-  float bv[TN];
-  int ncol[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    ncol[j] = bn + wn * (BN / WN) + j * 16 + col_l;
-    bv[j] = (a.bias != nullptr && ncol[j] < a.NC) ? a.bias[ncol[j]] : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
-      if (m >= a.M) continue;
-      const long orow = out_row<MODE>(a, m);
-      const Up2Row ur = up2_row(a, m);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = ncol[j];
-        if (n >= a.NC) continue;
-        float v = acc[i][j][q] + bv[j];
-        v += up2_val(ur, n);
-        const long off = orow + n;
-        if (a.epilogue == UM_EPI_RESIDUAL)
-          v += to_f32(reinterpret_cast<const T*>(a.residual)[(long)m * a.ldr + n]);
-        if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
-        if (a.out_f32) {
-          float* o = reinterpret_cast<float*>(a.out) + off;
-          if (a.accumulate) v += *o;
-          *o = v;
-        } else if (staged) {  // accumulate (if any) happens at the row store
-          sOut[(m - bm) * BN + (n - bn)] = from_f32<T>(v);
-        } else {
-          T* o = reinterpret_cast<T*>(a.out) + off;
-          if (a.accumulate) v += to_f32(*o);
-          *o = from_f32<T>(v);
-        }
-        csum[j] += v;
-        csq[j] += v * v;
-      }
-    }
   }
   if (a.epilogue == UM_EPI_STATS) {
 #pragma unroll
@@ -950,6 +865,7 @@ struct Knobs {
   int pad_dgrad;
   int fold_split_nc;
   int halo_max_nc;
+  int halo_pf2;
   Knobs() {
     auto env = [](const char* n, int d) {
       const char* v = getenv(n);
@@ -1006,6 +922,8 @@ struct Knobs {
     // C32 K8 125 -> 85; one pass stays ahead from C = 128 up (16x32 C640:
     // 106 vs 140, 8x16 C512: 53 vs 79)
     fold_split_nc = env("UMAMD_FOLD_SPLIT_NC", 64);
+    // halo conv: weight tap rows loaded two rows ahead (halo_conv.hip PF2)
+    halo_pf2 = env("UMAMD_HALO_PF2", 0);
   }
 };
 Knobs& knobs() {
@@ -1082,7 +1000,7 @@ void split_plan(Plan& p, int M, int NC, int taps, int ach, long ws_bytes, bool g
 template <typename T, int BK, int BM, int BN, int WM, int WN, int MODE>
 int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
   const int ntm = ceil_div(a.M, BM), ntn = ceil_div(a.NC, BN);
-  if constexpr (sizeof(T) == 2 && BK == 64 && WM == 2 && WN == 2 && MODE != 2 && MODE != 3) {
+  if constexpr (sizeof(T) == 2 && BK == 64 && WM == 2 && WN == 2 && MODE != 2) {
     if (a.pmode != umamd::IG_FOLD && (knobs().glds & (BM == 64 ? 1 : 2))) {
       const bool w8 = BM == 64 && (knobs().glds & 4);
       const long blocks = (long)ntm * ntn * p.splits;
@@ -1130,8 +1048,6 @@ int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
 
 template <typename T, int BK, int BM, int BN, int WM, int WN>
 int launch(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
-  if (a.up2 != nullptr)  // plain rows + the up2 add (register main loop, no split)
-    return launch_cls<T, BK, BM, BN, WM, WN, 3>(a, p, ws, st);
   return a.cls ? launch_cls<T, BK, BM, BN, WM, WN, 1>(a, p, ws, st)
                : launch_cls<T, BK, BM, BN, WM, WN, 0>(a, p, ws, st);
 }
@@ -1177,6 +1093,7 @@ bool igemm_halo_dgrad(int dtype, int N, int H, int W, int C, int R) {
   return (long)N * (H / 8) * (W / 32) >= k.halo_min_tiles;
 }
 int igemm_pad_dgrad() { return knobs().pad_dgrad; }
+int igemm_halo_pf2() { return knobs().halo_pf2; }
 
 int igemm_border_list(IgArgs& a) {
   const int H = a.oh, W = a.ow, p = a.fold_pad;
@@ -1201,10 +1118,6 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   if (a_in.M == 0) return UM_OK;
   IgArgs a = a_in;
   a.stats_rows = igemm_stats_rows(a.M, a.NC);
-  if (a.up2 != nullptr) {  // the up2 add lives in the one-pass epilogue only
-    ws = nullptr;
-    ws_bytes = 0;
-  }
   {
     // column-major tile order when B (NC x taps x ach) is larger than the
     // gathered image A (M x ach): knob xcd_col 0 = never, 1 = auto, 2 = always
@@ -1303,6 +1216,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "glds_deep_blocks")) f = &k.glds_deep_blocks;
   else if (!strcmp(key, "fold_split_nc")) f = &k.fold_split_nc;
   else if (!strcmp(key, "halo_max_nc")) f = &k.halo_max_nc;
+  else if (!strcmp(key, "halo_pf2")) f = &k.halo_pf2;
   if (!f) return -1;
   const int old = *f;
   *f = value;

@@ -33,7 +33,7 @@ class RandomlyConnectedModel(nn.Module):
         if h % 32 or w % 32:
             raise ValueError(f'image size {h}x{w}: height and width must be multiples of 32')
         x = U.image_to_nhwc(image, self.compute_dtype)
-        with P.scope(self._packer), U.stat_scope(self._stats, x.device):
+        with P.scope(self._packer), U.stat_scope(self._stats, x.device), U.grad_slots():
             feats = self.encoder._fwd(x)
             disps = self.decoder._fwd(x, *feats, scale=float(scale))
         disps = tuple(d.permute(0, 3, 1, 2) for d in disps)  # logical NCHW, NHWC memory

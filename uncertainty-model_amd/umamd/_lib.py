@@ -15,6 +15,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libumamd.so')
 
 UM_F32, UM_BF16 = 0, 1
+# OR'ed into the dtype of the um_bn_elu_* entries / um_conv2d_fwd_up2: the
+# pre-BN y is stored in the activation dtype (include/umamd.h)
+Y_ACT = 0x100
 PAD_ZERO, PAD_REFLECT = 0, 1
 EPI_NONE, EPI_STATS, EPI_SIGMOID_SCALE, EPI_RESIDUAL, EPI_STAT_SLOTS = 0, 1, 2, 3, 4
 STAT_SLOTS = 16  # UM_STAT_SLOTS (include/umamd.h)
@@ -43,6 +46,13 @@ class WredDesc(ctypes.Structure):
 
 
 MWG_MAX, MWG_SRC = 24, 8  # UM_MWG_MAX, UM_MWG_SRC
+CSUM_MAX = 24  # UM_CSUM_MAX
+
+
+class CsumDesc(ctypes.Structure):
+    """um_csum_desc: one bias gradient (column sum) of um_colsum_batch"""
+    _fields_ = [('y', _P), ('parts', _P), ('out', _P), ('M', _I), ('C', _I), ('ld', _I),
+                ('nparts', _I), ('creal', _I)]
 
 
 class MwgDesc(ctypes.Structure):
@@ -78,6 +88,7 @@ _SIG = {
     'um_conv_wgrad_reduce_seg': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, 's']),
     'um_conv_wgrad_reduce_batch': (_I, [_P, _I, 's']),
     'um_colsum_parts': (_I, [_I]),
+    'um_colsum_batch': (_I, [_I, _P, _I, 's']),
     'um_colsum': (_I, [_I, _I, _I, _I, _P, _P, 's']),
     'um_reduce_rows': (_I, [_P, _I, _I, _I, _P, _I, _P, 's']),
     'um_colred_ws': (_L, [_I, _I, _I]),

@@ -178,6 +178,13 @@ def batched_launch(descs):
             chunk = ds[i:i + cap]
             arr = (kind * len(chunk))(*chunk)
             call(name, _ct.cast(arr, ctypes_p), len(chunk))
+    cs = [d for d in descs if isinstance(d, _Csum)]
+    for dt in sorted({d.dtype for d in cs}):
+        ds = [d.desc for d in cs if d.dtype == dt]
+        for i in range(0, len(ds), L.CSUM_MAX):
+            chunk = ds[i:i + L.CSUM_MAX]
+            arr = (L.CsumDesc * len(chunk))(*chunk)
+            call('um_colsum_batch', dt, _ct.cast(arr, ctypes_p), len(chunk))
 
 
 def _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw_ptr, segs):
@@ -239,10 +246,33 @@ def _param_grad(tensors, out, launch):
     return out
 
 
+class _Csum:
+    """a queued bias gradient for um_colsum_batch (descriptor + dtype)"""
+    __slots__ = ('desc', 'dtype')
+
+    def __init__(self, desc, dtype):
+        self.desc, self.dtype = desc, dtype
+
+
+# the side stream's bias gradients as one um_colsum_batch (two launches) per
+# flush instead of um_colsum + um_reduce_rows per bias
+_CSUM_BATCH = os.environ.get('UMAMD_CSUM_BATCH', '1') == '1'
+
+
 def _colsum_grad(y, C):
     """a bias gradient (sum over pixels of y[..., :C]) as _param_grad"""
     out = torch.empty((C,), dtype=torch.float32, device=y.device)
     optr = ptr(out)
+    if _CSUM_BATCH and _overlap.active() is not None and C % 8 == 0 and y.shape[-1] % 8 == 0:
+        M = y.numel() // y.shape[-1]
+        nparts = query('um_colsum_parts', M)
+        parts = torch.empty((nparts, C), dtype=torch.float32, device=y.device)
+        d = L.CsumDesc()
+        d.y, d.parts, d.out = y.data_ptr(), parts.data_ptr(), optr
+        d.M, d.C, d.ld, d.nparts, d.creal = M, C, y.shape[-1], nparts, C
+        # parts is allocated on the launch stream: listed with y so the flush
+        # marks it used by the side stream (record_stream) before it is freed
+        return _param_grad((y, parts), out, lambda d=_Csum(d, _dt(y)), keep=parts: (keep, d))
     return _param_grad((y,), out, lambda: _colsum_into(y, C, optr))
 
 
@@ -259,6 +289,22 @@ _FUSED_SE = os.environ.get('UMAMD_FUSED_SE', '1') == '1'
 #  - single-process BN statistics as f64 atomics into zeroed slots, finished
 #    by the consumer kernels (no reduction launch per BN layer and direction)
 _BN_SLOTS = os.environ.get('UMAMD_BN_SLOTS', '1') == '1'
+#  - the pre-BN conv output y stored in the activation dtype (bf16) instead of
+#    f32, as a bf16 autocast conv feeding BatchNorm2d: the conv epilogue still
+#    takes the statistics from its f32 accumulators; the three BN passes and
+#    the conv's store move 2 bytes per element less
+_Y_ACT = os.environ.get('UMAMD_Y_ACT', '1') == '1'
+
+
+def _ydtype(dt):
+    """storage dtype of the pre-BN conv output for activations of ``dt``"""
+    return dt if (_Y_ACT and dt == torch.bfloat16) else torch.float32
+
+
+def _ydt(a, y):
+    """dtype code of a BN entry: activations ``a`` (a / da), plus UM_Y_ACT
+    when the pre-BN ``y`` is stored in their dtype rather than f32"""
+    return _dt(a) | (L.Y_ACT if y.dtype != torch.float32 else 0)
 
 
 class StatArena:
@@ -321,6 +367,90 @@ def stat_scope(arena: Optional[StatArena], device):
         if _ARENA is not None:
             _ARENA.end()
         _ARENA = prev
+
+
+class GradSlots:
+    """Input gradients of activations that several umamd autograd functions
+    consume inside one model forward: encoder stage outputs (next stage +
+    decoder), decoder outputs (next stage + disparity head), SE-gated skips
+    (this stage's concat + the next stage's skip conv), the decoder's input.
+    The first consumer to run its backward writes the gradient into a fresh
+    buffer and hands that to autograd; every later one ACCUMULATES into the
+    same buffer (GEMM / concat-adjoint accumulate epilogues) and returns None,
+    so autograd sums nothing -- it would launch one elementwise add per extra
+    consumer (12 bf16 adds per step).  Consumers outside a model forward
+    (the loss, user code) are not registered and go through autograd as
+    usual, which stays correct: autograd adds their gradient to the buffer's.
+    UMAMD_GRAD_SLOTS=0 turns it off."""
+
+    def __init__(self):
+        self.uses = {}
+        self.bufs = {}
+
+    @staticmethod
+    def key(t):
+        return (t.data_ptr(), tuple(t.shape), t.dtype)
+
+    def use(self, t):
+        """a consumer's forward: note one more registered use of t"""
+        if t is not None and t.requires_grad:
+            k = self.key(t)
+            self.uses[k] = self.uses.get(k, 0) + 1
+            return k
+        return None
+
+    def target(self, k):
+        """a consumer's backward: (buffer to accumulate into, or None)"""
+        if k is None or self.uses.get(k, 0) <= 1:
+            return None
+        e = self.bufs.get(k)
+        return e[0] if e is not None else None
+
+    def done(self, k, g):
+        """after writing (or accumulating into) g: what to return to autograd"""
+        if k is None or self.uses.get(k, 0) <= 1:
+            return g
+        e = self.bufs.get(k)
+        if e is None:  # first consumer: keep the buffer for the others
+            self.bufs[k] = [g, self.uses[k] - 1]
+            return g
+        e[1] -= 1
+        if e[1] <= 0:
+            del self.bufs[k]
+        return None
+
+
+_GSLOTS: Optional[GradSlots] = None
+_GRAD_SLOTS = os.environ.get('UMAMD_GRAD_SLOTS', '1') == '1'
+
+
+@contextmanager
+def grad_slots():
+    """one GradSlots registry for the consumers called inside (a model forward)"""
+    global _GSLOTS
+    prev = _GSLOTS
+    _GSLOTS = GradSlots() if _GRAD_SLOTS else None
+    try:
+        yield
+    finally:
+        _GSLOTS = prev
+
+
+def _use(ctx, *ts):
+    """forward: register the inputs ts; ctx.gk = their keys, ctx.gs = registry"""
+    ctx.gs = _GSLOTS
+    ctx.gk = [(_GSLOTS.use(t) if _GSLOTS is not None else None) for t in ts]
+
+
+def _slot(ctx, i):
+    """backward: (accumulate target or None) for registered input i"""
+    gs = getattr(ctx, 'gs', None)
+    return gs.target(ctx.gk[i]) if gs is not None else None
+
+
+def _give(ctx, i, g):
+    gs = getattr(ctx, 'gs', None)
+    return gs.done(ctx.gk[i], g) if gs is not None and g is not None else g
 
 
 def _const_vec(value: float, n: int, device) -> torch.Tensor:
@@ -455,7 +585,7 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
         slots_f = _ARENA.take(nslot + 1)
         slots_b = _ARENA.take(nslot + 1)
         y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
-                      out_dtype=torch.float32, epi=L.EPI_STAT_SLOTS, stats=slots_f,
+                      out_dtype=_ydtype(x.dtype), epi=L.EPI_STAT_SLOTS, stats=slots_f,
                       creal=Creal) if yconv is None else yconv(L.EPI_STAT_SLOTS, slots_f)
         if sync.collective:  # the conv stored this rank's count after the slots
             sync.all_reduce(slots_f)
@@ -469,7 +599,7 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
         parts = torch.empty((nparts, K, 2), dtype=torch.float32, device=dev)
         epi = L.EPI_STATS if training else L.EPI_NONE
         y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
-                      out_dtype=torch.float32, epi=epi, stats=parts, creal=Creal) \
+                      out_dtype=_ydtype(x.dtype), epi=epi, stats=parts, creal=Creal) \
             if yconv is None else yconv(epi, parts)
         mean, invstd, scale, shift = _bn_forward_coeffs(parts, nparts, K, M, bn, sync,
                                                         training, dev)
@@ -477,11 +607,11 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
         sync = None
         training = False
         y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
-                      out_dtype=torch.float32, creal=Creal) if yconv is None \
+                      out_dtype=_ydtype(x.dtype), creal=Creal) if yconv is None \
             else yconv(L.EPI_NONE, None)
         mean = shift = _const_vec(0.0, K, dev)
         invstd = scale = _const_vec(1.0, K, dev)
-    a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y is f32 (pre-BN)
+    a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y: pre-BN, f32 or bf16 (_ydtype)
     pool = None
     if w1 is not None and _FUSED_SE:  # the SE squeeze rides in the BN-apply pass
         npool = query('um_bn_fwd_pool_parts_c', M, P * Q, K)
@@ -496,18 +626,18 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
             msrcs, mwidx, mw = merge
             n = len(msrcs)
             merged = torch.empty_like(a)
-            call('um_bn_elu_fwd_slots_merge', _dt(a), M, K, ptr(y), K, ptr(slots_f), count,
+            call('um_bn_elu_fwd_slots_merge', _ydt(a, y), M, K, ptr(y), K, ptr(slots_f), count,
                  ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K, int(spec.elu), n,
                  (ctypes_p * n)(*[t.data_ptr() if t is not None else None for t in msrcs]),
                  (ctypes_i * n)(*mwidx), ptr(mw), msrcs.index(None), ptr(merged))
         else:
-            call('um_bn_elu_fwd_slots', _dt(a), M, K, ptr(y), K, ptr(slots_f), count,
+            call('um_bn_elu_fwd_slots', _ydt(a, y), M, K, ptr(y), K, ptr(slots_f), count,
                  ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K,
                  int(spec.elu), P * Q, ptr(pool))
     else:
-        call('um_bn_elu_fwd', _dt(a), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
+        call('um_bn_elu_fwd', _ydt(a, y), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
              int(spec.elu), P * Q, ptr(pool))
     inv_hw = 1.0 / (P * Q)
     if w1 is not None and not _FUSED_SE:  # separate squeeze: the means, one row per image
@@ -578,7 +708,7 @@ def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=
         if gamma is not None:
             dgamma = torch.empty(K, dtype=torch.float32, device=dev)
             dbeta = torch.empty(K, dtype=torch.float32, device=dev)
-        call('um_bn_elu_bwd_reduce_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+        call('um_bn_elu_bwd_reduce_slots', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K,
              ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
              ptr(slots_b))
         local, bcount, bscale = None, float(M), 1.0
@@ -607,19 +737,19 @@ def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=
             # one launch: the reduce kernel's last blocks finish the coefficients
             fin = torch.empty((query('um_bn_bwd_fin_ws', M, K) // 8,), dtype=torch.float64,
                               device=dev)
-            call('um_bn_elu_bwd_reduce_coeffs', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+            call('um_bn_elu_bwd_reduce_coeffs', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
                  ptr(parts), ptr(fin), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dbias),
                  ptr(k1), ptr(k2), ptr(k3))
         elif single:
-            call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+            call('um_bn_elu_bwd_reduce', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
                  ptr(parts))
             call('um_bn_bwd_stats_coeffs', ptr(parts), nb, K, ptr(_colred_ws(nb, K, 2, dev)),
                  float(M), ptr(gamma), ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(dbias),
                  ptr(k1), ptr(k2), ptr(k3))
         else:
-            call('um_bn_elu_bwd_reduce', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+            call('um_bn_elu_bwd_reduce', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
                  ptr(parts))
             ws = _colred_ws(nb, K, 2, dev)
@@ -642,12 +772,12 @@ def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=
     reduce_b = need_b and dbias is None
     bparts = torch.empty((nbp, K), dtype=torch.float32, device=dev) if reduce_b else None
     if ctx.has_bn and slots_b is not None:
-        call('um_bn_elu_bwd_apply_slots', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K,
+        call('um_bn_elu_bwd_apply_slots', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K,
              ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
              ptr(slots_b), bcount, ptr(local), ptr(gamma), ptr(dgamma), ptr(dbeta),
              ptr(dbias), bscale, ptr(dy), K)
     else:
-        call('um_bn_elu_bwd_apply', _dt(da), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
+        call('um_bn_elu_bwd_apply', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K, ptr(mean),
              ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu), ptr(k1),
              ptr(k2), ptr(k3), ptr(dy), K, ptr(bparts))
     if conv_bwd is not None:  # the caller's conv part (skip_conv_bn_elu): dy -> (dx, dW)
@@ -674,6 +804,7 @@ class ConvBNELUFn(torch.autograd.Function):
         x_, wT, y, mean, invstd, scale, shift, gamma_, w1_, w2_ = st.saved
         st.saved = None
         ctx.st = st
+        _use(ctx, x)
         ctx.save_for_backward(x_, wT, y, mean, invstd, scale, shift, gamma_, w1_, w2_)
         return outs if len(outs) > 1 else outs[0]
 
@@ -681,10 +812,12 @@ class ConvBNELUFn(torch.autograd.Function):
     def backward(ctx, da, ds=None):
         st = ctx.st
         st.saved = ctx.saved_tensors
-        out = _cbe_bwd(st, da, ds, need_x=ctx.needs_input_grad[0],
-                       need_b=ctx.needs_input_grad[2])
+        tgt = _slot(ctx, 0) if ctx.needs_input_grad[0] else None
+        dx, *rest = _cbe_bwd(st, da, ds, need_x=ctx.needs_input_grad[0],
+                             need_b=ctx.needs_input_grad[2], dx=tgt,
+                             dx_accumulate=tgt is not None)
         st.saved = None
-        return (*out, None)
+        return (_give(ctx, 0, dx), *rest, None)
 
 
 def conv_bn_elu(x, conv, bn, pad, pad_mode, se=None, elu=True, segs=None):
@@ -709,9 +842,10 @@ class SkipConvFn(torch.autograd.Function):
 
         W [fm | up2(g*skip)] = W_f fm + up2(W_s (g*skip))
 
-    The skip half is convolved at the skip's (quarter) pixel count into an
-    f32 map z, and um_conv2d_fwd_up2 adds up2(z) in the epilogue of the
-    feature-map half (before the BN statistics).  Backward: t = up2^T(dy) at
+    The skip half is convolved at the skip's (quarter) pixel count into a
+    map z (stored like the pre-BN y), and um_conv2d_fwd_up2 writes up2(z)
+    into y and accumulates the feature-map half onto it (the BN statistics
+    are taken on the sum).  Backward: t = up2^T(dy) at
     the low resolution, dW_s = t (x) (g*skip), d(g*skip) = W_s^T t, the gate
     adjoint as the concat's; dW_f and d fm at full resolution."""
 
@@ -728,13 +862,13 @@ class SkipConvFn(torch.autograd.Function):
         Cg = gs.shape[-1]
         wf_s, wT_s = _pack(weight, Cg, dt, segs=[(fin, 0, skin)])
         wf_f, wT_f = _pack(weight, Cf, dt, segs=[(0, 0, fin)])
-        z = _conv_fwd(gs, wf_s, None, K, 1, 1, 0, L.PAD_ZERO, out_dtype=torch.float32,
-                      creal=skin)
+        ydt = _ydtype(dt)
+        z = _conv_fwd(gs, wf_s, None, K, 1, 1, 0, L.PAD_ZERO, out_dtype=ydt, creal=skin)
         bias_f = bias.detach().float().contiguous() if bias is not None else None
 
         def yconv(epi, stats):
-            y = torch.empty((N, H, W, K), dtype=torch.float32, device=fm.device)
-            call('um_conv2d_fwd_up2', _dt(fm), N, H, W, Cf, Cf, ptr(fm), ptr(wf_f), ptr(bias_f),
+            y = torch.empty((N, H, W, K), dtype=ydt, device=fm.device)
+            call('um_conv2d_fwd_up2', _dt(fm) | (L.Y_ACT if ydt != torch.float32 else 0), N, H, W, Cf, Cf, ptr(fm), ptr(wf_f), ptr(bias_f),
                  K, H, W, ptr(y), K, epi, ptr(stats), ptr(z), h, w, K,
                  work=_conv_flops(N, H, W, K, 1, fin))  # the z conv is its own launch
             return y
@@ -744,6 +878,7 @@ class SkipConvFn(torch.autograd.Function):
         st.saved = None
         ctx.st = st
         ctx.geo = (N, H, W, Cf, h, w, Cg, K, fin, skin)
+        _use(ctx, fm, skip, gate)
         ctx.save_for_backward(fm, skip, gate, gs, wT_s, wT_f, y, mean, invstd, scale, shift,
                               gamma_, w1_, w2_)
         return outs if len(outs) > 1 else outs[0]
@@ -771,14 +906,23 @@ class SkipConvFn(torch.autograd.Function):
             _conv_wgrad(gs, t, K, K, fin + skin, 1, 1, 0, L.PAD_ZERO, dw=dW,
                         segs=[(fin, 0, skin)])
             if need_skip or need_gate:
-                dgs = _conv_dgrad(t, wT_s, (N, h, w, Cg), K, 1, 1, 0, L.PAD_ZERO, creal=skin)
+                tgt = _slot(ctx, 1) if need_skip else None
                 if gate is None:
-                    res['skip'] = dgs
+                    res['skip'] = _conv_dgrad(t, wT_s, (N, h, w, Cg), K, 1, 1, 0, L.PAD_ZERO,
+                                              dx=tgt, accumulate=tgt is not None, creal=skin)
                 else:
-                    res['skip'], res['gate'] = _gated_copy_bwd(dgs, skip, gate, skin,
-                                                               need_skip, need_gate)
-            dfm = _conv_dgrad(dy, wT_f, (N, H, W, Cf), K, 1, 1, 0, L.PAD_ZERO, creal=fin) \
-                if need_fm else None
+                    dgs = _conv_dgrad(t, wT_s, (N, h, w, Cg), K, 1, 1, 0, L.PAD_ZERO,
+                                      creal=skin)
+                    res['skip'], res['gate'] = _gated_copy_bwd(
+                        dgs, skip, gate, skin, need_skip, need_gate, dsk=tgt,
+                        dg=_slot(ctx, 2) if need_gate else None)
+                    res['gate'] = _give(ctx, 2, res['gate'])
+                res['skip'] = _give(ctx, 1, res['skip'])
+            dfm = None
+            if need_fm:
+                tgt = _slot(ctx, 0)
+                dfm = _give(ctx, 0, _conv_dgrad(dy, wT_f, (N, H, W, Cf), K, 1, 1, 0, L.PAD_ZERO,
+                                                dx=tgt, accumulate=tgt is not None, creal=fin))
             return dfm, dW
 
         dfm, dW, dbias, dgamma, dbeta, dw1, dw2 = _cbe_bwd(
@@ -799,20 +943,24 @@ def _gated_copy(skip, gate, C):
     return out
 
 
-def _gated_copy_bwd(dgs, skip, gate, C, need_skip, need_gate):
-    """adjoint of _gated_copy: (d skip, d gate)"""
+def _gated_copy_bwd(dgs, skip, gate, C, need_skip, need_gate, dsk=None, dg=None):
+    """adjoint of _gated_copy: (d skip, d gate); ``dsk`` / ``dg``: accumulate
+    into these tensors (else fresh ones are written)"""
     N, h, w, Ct = dgs.shape
     s = L.CatSrc(skip.data_ptr(), gate.data_ptr(), C, skip.shape[-1], L.CAT_COPY, 0, _dt(skip),
                  h, w)
-    dsk = torch.empty_like(skip) if need_skip else None
-    dg = torch.zeros_like(gate) if need_gate else None
+    acc = int(dsk is not None) | (2 if need_gate and dg is None else 0)
+    if need_skip and dsk is None:
+        dsk = torch.empty_like(skip)
+    if need_gate and dg is None:
+        dg = torch.empty_like(gate)
     ws = None
     if need_gate:
         ws = torch.empty((query('um_concat_bwd_ws', N, h, w, C),), dtype=torch.float32,
                          device=dgs.device)
-    call('um_concat_bwd_src', _dt(dgs), N, h, w, ptr(dgs), Ct, _ct.byref(s), ptr(dsk),
-         skip.shape[-1], _dt(skip), 0, ptr(dg), ptr(ws))
-    return dsk, dg
+    call('um_concat_bwd_src', _dt(dgs), N, h, w, ptr(dgs), Ct, _ct.byref(s),
+         ptr(dsk) if need_skip else None, skip.shape[-1], _dt(skip), acc, ptr(dg), ptr(ws))
+    return (dsk if need_skip else None), dg
 
 
 _SKIP_CONV = os.environ.get('UMAMD_SKIP_CONV', '1') == '1'
@@ -975,12 +1123,13 @@ class GraphBlockFn(torch.autograd.Function):
             k = len(gs.out_nodes)
             out = _merge_launch([a[o] for o in gs.out_nodes], None, [0] * k, [1.0 / k] * k,
                                 torch.empty_like(a[gs.out_nodes[0]]))
-        ctx.gs, ctx.a, ctx.states = gs, a, states
+        ctx.gspec, ctx.a, ctx.states = gs, a, states
+        _use(ctx, x)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        gs, a, states = ctx.gs, ctx.a, ctx.states
+        gs, a, states = ctx.gspec, ctx.a, ctx.states
         dout = dout.contiguous()
         if dout.dtype != a[0].dtype:
             dout = dout.to(a[0].dtype)
@@ -999,8 +1148,8 @@ class GraphBlockFn(torch.autograd.Function):
             for o, t in zip(outs, bufs):
                 da[o] = t
         grads = [None] * len(gs.params)
-        dx_stage = None
         need_x = ctx.needs_input_grad[1]
+        dx_stage = _slot(ctx, 0) if need_x else None  # accumulate into another consumer's
         for j in reversed(range(len(gs.nodes))):
             preds = gs.nodes[j]
             o, n = gs.slices[j]
@@ -1055,7 +1204,7 @@ class GraphBlockFn(torch.autograd.Function):
             states[j] = None  # release this node's saved tensors
         ctx.a = ctx.states = None
         grads = [gr if p is not None else None for gr, p in zip(grads, gs.params)]
-        return (None, dx_stage, *grads)
+        return (None, _give(ctx, 0, dx_stage), *grads)
 
 
 def graph_block(x, block):
@@ -1077,7 +1226,7 @@ class AttentionFn(torch.autograd.Function):
         pk = _packer.active() or _packer.WeightPacker()
         # rows [iC, (i+1)C) of wf; columns [iC, (i+1)C) of wT (row stride 3C)
         wf, wT = pk.pack_rows((wk, wq, wv), C, dt)
-        bqkv = torch.cat([bk.detach(), bq.detach(), bv.detach()]).float().contiguous()
+        bqkv = pk.pack_bias((bk, bq, bv), C)  # refreshed by the per-forward batch launch
         qkv = _conv_fwd(x, wf, bqkv, 3 * C, 1, 1, 0, L.PAD_ZERO)
         kmax = torch.empty((N, C), dtype=torch.float32, device=dev)
         ksum = torch.empty_like(kmax)
@@ -1158,6 +1307,8 @@ class ConcatFn(torch.autograd.Function):
         call('um_concat_build', L.dtype_code(dtype), N, H, W, ptr(out), Ctot, Ctot,
              len(srcs), structs)
         ctx.meta = meta
+        # slot-able inputs: the sources (0..n-1), then the gates in source order
+        _use(ctx, *[t for t, _ in srcs], *[gt for _, gt in srcs if gt is not None])
         ctx.save_for_backward(*saved)
         return out
 
@@ -1169,6 +1320,7 @@ class ConcatFn(torch.autograd.Function):
         saved = list(ctx.saved_tensors)
         grads = []
         k = 1  # index into needs_input_grad (0 = meta)
+        gi = len(meta['srcs'])  # slot index of the next gate
         for i, (op, C) in enumerate(meta['srcs']):
             coff = meta['coffs'][i]
             t = saved.pop(0)
@@ -1178,18 +1330,26 @@ class ConcatFn(torch.autograd.Function):
             h, w = (H, W) if op == L.CAT_COPY else (H // 2, W // 2)
             s = L.CatSrc(t.data_ptr(), gate.data_ptr() if gate is not None else None, C,
                          t.shape[-1], op, coff, _dt(t), h, w)
-            dt_ = torch.empty_like(t) if need_t else None
-            dg = torch.zeros_like(gate) if need_g else None
+            tgt = _slot(ctx, i) if need_t else None
+            dt_ = (tgt if tgt is not None else torch.empty_like(t)) if need_t else None
+            gslot = gi
+            if gate is not None:
+                gi += 1
+            gtgt = _slot(ctx, gslot) if need_g else None
+            # the gate gradient is written (flag bit 1) unless it accumulates
+            # into another consumer's (no zero fill)
+            dg = (gtgt if gtgt is not None else torch.empty_like(gate)) if need_g else None
             if need_t or need_g:
                 ws = None
                 if need_g:
                     nws = query('um_concat_bwd_ws', N, s.h, s.w, s.C)
                     ws = torch.empty((nws,), dtype=torch.float32, device=g.device)
+                flags = int(tgt is not None) | (2 if need_g and gtgt is None else 0)
                 call('um_concat_bwd_src', L.dtype_code(dtype), N, H, W, ptr(g), Ctot,
-                     _ct.byref(s), ptr(dt_), t.shape[-1], _dt(t), 0, ptr(dg), ptr(ws))
-            grads.append(dt_)
+                     _ct.byref(s), ptr(dt_), t.shape[-1], _dt(t), flags, ptr(dg), ptr(ws))
+            grads.append(_give(ctx, i, dt_))
             if gate is not None:
-                grads.append(dg)
+                grads.append(_give(ctx, gslot, dg))
             k += 2 if gate is not None else 1
         return (None, *grads)
 
@@ -1230,6 +1390,7 @@ class DispHeadFn(torch.autograd.Function):
                       out_dtype=torch.float32, epi=L.EPI_SIGMOID_SCALE, epi_scale=scale,
                       creal=Creal)
         ctx.scale = float(scale)
+        _use(ctx, x)
         ctx.save_for_backward(x, wT, d)
         ctx.geom = (K, Kp, Creal, R)
         return d
@@ -1246,9 +1407,12 @@ class DispHeadFn(torch.autograd.Function):
              ptr(dl), Kp)
         dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)
         db = _colsum_grad(dl, Kp)[:K]  # channels K..Kp of dl are zero
-        dx = _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT, creal=Creal,
-                         kreal=K) \
-            if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            tgt = _slot(ctx, 0)
+            dx = _give(ctx, 0, _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT,
+                                           dx=tgt, accumulate=tgt is not None, creal=Creal,
+                                           kreal=K))
         return dx, dW, db, None
 
 

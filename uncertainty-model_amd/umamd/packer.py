@@ -156,6 +156,29 @@ class WeightPacker:
                  f[i * C].data_ptr(), t.data_ptr() + i * C * es, n * C)
         return e
 
+    def pack_bias(self, biases, C: int):
+        """The attention's fused K/Q/V bias: one f32 [nC] vector of the n
+        biases (each [C], f32 parameters), refreshed by the f32 batch launch
+        (a bias is packed as a [C][1][1][1] weight into the data-gradient
+        layout [1][1][1][nC] at column i*C) instead of a torch.cat per
+        attention block and step."""
+        n = len(biases)
+        key = ('bias', tuple(b.data_ptr() for b in biases), C)
+        e = self.entries.get(key)
+        if e is not None and self.batched and key in self.registered:
+            return e
+        dev = biases[0].device
+        if e is None:
+            e = torch.empty((n * C,), dtype=torch.float32, device=dev)
+            if all(_f32(b).data_ptr() == b.data_ptr() for b in biases):
+                for i, b in enumerate(biases):
+                    self._register(b, b, None, e.data_ptr() + i * C * 4, C, 1, 1, 1, n * C,
+                                   None, torch.float32)
+                self.registered.add(key)
+            self.entries[key] = e
+        torch.cat([_f32(b) for b in biases], out=e)
+        return e
+
     def _register(self, weight, w32, wf, wT, K, Creal, R, C, ldT, segs, dtype):
         if w32.data_ptr() != weight.data_ptr():
             # the batch reads the parameter memory directly: only f32 contiguous params
