@@ -437,6 +437,33 @@ def test_wgrad_reduce_batch_matches_per_conv(monkeypatch):
         assert torch.equal(r, got)
 
 
+# slab reduction of the large 3x3..7x7 weights (>= 256K elements: the LDS-
+# transposed kernel with contiguous dW stores) against torch, with padded
+# K / C, a segment map (concat input) and accumulate
+@pytest.mark.parametrize('case', [(3, 64, 60, 3, 512, 500, None), (2, 32, 32, 5, 256, 256, None),
+                                  (5, 24, 24, 7, 200, 200, None),
+                                  (2, 48, 40, 3, 640, 600, [(0, 0, 300), (300, 320, 300)])])
+@pytest.mark.parametrize('accumulate', [0, 1])
+def test_wgrad_reduce_large(case, accumulate):
+    from umamd import functional as U
+    from umamd._lib import call, ptr
+    splits, K, Kreal, R, C, Creal, segs = case
+    g = torch.Generator().manual_seed(8)
+    slabs = torch.randn(splits, K, R, R, C, generator=g).to(DEV)
+    dw0 = torch.randn(Kreal, Creal, R, R, generator=g).to(DEV)
+    dw = dw0.clone()
+    n, a0, b0, l0 = U._seg_arrays(segs)
+    call('um_conv_wgrad_reduce_seg', ptr(slabs), splits, K, Kreal, R, C, Creal, ptr(dw),
+         accumulate, n, a0, b0, l0)
+    torch.cuda.synchronize()
+    ref = slabs.double().sum(0)[:Kreal].permute(0, 3, 1, 2).cpu()  # [Kreal][C][R][R]
+    exp = dw0.double().cpu().clone() if accumulate else torch.full_like(dw0.double().cpu(), float('nan'))
+    for src0, dst0, ln in (segs or [(0, 0, Creal)]):
+        part = ref[:, dst0:dst0 + ln]
+        exp[:, src0:src0 + ln] = part + (exp[:, src0:src0 + ln] if accumulate else 0)
+    assert torch.allclose(dw.double().cpu(), exp, rtol=1e-5, atol=1e-5)
+
+
 # the side stream's batched bias gradients (um_colsum_batch: one partial-row
 # pass + one f64 finish per flush) against the per-bias reduction
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
@@ -453,6 +480,49 @@ def test_colsum_batch_matches_per_bias(dtype):
     torch.cuda.synchronize()
     for o, r in zip(outs, refs):
         assert torch.allclose(o, r, rtol=1e-5, atol=1e-4), float((o - r).abs().max())
+
+
+# the decoder skip conv's feature-map half (um_conv2d_fwd_up2): y = W fm +
+# bias + up2(z) with the BN statistics slots taken on the sum, f32 y and the
+# bf16 build's y (UM_Y_ACT: the accumulating GEMM's statistics in the staged
+# 16-byte row store), against f64 torch on the same operands
+@pytest.mark.parametrize('case', [(2, 64, 128, 8, 32), (2, 32, 64, 32, 64), (1, 16, 24, 16, 32),
+                                  (2, 128, 64, 8, 16)])
+@pytest.mark.parametrize('yact', [False, True])
+def test_conv_fwd_up2_slots(case, yact):
+    from umamd import functional as U
+    from umamd import _lib as L
+    from umamd._lib import call, ptr
+    N, H, W, Cf, K = case
+    h, w = H // 2, W // 2
+    g = torch.Generator().manual_seed(5)
+    fm = torch.rand(N, H, W, Cf, generator=g).to(torch.bfloat16).to(DEV)
+    ydt = torch.bfloat16 if yact else torch.float32
+    z = torch.randn(N, h, w, K, generator=g).to(ydt).to(DEV)
+    wt = torch.randn(K, Cf, 1, 1, generator=g).to(DEV)
+    bias = torch.randn(K, generator=g).to(DEV)
+    wf, _ = U._pack(wt, Cf, torch.bfloat16)
+    y = torch.empty(N, H, W, K, dtype=ydt, device=DEV)
+    slots = torch.zeros(L.STAT_SLOTS * K * 2 + 1, dtype=torch.float64, device=DEV)
+    call('um_conv2d_fwd_up2', L.UM_BF16 | (L.Y_ACT if yact else 0), N, H, W, Cf, Cf, ptr(fm),
+         ptr(wf), ptr(bias), K, H, W, ptr(y), K, L.EPI_STAT_SLOTS, ptr(slots), ptr(z), h, w, K)
+    torch.cuda.synchronize()
+    wq = wt.to(torch.bfloat16).double()[:, :, 0, 0]
+    ref = torch.einsum('nhwc,kc->nhwk', fm.double(), wq) + bias.double()
+    up = F.interpolate(z.double().permute(0, 3, 1, 2), scale_factor=2, mode='bilinear',
+                       align_corners=True).permute(0, 2, 3, 1)
+    ref = ref + up
+    tol = 2e-2 if yact else 1e-5
+    assert _rel(y.double(), ref) < tol
+    st = slots[:L.STAT_SLOTS * K * 2].view(L.STAT_SLOTS, K, 2).sum(0)
+    s1, s2 = ref.sum(dim=(0, 1, 2)), (ref * ref).sum(dim=(0, 1, 2))
+    scale1 = ref.abs().sum(dim=(0, 1, 2))
+    # bf16 y: the statistics are of bf16(W fm + bias) + bf16(up2 z), the
+    # reference of the exact sum (two 2^-9 roundings per element)
+    stol = 1e-3 if yact else 1e-4
+    assert float(((st[:, 0] - s1).abs() / scale1).max()) < stol
+    assert float(((st[:, 1] - s2).abs() / s2).max()) < stol
+    assert float(slots[-1]) == N * H * W
 
 
 # x2 bilinear (align_corners=True) upsample of a concat source: forward and

@@ -512,6 +512,52 @@ __device__ __forceinline__ void wgrad_reduce4_body(const float* __restrict__ sla
   }
 }
 
+// Slab reduce of the large 3x3..7x7 weights (>= 256K elements): block (64-
+// channel chunk, output row k) sums the splits of slab rows [k][rs][c0, c0+64)
+// for every tap into an LDS tile, then writes dW[k][c][rs] of its chunk as
+// one contiguous run.  The float4 reduce's 4-byte stores at stride R*R leave
+// partially written lines all over the 2-13 MB weight in every XCD's L2
+// (15-19 us per 3x3/512 layer for ~37 MB of slab traffic).
+constexpr int WRT_CW = 64;
+__global__ void __launch_bounds__(256) wgrad_reduce_t_kernel(const float* __restrict__ slabs,
+                                                             int splits, int K, int R, int C,
+                                                             int Creal, float* __restrict__ dw,
+                                                             int accumulate, Segs sg) {
+  extern __shared__ float tile[];  // [R*R][WRT_CW + 1]
+  const int k = blockIdx.y, c0 = blockIdx.x * WRT_CW;
+  const int RR = R * R, RRC = RR * C;
+  const int cw = min(WRT_CW, C - c0);
+  const long zs = (long)K * RRC;
+  const float* __restrict__ base = slabs + (long)k * RRC + c0;
+  const int n = RR * WRT_CW;
+  for (int e = threadIdx.x; e < n; e += 256) {
+    const int rs = e / WRT_CW, cl = e - rs * WRT_CW;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    if (cl < cw) {
+      const float* p = base + rs * C + cl;
+      int z = 0;
+      for (; z + 3 < splits; z += 4, p += 4 * zs) {
+        v0 += p[0];
+        v1 += p[zs];
+        v2 += p[2 * zs];
+        v3 += p[3 * zs];
+      }
+      for (; z < splits; ++z, p += zs) v0 += p[0];
+    }
+    tile[rs * (WRT_CW + 1) + cl] = (v0 + v1) + (v2 + v3);
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < n; q += 256) {
+    const int cl = q / RR, rs = q - cl * RR;
+    if (cl >= cw) continue;
+    const int c = seg_src(sg, c0 + cl);
+    if (c < 0) continue;
+    const long o = ((long)k * Creal + c) * RR + rs;
+    const float v = tile[rs * (WRT_CW + 1) + cl];
+    dw[o] = accumulate ? dw[o] + v : v;
+  }
+}
+
 __global__ void __launch_bounds__(256) wgrad_reduce4_kernel(const float* __restrict__ slabs,
                                                             int splits, int K, int Kreal, int R,
                                                             int C, int Creal,
@@ -1071,6 +1117,17 @@ int um_conv_wgrad_reduce_seg(const float* slabs, int splits, int K, int Kreal, i
   UM_CHECK_ARG(make_segs(g, nseg, src0, dst0, len, Creal, C), "um_conv_wgrad_reduce: segments");
   const long total = (long)Kreal * R * R * C;
   const long RRC = (long)R * R * C;
+  static const int wred_t = [] {
+    const char* e = getenv("UMAMD_WRED_T");
+    return e ? atoi(e) : 1;
+  }();
+  if (wred_t && R > 1 && total >= (1l << 18)) {
+    const size_t shm = (size_t)R * R * (WRT_CW + 1) * sizeof(float);
+    hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3(ceil_div(C, WRT_CW), Kreal), dim3(256), shm, st,
+                       slabs, splits, K, R, C, Creal, dw, accumulate, g);
+    UM_LAUNCH_CHECK();
+    return UM_OK;
+  }
   if (RRC % 4 == 0 && (long)splits * K * RRC < (1l << 33)) {
     const long total4 = total / 4;
     int L = 1;

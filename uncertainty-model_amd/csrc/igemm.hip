@@ -262,8 +262,15 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
     }
     return;
   }
-  const bool staged = sOut != nullptr && !a.out_f32 && a.NC % 8 == 0 && a.ld_out % 8 == 0 &&
-                      !(a.accumulate && a.epilogue == UM_EPI_STATS);
+  const bool stageable = sOut != nullptr && !a.out_f32 && a.NC % 8 == 0 && a.ld_out % 8 == 0;
+  // accumulate + statistics slots (the decoder skip conv's feature-map half
+  // onto up2(z)): the statistics of the SUM are taken in the 16-byte row
+  // store (WN == 1: one wave per row of sStat) instead of a 2-byte
+  // read-modify-write per element in the MFMA layout
+  constexpr bool kRows = WN == 1 && 256 % (BN / 8) == 0;  // a thread keeps one column group
+  const bool stat_rows = kRows && stageable && a.accumulate && a.epilogue == UM_EPI_STATS &&
+                         a.stat_slots;
+  const bool staged = stageable && (!(a.accumulate && a.epilogue == UM_EPI_STATS) || stat_rows);
   float csum[TN], csq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
@@ -298,7 +305,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
         csq[j] += v * v;
       }
   }
-  if (a.epilogue == UM_EPI_STATS) {
+  if (a.epilogue == UM_EPI_STATS && !stat_rows) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       float sm = csum[j], sq = csq[j];
@@ -343,6 +350,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
   if (staged) {
     __syncthreads();
     constexpr int CPR = BN / 8;
+    float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pq[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int c = tid; c < BM * CPR; c += (int)blockDim.x) {
       const int r = c / CPR, c8 = (c - r * CPR) * 8;
       const int m = bm + r, n = bn + c8;
@@ -355,11 +363,42 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
 #pragma unroll
         for (int e = 0; e < 8; ++e) x[e] += y[e];
         store8(o, x);
+        if (stat_rows)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            ps[e] += x[e];
+            pq[e] += x[e] * x[e];
+          }
       } else {
         Raw8<T> v;
         raw_load8(&sOut[r * BN + c8], v);
         raw_store8(o, v);
       }
+    }
+    if constexpr (kRows) if (stat_rows) {
+      // lanes of one wave with the same column group: lane % CPR
+#pragma unroll
+      for (int sh = CPR; sh < 64; sh <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ps[e] += __shfl_xor(ps[e], sh, 64);
+          pq[e] += __shfl_xor(pq[e], sh, 64);
+        }
+      if (lane < CPR)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sStat[wave][lane * 8 + e][0] = ps[e];
+          sStat[wave][lane * 8 + e][1] = pq[e];
+        }
+      __syncthreads();
+      stat_slots_count(reinterpret_cast<double*>(a.stats), a.NC, a.M);
+      stat_slots_add_row(reinterpret_cast<double*>(a.stats), bm / BM, a.NC, bn,
+                         min(BN, a.NC - bn), [&](int i) {
+                           float v = 0.f;
+#pragma unroll
+                           for (int w = 0; w < WM; ++w) v += sStat[w][i >> 1][i & 1];
+                           return v;
+                         });
     }
   }
 }
