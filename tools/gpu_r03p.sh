@@ -10,7 +10,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -2 $OUT/tests.log
 timeout -k 10 120 python -u tools/up2_micro.py > $OUT/up2_micro.txt 2>&1 || { echo UP2 FAILED; tail $OUT/up2_micro.txt; exit 1; }
 cat $OUT/up2_micro.txt
-tools/gpu_arms.sh ${T}_arms "UMAMD_X=0" "UMAMD_WRED_T=0"
+tools/gpu_arms.sh ${T}_arms "UMAMD_X=0" "UMAMD_UP2_VALU=0"
 tools/prof_step.sh ${T}_prof --loader-steps 0 --fp32-steps 0 --no-loss-delta --eager-steps 0 --no-roofline || { echo PROF FAILED; exit 1; }
 head -3 gpurun_out/${T}_prof/step_kernels.txt
 head -25 gpurun_out/${T}_prof/gaps.txt

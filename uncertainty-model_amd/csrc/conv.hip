@@ -863,6 +863,133 @@ int um_conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                     y, ldy, epilogue, epi_scale, residual, ldr, stats, ws, ws_bytes, 0, st);
 }
 
+}  // extern "C"
+
+namespace {
+// The decoder skip conv's feature-map half when the feature map is narrow
+// (C <= 16: the image at 256x512): y = W x + bias + up2(z)
+// and the BN statistics slots of y in ONE VALU pass.  The GEMM route (an
+// upsample pass into y, then an accumulating 1x1 GEMM with 256-row tiles on
+// an 8..32-deep reduction) moves y three times and runs the MFMA tiles on a
+// reduction they cannot fill; here x and z are read once and y written once.
+// Thread = (pixel, 8 output channels): the K/8 groups of a pixel are
+// consecutive lanes (one contiguous run per pixel); W in LDS as f32 (the
+// lanes of a wave read G distinct rows: broadcast reads).
+template <typename T, typename TY, int C>
+__global__ void __launch_bounds__(256) conv1x1_up2_kernel(
+    const T* __restrict__ x, int ldx, const T* __restrict__ wf, const float* __restrict__ bias,
+    int K, int H, int W, long M, TY* __restrict__ y, int ldy, const TY* __restrict__ z, int h,
+    int w, int ldz, double* __restrict__ slots) {
+  extern __shared__ float sm[];  // W [K][C] f32, then the statistics [4 waves][K][2]
+  float* sW = sm;
+  float* sS = sm + K * C;
+  for (int i = threadIdx.x; i < K * C; i += 256) sW[i] = to_f32(wf[i]);
+  __syncthreads();
+  const int G = K / 8;  // 256 % G == 0 (host): a thread keeps its group
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = threadIdx.x % G, k0 = g * 8;
+  float b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b[e] = bias ? bias[k0 + e] : 0.f;
+  const float scy = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+  const float scx = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  float ps[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pq[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // one output row (n, oy) per block iteration: 32-bit index math only, the
+  // vertical taps and weights once per row
+  const int rows = (int)(M / W), items = W * G, gs = __ffs(G) - 1;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int n = row / H, oy = row - n * H;
+    const float fy = scy * (float)oy;
+    const int y0 = min((int)fy, h - 1);
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0);
+    const float ly = fy - (float)y0;
+    const TY* __restrict__ z0 = z + ((long)n * h + y0) * w * ldz + k0;
+    const TY* __restrict__ z1 = z + ((long)n * h + y1) * w * ldz + k0;
+    const long mrow = (long)row * W;
+    for (int i = threadIdx.x; i < items; i += 256) {
+      const int ox = i >> gs;  // G is a power of two
+      // re-read W from LDS per pixel (broadcast reads) instead of keeping 8*C
+      // weights live in VGPRs (170-250 VGPRs, 2 waves per SIMD)
+      asm volatile("" ::: "memory");
+      const long m = mrow + ox;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = b[e];
+#pragma unroll
+      for (int c = 0; c < C; c += 8) {
+        float xv[8];
+        load8(x + m * ldx + c, xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float4 w0 = *reinterpret_cast<const float4*>(&sW[(k0 + e) * C + c]);
+          const float4 w1 = *reinterpret_cast<const float4*>(&sW[(k0 + e) * C + c + 4]);
+          v[e] += w0.x * xv[0] + w0.y * xv[1] + w0.z * xv[2] + w0.w * xv[3] + w1.x * xv[4] +
+                  w1.y * xv[5] + w1.z * xv[6] + w1.w * xv[7];
+        }
+      }
+      // torch upsample_bilinear2d(align_corners=True), as the concat kernel
+      const float fx = scx * (float)ox;
+      const int x0 = min((int)fx, w - 1);
+      const int x1 = x0 + (x0 < w - 1 ? 1 : 0);
+      const float lx = fx - (float)x0;
+      float a00[8], a01[8], a10[8], a11[8];
+      load8(z0 + (long)x0 * ldz, a00);
+      load8(z0 + (long)x1 * ldz, a01);
+      load8(z1 + (long)x0 * ldz, a10);
+      load8(z1 + (long)x1 * ldz, a11);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] += (1.f - ly) * ((1.f - lx) * a00[e] + lx * a01[e]) +
+                ly * ((1.f - lx) * a10[e] + lx * a11[e]);
+      store8(y + m * ldy + k0, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ps[e] += v[e];
+        pq[e] += v[e] * v[e];
+      }
+    }
+  }
+  if (slots == nullptr) return;
+  // lanes of a wave with the same group: lane % G
+  for (int sh = G; sh < 64; sh <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ps[e] += __shfl_xor(ps[e], sh, 64);
+      pq[e] += __shfl_xor(pq[e], sh, 64);
+    }
+  if (lane < G)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sS[(wave * K + k0 + e) * 2] = ps[e];
+      sS[(wave * K + k0 + e) * 2 + 1] = pq[e];
+    }
+  __syncthreads();
+  stat_slots_count(slots, K, M);
+  stat_slots_add_row(slots, blockIdx.x, K, 0, K, [&](int i) {
+    return sS[i] + sS[2 * K + i] + sS[4 * K + i] + sS[6 * K + i];
+  });
+}
+
+template <typename T, typename TY>
+int launch_conv1x1_up2(int C, const void* x, int ldx, const void* wf, const float* bias, int K,
+                       int N, int H, int W, void* y, int ldy, const void* z, int h, int w, int ldz,
+                       double* slots, hipStream_t st) {
+  const long M = (long)N * H * W;
+  const int grid = std::min(N * H, 4096);
+  const size_t shm = ((size_t)K * C + 8 * (size_t)K) * sizeof(float);
+#define UM_C1UP(CC)                                                                            \
+  hipLaunchKernelGGL((conv1x1_up2_kernel<T, TY, CC>), dim3(grid), dim3(256), shm, st,           \
+                     (const T*)x, ldx, (const T*)wf, bias, K, H, W, M, (TY*)y, ldy, (const TY*)z, \
+                     h, w, ldz, slots)
+  if (C == 8) UM_C1UP(8); else UM_C1UP(16);
+#undef UM_C1UP
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int um_conv2d_fwd_up2(int dtype, int N, int H, int W, int C, int ldx, const void* x,
                       const void* wf, const float* bias, int K, int P, int Q, void* y, int ldy,
                       int epilogue, float* stats, const void* up2, int up2_h, int up2_w,
@@ -877,6 +1004,23 @@ int um_conv2d_fwd_up2(int dtype, int N, int H, int W, int C, int ldx, const void
                "um_conv2d_fwd_up2: epilogue");
   UM_CHECK_ARG(K % 8 == 0 && ldy % 8 == 0 && up2_ld % 8 == 0 && P == H && Q == W,
                "um_conv2d_fwd_up2: K / strides must be multiples of 8, 1x1 same-size conv");
+  static const int valu = [] {
+    const char* e = getenv("UMAMD_UP2_VALU");
+    return e ? atoi(e) : 1;
+  }();
+  const int G = K / 8;
+  if (valu && C % 8 == 0 && C <= 16 && K <= 128 && 256 % G == 0 && ldx % 8 == 0 &&
+      (epilogue == UM_EPI_NONE || epilogue == UM_EPI_STAT_SLOTS)) {
+    double* sl = epilogue == UM_EPI_STAT_SLOTS ? reinterpret_cast<double*>(stats) : nullptr;
+    if (dtype == UM_BF16 && ydt == UM_BF16)
+      return launch_conv1x1_up2<bf16_t, bf16_t>(C, x, ldx, wf, bias, K, N, H, W, y, ldy, up2,
+                                                up2_h, up2_w, up2_ld, sl, st);
+    if (dtype == UM_BF16)
+      return launch_conv1x1_up2<bf16_t, float>(C, x, ldx, wf, bias, K, N, H, W, y, ldy, up2,
+                                               up2_h, up2_w, up2_ld, sl, st);
+    return launch_conv1x1_up2<float, float>(C, x, ldx, wf, bias, K, N, H, W, y, ldy, up2, up2_h,
+                                            up2_w, up2_ld, sl, st);
+  }
   // y = up2(z) by one vectorised upsample pass (the concat kernel with one
   // UP2 source), then the GEMM ADDS W x + bias into y, with the BN
   // statistics taken on the sum in its epilogue (an in-epilogue gather of the
