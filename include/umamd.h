@@ -155,6 +155,7 @@ typedef struct {
   void* wT;         /* [C][R][R][ldT] (nullable; column offset applied) */
   int K, Creal, R, C, ldT, block0;
   int nseg, src0[UM_PACK_MAXSEG], dst0[UM_PACK_MAXSEG], len[UM_PACK_MAXSEG];
+  int split;        /* bf16 only: pack 2K rows, see um_pack_weight_split (tiles: 2K) */
 } um_pack_desc;
 int um_pack_batch(int dtype, const um_pack_desc* table, int ndesc, const int* blk2desc,
                   int nblocks, hipStream_t stream);
@@ -166,6 +167,15 @@ int um_pack_desc_size(void);
  * elements) and wT [C][R][R][ldT] (column offset applied by the caller); C >= Creal, zero fill */
 int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C,
                    void* wf, void* wT, int ldT, hipStream_t stream);
+
+/* split-bf16 pack (bf16 only): wf [2K][R][R][C] and wT [C][R][R][ldT >= 2K]
+ * hold rows k < K = bf16(w[k]) and rows K + k = bf16(w[k] - bf16(w[k])), so a
+ * GEMM over the 2K rows whose output pairs (k, K + k) are summed in f32 sees
+ * the f32 weight to ~2^-17 relative at bf16 MFMA rates.  Used by the
+ * disparity/uncertainty heads (reference model/layers/decoder.py:244-247),
+ * whose 4 outputs pad to 8 GEMM columns anyway. */
+int um_pack_weight_split(const float* w, int K, int Creal, int R, int C, void* wf, void* wT,
+                         int ldT, hipStream_t stream);
 
 /* per-channel column sums of y[M][C] (pixel stride ld) -> partial rows [parts][C] */
 /* Several bias gradients (um_colsum + um_reduce_rows each) in two launches:
@@ -251,7 +261,13 @@ int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const 
                         float momentum, float* running_mean, float* running_var,
                         long long* num_batches_tracked, float* mean, float* invstd, float* scale,
                         float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
-                        hipStream_t stream);
+                        float* ycen, const float* conv_bias, hipStream_t stream);
+/* ycen (optional, [C] f32, persistent per layer): the bf16 pre-BN output is
+ * stored centred.  The conv ran with bias = ycen instead of conv_bias, so y
+ * holds y_true - conv_bias + ycen; mean/invstd/scale/shift describe that y
+ * (the BN output is unchanged), the running mean gets the true mean, and
+ * ycen is updated to minus this step's conv-only mean for the next step.
+ * Null: y is the conv's output with its own bias. */
 /* um_bn_elu_fwd_slots plus the NodeBlock merge of the next graph node
  * (reference model/layers/encoder.py:115-124): merged = sum_i
  * sigmoid(w[widx[i]]) * src_i over nsrc (2..8) sources [M][lda] of the
@@ -264,7 +280,8 @@ int um_bn_elu_fwd_slots_merge(int dtype, long M, int C, const void* y, int ldy,
                               float* running_var, long long* num_batches_tracked, float* mean,
                               float* invstd, float* scale, float* shift, void* a, int lda,
                               int apply_elu, int nsrc, const void* const* srcs, const int* widx,
-                              const float* w, int self, void* merged, hipStream_t stream);
+                              const float* w, int self, void* merged, float* ycen,
+                              const float* conv_bias, hipStream_t stream);
 /* backward sums (sum dz, sum dz*xhat) added into zeroed f64 slots
  * [UM_STAT_SLOTS][C][2] instead of partial rows */
 int um_bn_elu_bwd_reduce_slots(int dtype, long M, int C, long HW, const void* da, int ldda,
@@ -349,6 +366,15 @@ int um_axpy(int dtype, long n, float alpha, const void* x, void* y, hipStream_t 
 /* d/dlogit of scale*sigmoid(logit): disp head, reference model/layers/decoder.py:246 */
 int um_sigmoid_scale_bwd(int dtype, long M, int C, const float* d, int ldd, const float* dd,
                          int lddd, float scale, void* dlogit, int ldo, hipStream_t stream);
+/* split-bf16 head (um_pack_weight_split): forward finish d[m][k] = scale *
+ * sigmoid(z[m][k] + z[m][K + k] + bias[k]) over the 2K-column f32 GEMM
+ * output z, and the backward's dlogit written to channels k AND K + k (so the
+ * data-gradient GEMM over the 2K split rows sums both halves of the weight);
+ * channels [2K, ldo) zeroed. */
+int um_head_split_fin(long M, int K, const float* z, int ldz, const float* bias, float scale,
+                      float* d, int ldd, hipStream_t stream);
+int um_sigmoid_scale_bwd_split(int dtype, long M, int C, const float* d, int ldd, const float* dd,
+                               int lddd, float scale, void* dlogit, int ldo, hipStream_t stream);
 
 /* ----------------------------------------------------------- attention ---
  * EfficientAttention core, reference model/layers/attention.py:42-76.

@@ -344,6 +344,44 @@ def gen_traj(ref_model, ref_loss, ref_utils, cfg, steps=10, b=8, h=256, w=512):
     save('traj_c2.npz', **arrays)
 
 
+def gen_traj_bf16(ref_model, ref_loss, ref_utils, cfg, steps=10, b=8, h=256, w=512):
+    """The same 10 config-2 steps as gen_traj, with the reference's forward and
+    loss under CPU bf16 autocast (torch.autocast('cpu', torch.bfloat16); the
+    backward and Adam as autocast leaves them).  This is the reference's OWN
+    bf16 deviation at exactly the bench's workload (weights, pair, scale), the
+    yardstick BASELINE.md's bf16 bar was measured with (at other
+    weights).  Stores the per-step loss scalars and the step-0 disparity sums."""
+    sys.path.insert(0, REPO)
+    from oracle import step as OS  # noqa: E402
+    sd, _ = _formula_weights(cfg)
+    m = _ref_model(ref_model, cfg)
+    m.load_state_dict(sd)
+    m.train()
+    lcfg = json.loads(json.dumps(cfg['loss']))
+    lcfg['error_loss_config']['loss_type'] = 'bayesian'
+    lf = ref_loss.TukraUncertaintyLoss(**lcfg)
+    opt = torch.optim.Adam(m.parameters(), 1e-4)
+    left, right = OS.bench_inputs(b, h, w)
+    arrays = {'shape': np.array([b, h, w]), 'seed': np.int64(1234), 'scale': np.float64(0.3)}
+    for step in range(steps):
+        with torch.autocast('cpu', dtype=torch.bfloat16):
+            pyr = ref_utils.scale_pyramid(torch.cat([left, right], 1), 4)
+            opt.zero_grad()
+            disps = m(left, 0.3)
+            recon = ref_utils.reconstruct_pyramid(disps, pyr)
+            dl, el = lf(pyr, disps, recon, step, None)
+        (dl + el).float().backward()
+        if step == 0:
+            for i, d in enumerate(disps):
+                arrays[f'step0_disp{i}_sum'] = d.detach().double().sum()
+                arrays[f'step0_disp{i}_abssum'] = d.detach().double().abs().sum()
+        opt.step()
+        arrays[f'disp_loss_{step}'] = np.float64(float(dl))
+        arrays[f'error_loss_{step}'] = np.float64(float(el))
+        print(f'traj bf16 step {step}: {float(dl):.6f} {float(el):.6f}', flush=True)
+    save('traj_c2_bf16.npz', **arrays)
+
+
 def gen_nodes10(ref_model, cfg10):
     sd, specs = _formula_weights(cfg10)
     m = _ref_model(ref_model, cfg10)
@@ -519,6 +557,8 @@ def main():
         gen_nodes10(ref_model, cfg10)
     if 'traj' in which:  # BASELINE config 2, full size (slow: ~1 min on 8 cores)
         gen_traj(ref_model, ref_loss, ref_utils, cfg)
+    if 'traj_bf16' in which:  # the reference's own bf16-autocast deviation at config 2
+        gen_traj_bf16(ref_model, ref_loss, ref_utils, cfg)
     if 'c1' in which:  # BASELINE config 1: 128x256, batch 2, l1 error loss, one step
         gen_step(ref_model, ref_loss, ref_utils, cfg, 'l1', steps=1, tag='c1_l1', b=2, h=128,
                  w=256, disp_levels=(2, 3))

@@ -294,10 +294,10 @@ def test_batched_weight_pack_matches_per_site_pack(dtype):
                 continue
             f, t = e
             w = params[key[1]]
-            Cp, dt, ldT, segs = key[3], key[4], key[5], key[6]
+            Cp, dt, ldT, segs, split = key[3], key[4], key[5], key[6], key[9]
             f2 = torch.empty_like(f) if f is not None else None
             t2 = torch.zeros_like(t) if t is not None else None
-            _pack_one(w.detach(), f2, t2, Cp, ldT, list(segs) if segs else None, dt)
+            _pack_one(w.detach(), f2, t2, Cp, ldT, list(segs) if segs else None, dt, split)
             if f is not None:
                 assert torch.equal(f, f2), key
             if t is not None:

@@ -755,3 +755,52 @@ def test_dgrad_stride2_classes(case, cls4):
     finally:
         lib().um_set_tuning(b'cls4', old)
     assert _rel(_nchw(dx), ref) < 1e-2
+
+
+@pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 16), (256, 4, 8)])
+def test_disp_head_split(C, H, W, monkeypatch):
+    """The bf16 disparity/uncertainty head with split-bf16 weights
+    (um_pack_weight_split: hi + lo rows in the padding columns of the
+    4-output GEMM) against an f64 reference with the UNROUNDED f32 weights:
+    the forward is f32-accurate (the plain bf16 head is off by the weight
+    rounding), and the backward sums both halves of the weight."""
+    import umamd.functional as U
+    N, K, scale = 2, 4, 0.3
+    x = F.elu(torch.randn(N, C, H, W)).to(torch.bfloat16).float()
+    conv = nn.Conv2d(C, K, 3)
+    nn.init.xavier_uniform_(conv.weight)
+    conv.bias.data.uniform_(-0.5, 0.5)
+    conv = conv.to(DEV)
+    dd = torch.randn(N, K, H, W)
+
+    def ref():
+        xr = x.double().requires_grad_(True)
+        wr = conv.weight.detach().double().cpu().requires_grad_(True)
+        z = F.conv2d(F.pad(xr, (1, 1, 1, 1), mode='reflect'), wr,
+                     conv.bias.detach().double().cpu())
+        d = scale * torch.sigmoid(z)
+        d.backward(dd.double())
+        return d.detach(), xr.grad, wr.grad
+
+    def run(split):
+        monkeypatch.setattr(U, '_SPLIT_HEAD', split)
+        xd = _nhwc(x).to(torch.bfloat16)
+        Cp = (C + 7) // 8 * 8
+        if Cp != C:
+            xd = F.pad(xd, (0, Cp - C))
+        xd.requires_grad_(True)
+        conv.weight.grad = None
+        d = U.disp_head(xd, conv, scale)
+        d.backward(_nhwc(dd))
+        return _nchw(d), _nchw(xd.grad)[:, :C], conv.weight.grad.cpu()
+
+    d_ref, dx_ref, dw_ref = ref()
+    d_s, dx_s, dw_s = run(True)
+    d_p, dx_p, dw_p = run(False)
+    e_s, e_p = _rel(d_s, d_ref), _rel(d_p, d_ref)
+    assert e_s <= 2e-5, (e_s, e_p)
+    assert e_s < e_p, (e_s, e_p)
+    # backward: dlogit is bf16 in both, the split one sees the f32 weight
+    assert _rel(dx_s, dx_ref) <= 1e-2, _rel(dx_s, dx_ref)
+    assert _rel(dw_s, dw_ref) <= 1e-2, _rel(dw_s, dw_ref)
+    assert _rel(dx_s, dx_ref) <= _rel(dx_p, dx_ref) * 1.5 + 1e-4

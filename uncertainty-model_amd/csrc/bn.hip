@@ -67,6 +67,17 @@ struct FwdFin {
   float *running_mean, *running_var;
   long long* nbt;
   float *mean, *invstd, *scale, *shift;
+  // centred pre-BN output (bf16 y): the conv ran with bias ycen instead of
+  // its own bias, so the slots hold the statistics of y' = y - bias + ycen.
+  // The BN output is the same (it is invariant to a per-channel shift of its
+  // input); mean/invstd/scale/shift are those of y' (what the backward
+  // recomputes xhat from), the running mean gets the true mean
+  // mean' - ycen + bias, and ycen becomes nb - mean' (minus the conv-only mean:
+  // the next step's y' is centred on this step's mean before its bf16
+  // rounding, which otherwise costs |mean| * 2^-9 against a batch std that is
+  // ~1/17 of the mean in smooth layers)
+  float* ycen;
+  const float* bias;
 };
 
 // s_sc / s_sh hold channels [c0, c0 + n) (this block's slice) at [c - c0]
@@ -89,9 +100,15 @@ __device__ __forceinline__ void fwd_fin_coeffs(const FwdFin& f, int C, int c0, i
       f.invstd[c] = invstd;
       f.scale[c] = sc;
       f.shift[c] = sh;
+      float tmean = (float)mean;  // the true mean of this layer's y
+      if (f.ycen != nullptr) {
+        const float nb = f.ycen[c];
+        tmean = (float)mean - nb + (f.bias ? f.bias[c] : 0.f);
+        f.ycen[c] = nb - (float)mean;
+      }
       if (f.running_mean != nullptr) {
         const double unb = count > 1 ? var * count / (count - 1) : var;
-        f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
+        f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * tmean;
         f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unb;
       }
     }
@@ -439,7 +456,8 @@ struct ApplyFin {
   double count;         // <= 0: read after the slots (SyncBN)
   const float* gamma;
   float *dgamma, *dbeta, *dbias;
-  const double* local;  // SyncBN: this rank's slots before the all-reduce (dgamma/dbeta)
+  const double* local;  // SyncBN: this rank's slots before the all-reduce (dgamma/dbeta),
+                        // or null: dgamma/dbeta from the global sums x dbias_scale
   float dbias_scale;    // SyncBN: 1/world (DDP averages the ranks' bias gradients)
 };
 
@@ -457,8 +475,11 @@ __device__ __forceinline__ void apply_fin_coeffs(const ApplyFin& f, int C, int c
     s_k3[c - c0] = (float)(s1 / count);
     if (pub) {
       if (f.local == nullptr) {
-        if (f.dgamma) f.dgamma[c] = (float)s1;
-        if (f.dbeta) f.dbeta[c] = (float)s0;
+        // SyncBN without the local copy: the global sums / world.  DDP
+        // averages the ranks' gradients, so the result equals the average of
+        // the per-rank sums torch SyncBatchNorm uses (dbias_scale = 1 alone)
+        if (f.dgamma) f.dgamma[c] = f.dbias_scale * (float)s1;
+        if (f.dbeta) f.dbeta[c] = f.dbias_scale * (float)s0;
       }
       // conv-bias gradient sum_m dy = k1 (s0 - n k2 - k3 sum xhat), sum xhat = 0
       // (global sums; dbias_scale spreads it over the ranks' gradient average)
@@ -663,10 +684,11 @@ int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const 
                         float momentum, float* running_mean, float* running_var,
                         long long* num_batches_tracked, float* mean, float* invstd, float* scale,
                         float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
-                        hipStream_t st) {
+                        float* ycen, const float* conv_bias, hipStream_t st) {
   UM_CHECK_ARG(slots != nullptr && mean && invstd && scale && shift,
                "um_bn_elu_fwd_slots: slots / coefficient outputs");
   FwdFin fin{};
+  fin.ycen = ycen; fin.bias = conv_bias;
   fin.slots = slots; fin.count = count; fin.gamma = gamma; fin.beta = beta;
   fin.eps = eps; fin.momentum = momentum;
   fin.running_mean = running_mean; fin.running_var = running_var; fin.nbt = num_batches_tracked;
@@ -681,7 +703,8 @@ int um_bn_elu_fwd_slots_merge(int dtype, long M, int C, const void* y, int ldy,
                               float* running_var, long long* num_batches_tracked, float* mean,
                               float* invstd, float* scale, float* shift, void* a, int lda,
                               int apply_elu, int nsrc, const void* const* srcs, const int* widx,
-                              const float* w, int self, void* merged, hipStream_t st) {
+                              const float* w, int self, void* merged, float* ycen,
+                              const float* conv_bias, hipStream_t st) {
   UM_CHECK_ARG(slots != nullptr && mean && invstd && scale && shift,
                "um_bn_elu_fwd_slots_merge: slots / coefficient outputs");
   UM_CHECK_ARG(nsrc >= 2 && nsrc <= FMERGE_MAX && self >= 0 && self < nsrc && srcs && widx &&
@@ -692,6 +715,7 @@ int um_bn_elu_fwd_slots_merge(int dtype, long M, int C, const void* y, int ldy,
   fin.eps = eps; fin.momentum = momentum;
   fin.running_mean = running_mean; fin.running_var = running_var; fin.nbt = num_batches_tracked;
   fin.mean = mean; fin.invstd = invstd; fin.scale = scale; fin.shift = shift;
+  fin.ycen = ycen; fin.bias = conv_bias;
   MergeOut mo{};
   mo.n = nsrc;
   mo.self = self;

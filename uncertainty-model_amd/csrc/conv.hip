@@ -617,21 +617,33 @@ __global__ void __launch_bounds__(256) wgrad_reduce_batch_kernel(WredBatch b) {
 #undef WSEL
 }
 
+// split-bf16 value of a packed row: rows [0, K) the weight rounded to the
+// activation type, rows [K, 2K) (split packs only) its rounding residual, so
+// that a GEMM over both row sets summed in f32 sees the f32 weight to ~2^-17
+template <typename T>
+__device__ __forceinline__ float split_part(float v, bool lo) {
+  return lo ? v - to_f32(from_f32<T>(v)) : v;
+}
+
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ w, int K, int Creal, int R, int C,
-                                   T* __restrict__ wf, T* __restrict__ wT, int ldT, Segs sg) {
-  const long total = (long)K * R * R * C;
+                                   T* __restrict__ wf, T* __restrict__ wT, int ldT, Segs sg,
+                                   int split) {
+  const int K2 = split ? 2 * K : K;
+  const long total = (long)K2 * R * R * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    // i indexes wf [K][R][R][C]
+    // i indexes wf [K2][R][R][C]
     const int c = i % C;
     const int s = (i / C) % R;
     const int r = (i / ((long)C * R)) % R;
-    const int k = i / ((long)C * R * R);
+    const int k2 = i / ((long)C * R * R);
+    const int k = k2 < K ? k2 : k2 - K;
     const int cs = seg_src(sg, c);
-    const float v = cs >= 0 ? w[(((long)k * Creal + cs) * R + r) * R + s] : 0.f;
+    const float v = split_part<T>(cs >= 0 ? w[(((long)k * Creal + cs) * R + r) * R + s] : 0.f,
+                                  k2 >= K);
     if (wf) wf[i] = from_f32<T>(v);
-    if (wT) wT[((long)c * R * R + r * R + s) * ldT + k] = from_f32<T>(v);
+    if (wT) wT[((long)c * R * R + r * R + s) * ldT + k2] = from_f32<T>(v);
   }
 }
 
@@ -1348,10 +1360,10 @@ int um_pack_weight_seg(int dtype, const float* w, int K, int Creal, int R, int C
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, w, K, Creal,
-                       R, C, (bf16_t*)wf, (bf16_t*)wT, ldT, g);
+                       R, C, (bf16_t*)wf, (bf16_t*)wT, ldT, g, 0);
   else
     hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, st, w, K, Creal, R,
-                       C, (float*)wf, (float*)wT, ldT, g);
+                       C, (float*)wf, (float*)wT, ldT, g, 0);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -1360,6 +1372,19 @@ int um_pack_weight(int dtype, const float* w, int K, int Creal, int R, int C, vo
                    int ldT, hipStream_t st) {
   return um_pack_weight_seg(dtype, w, K, Creal, R, C, wf, wT, ldT, 0, nullptr, nullptr, nullptr,
                             st);
+}
+
+int um_pack_weight_split(const float* w, int K, int Creal, int R, int C, void* wf, void* wT,
+                         int ldT, hipStream_t st) {
+  UM_CHECK_ARG(C >= Creal && (wT == nullptr || ldT >= 2 * K), "um_pack_weight_split: C / ldT");
+  Segs g{};
+  UM_CHECK_ARG(make_segs(g, 0, nullptr, nullptr, nullptr, Creal, C), "um_pack_weight_split");
+  const long total = 2L * K * R * R * C;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, w, K, Creal, R,
+                     C, (bf16_t*)wf, (bf16_t*)wT, ldT, g, 1);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
 }
 
 int um_colsum_batch(int dtype, const um_csum_desc* descs, int n, hipStream_t st) {
@@ -1436,12 +1461,14 @@ __device__ __forceinline__ void pack_tile(const um_pack_desc& d, int t, float* t
   constexpr int n = PK * per_k;
   const int nct = (d.C + CT - 1) / CT;
   const int k0 = (t / nct) * PK, c0 = (t % nct) * CT;
+  const int K2 = d.split ? 2 * d.K : d.K;  // packed rows (split: [hi | lo])
   for (int i = threadIdx.x; i < n; i += 256) {
     const int kk = i / per_k, rem = i - kk * per_k;
     const int cc = rem / RR, tap = rem - cc * RR;
-    const int k = k0 + kk, c = c0 + cc;
+    const int k2 = k0 + kk, c = c0 + cc;
+    const int k = k2 < d.K ? k2 : k2 - d.K;
     float v = 0.f;
-    if (k < d.K && c < d.C) {
+    if (k2 < K2 && c < d.C) {
       int cs = -1;
       if (d.nseg <= 0) cs = c < d.Creal ? c : -1;
       else
@@ -1449,7 +1476,7 @@ __device__ __forceinline__ void pack_tile(const um_pack_desc& d, int t, float* t
         for (int g = 0; g < UM_PACK_MAXSEG; ++g)  // static indices: no scratch copy of d
           if (g < d.nseg && c >= d.dst0[g] && c < d.dst0[g] + d.len[g])
             cs = d.src0[g] + c - d.dst0[g];
-      if (cs >= 0) v = d.w[((long)k * d.Creal + cs) * RR + tap];
+      if (cs >= 0) v = split_part<T>(d.w[((long)k * d.Creal + cs) * RR + tap], k2 >= d.K);
     }
     tile[kk * ldt + cc * RR + tap] = v;
   }
@@ -1465,7 +1492,7 @@ __device__ __forceinline__ void pack_tile(const um_pack_desc& d, int t, float* t
       const int kk = i / (per_k / 4), rem = i - kk * (per_k / 4);
       const int tap = rem / (CT / 4), c4 = (rem - tap * (CT / 4)) * 4;
       const int k = k0 + kk, c = c0 + c4;
-      if (k >= d.K || c >= d.C) continue;
+      if (k >= K2 || c >= d.C) continue;
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = tile[kk * ldt + (c4 + e) * RR + tap];
@@ -1477,15 +1504,15 @@ __device__ __forceinline__ void pack_tile(const um_pack_desc& d, int t, float* t
       const int cc = i / (RR * PK / 8), rem = i - cc * (RR * PK / 8);
       const int tap = rem / (PK / 8), k8 = (rem - tap * (PK / 8)) * 8;
       const int k = k0 + k8, c = c0 + cc;
-      if (c >= d.C || k >= d.K) continue;
+      if (c >= d.C || k >= K2) continue;
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = tile[(k8 + e) * ldt + cc * RR + tap];
       T* o = wT + ((long)c * RR + tap) * d.ldT + k;
-      if (vec && k + 8 <= d.K) {
+      if (vec && k + 8 <= K2) {
         store8(o, v);
       } else {
-        for (int e = 0; e < 8 && k + e < d.K; ++e) o[e] = from_f32<T>(v[e]);
+        for (int e = 0; e < 8 && k + e < K2; ++e) o[e] = from_f32<T>(v[e]);
       }
     }
   }
@@ -1515,6 +1542,8 @@ extern "C" int um_pack_tiles(int K, int C, int R) {
 extern "C" int um_pack_batch(int dtype, const um_pack_desc* table, int ndesc,
                              const int* blk2desc, int nblocks, hipStream_t st) {
   UM_CHECK_ARG(table != nullptr && blk2desc != nullptr && ndesc > 0, "um_pack_batch: table");
+  // (split descriptors are bf16-only; the table is device memory, so the
+  // binding checks that: umamd/packer.py)
   if (nblocks <= 0) return UM_OK;
   if (dtype == UM_BF16)
     hipLaunchKernelGGL(pack_batch_kernel<bf16_t>, dim3(nblocks), dim3(256), 0, st, table,

@@ -196,8 +196,10 @@ __global__ void axpy_kernel(long n, float alpha, const T* __restrict__ x, T* __r
     y[i] = from_f32<T>(to_f32(y[i]) + alpha * to_f32(x[i]));
 }
 
-// dlogit[m][c] = dd[m][c] * d * (1 - d/scale) for c < C; channels [C, ldo) zeroed
-template <typename T>
+// dlogit[m][c] = dd[m][c] * d * (1 - d/scale) for c < C (SPLIT: also at
+// C + c, the split-bf16 head's residual rows); the other channels of [0, ldo)
+// zeroed
+template <typename T, bool SPLIT>
 __global__ void sigmoid_scale_bwd_kernel(long M, int C, const float* __restrict__ d, int ldd,
                                          const float* __restrict__ dd, int lddd, float scale,
                                          T* __restrict__ dlogit, int ldo) {
@@ -205,13 +207,28 @@ __global__ void sigmoid_scale_bwd_kernel(long M, int C, const float* __restrict_
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     const long m = i / ldo;
-    const int c = i - m * ldo;
+    int c = i - m * ldo;
+    if (SPLIT && c >= C && c < 2 * C) c -= C;
     float v = 0.f;
     if (c < C) {
       const float dv = d[m * ldd + c];
       v = dd[m * lddd + c] * dv * (1.f - dv / scale);
     }
     dlogit[i] = from_f32<T>(v);
+  }
+}
+
+// the split-bf16 head's forward finish (um_head_split_fin)
+__global__ void head_split_fin_kernel(long M, int K, const float* __restrict__ z, int ldz,
+                                      const float* __restrict__ bias, float scale,
+                                      float* __restrict__ d, int ldd) {
+  const long total = M * K;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long m = i / K;
+    const int k = i - m * K;
+    const float* zr = z + m * ldz;
+    d[m * ldd + k] = scale * sigmoidf_(zr[k] + zr[K + k] + (bias ? bias[k] : 0.f));
   }
 }
 
@@ -323,11 +340,35 @@ int um_sigmoid_scale_bwd(int dtype, long M, int C, const float* d, int ldd, cons
                          int lddd, float scale, void* dlogit, int ldo, hipStream_t st) {
   const long total = M * ldo;
   if (dtype == UM_BF16)
-    hipLaunchKernelGGL(sigmoid_scale_bwd_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st,
-                       M, C, d, ldd, dd, lddd, scale, (bf16_t*)dlogit, ldo);
+    hipLaunchKernelGGL((sigmoid_scale_bwd_kernel<bf16_t, false>), dim3(grid_for(total)), dim3(256),
+                       0, st, M, C, d, ldd, dd, lddd, scale, (bf16_t*)dlogit, ldo);
   else
-    hipLaunchKernelGGL(sigmoid_scale_bwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, M,
-                       C, d, ldd, dd, lddd, scale, (float*)dlogit, ldo);
+    hipLaunchKernelGGL((sigmoid_scale_bwd_kernel<float, false>), dim3(grid_for(total)), dim3(256),
+                       0, st, M, C, d, ldd, dd, lddd, scale, (float*)dlogit, ldo);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_sigmoid_scale_bwd_split(int dtype, long M, int C, const float* d, int ldd, const float* dd,
+                               int lddd, float scale, void* dlogit, int ldo, hipStream_t st) {
+  UM_CHECK_ARG(ldo >= 2 * C, "um_sigmoid_scale_bwd_split: ldo < 2C");
+  const long total = M * ldo;
+  if (dtype == UM_BF16)
+    hipLaunchKernelGGL((sigmoid_scale_bwd_kernel<bf16_t, true>), dim3(grid_for(total)), dim3(256),
+                       0, st, M, C, d, ldd, dd, lddd, scale, (bf16_t*)dlogit, ldo);
+  else
+    hipLaunchKernelGGL((sigmoid_scale_bwd_kernel<float, true>), dim3(grid_for(total)), dim3(256),
+                       0, st, M, C, d, ldd, dd, lddd, scale, (float*)dlogit, ldo);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_head_split_fin(long M, int K, const float* z, int ldz, const float* bias, float scale,
+                      float* d, int ldd, hipStream_t st) {
+  UM_CHECK_ARG(ldz >= 2 * K && ldd >= K, "um_head_split_fin: ld");
+  const long total = M * K;
+  hipLaunchKernelGGL(head_split_fin_kernel, dim3(grid_for(total)), dim3(256), 0, st, M, K, z, ldz,
+                     bias, scale, d, ldd);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

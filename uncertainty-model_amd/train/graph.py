@@ -38,7 +38,6 @@ stream (``stream=``).
 from __future__ import annotations
 
 import os
-import time
 
 import torch
 from torch import distributed as dist
@@ -46,6 +45,7 @@ from torch.nn.parallel import DistributedDataParallel
 
 from umamd import lossfn as LF
 from umamd import overlap
+from umamd import rccl
 from umamd.gradsync import GradBuckets
 
 from . import utils as u
@@ -78,6 +78,14 @@ class CapturedTrainStep:
             mb = float(os.environ.get('UMAMD_GRAD_BUCKET_MB', '16'))
             self._buckets = GradBuckets(model.parameters(), self.group, self.world,
                                         cap_mb=mb if mb > 0 else 1e9)
+        # RCCL collectives of the step (SyncBN, gradient buckets) through the
+        # step's own communicator on the launch stream (umamd.rccl: no process
+        # group watchdog polling events of a capturing stream, no stream hop);
+        # UMAMD_OWN_RCCL=0 keeps the process group
+        self._comm = None
+        if self.group is not None and dist.get_backend(self.group) == 'nccl' and \
+                os.environ.get('UMAMD_OWN_RCCL', '1') != '0':
+            self._comm = rccl.comms_for(self.group)
         snap = self._snapshot(model, optimiser) if restore_state else None
         self.model, self.loss_function, self.optimiser = model, loss_function, optimiser
         self.scale, self.scales = float(scale), scales
@@ -92,22 +100,28 @@ class CapturedTrainStep:
         side = stream if stream is not None else torch.cuda.Stream()
         if side != cur:
             side.wait_stream(cur)
-        with torch.cuda.stream(side):
+        with torch.cuda.stream(side), rccl.use(self._comm):
             for _ in range(warmup):  # eager steps: allocator warm-up, optimiser state
                 optimiser.zero_grad(set_to_none=True)
                 self._fwd_bwd()
                 optimiser.step()
         cur.wait_stream(side)
         torch.cuda.synchronize()
-        self._drain_watchdog()
         optimiser.zero_grad(set_to_none=True)
         # capture on the warm-up stream so autograd's cached AccumulateGrad
-        # nodes see the stream they were created on
-        # the backward (autograd's device thread) launches into the capture
-        # too; the process group's watchdog is drained first (_drain_watchdog)
-        mode = os.environ.get('UMAMD_CAPTURE_MODE', 'global')
+        # nodes see the stream they were created on; the backward (autograd's
+        # device thread) launches into the capture too.
+        # Data parallel: the step's collectives go through its own RCCL
+        # communicator (umamd.rccl), so the process group's watchdog never
+        # polls an event of a stream that joins the capture; the capture is
+        # 'thread_local' all the same, so that its event queries (of earlier
+        # eager collectives: DDP's parameter broadcast, the id exchange) are
+        # never refused.  UMAMD_CAPTURE_MODE overrides.
+        mode = os.environ.get('UMAMD_CAPTURE_MODE',
+                              'thread_local' if self.group is not None else 'global')
         self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb, stream=side, capture_error_mode=mode):
+        with torch.cuda.graph(self.g_fb, stream=side, capture_error_mode=mode), \
+                rccl.use(self._comm):
             self.disp_loss, self.error_loss = self._fwd_bwd()
         # the returned losses are static graph outputs; detached, they keep no
         # autograd graph alive (its AccumulateGrad nodes remember the capture
@@ -124,16 +138,6 @@ class CapturedTrainStep:
             optimiser.step()
         if snap is not None:
             self._restore(model, optimiser, snap)
-
-    def _drain_watchdog(self):
-        """Let the process group's watchdog retire the warm-up collectives
-        before capturing: it polls the end events of outstanding work, and
-        HIP refuses (and invalidates the capture on) a query of an event
-        whose stream is capturing -- the RCCL stream joins the capture at
-        the first recorded collective.  Measured on MI355X: 0.5 s suffices;
-        without it the capture fails at random."""
-        if self.group is not None:
-            time.sleep(float(os.environ.get('UMAMD_CAPTURE_DRAIN_S', '1.0')))
 
     @staticmethod
     @torch.no_grad()
@@ -202,6 +206,18 @@ class CapturedTrainStep:
         if self._buckets is None:
             self._buckets = GradBuckets(self.model.parameters(), self.group, self.world)
         self._buckets.finish()
+
+    def close(self):
+        """Release what ties this step to the model: the gradient buckets'
+        post-accumulate-grad hooks (each would keep this step's flat buffer,
+        its raw gradients and its stream alive, and run on every later
+        backward) and the graphs.  train.train._GraphSteps calls it before a
+        recapture."""
+        if self._buckets is not None:
+            self._buckets.remove()
+            self._buckets = None
+        self.g_fb = self.g_opt = None
+        self._opt_tables = []
 
     def __call__(self, left=None, right=None):
         if left is not None:

@@ -140,7 +140,9 @@ class _GraphSteps:
             return None  # another batch shape: the caller steps eagerly
         self.optimiser.sync_lr()
         if self.key != key:
-            self.cap = None  # scale changed: drop the old graphs before capturing
+            if self.cap is not None:  # scale changed: drop the old graphs before capturing
+                self.cap.close()
+            self.cap = None
             torch.cuda.synchronize()
             self.cap = CapturedTrainStep(self.model, self.loss_function, self.optimiser, left,
                                          right, scale, scales=self.scales, stream=self.stream)
@@ -188,12 +190,12 @@ def train_one_epoch(model: Module, loader: DataLoader, loss_function: Module,
             with torch.cuda.stream(graphs.stream):
                 disp_loss, error_loss, disc_loss = train_step(
                     model, left, right, loss_function, model_optimiser, scale, scales, i, disc,
-                    disc_clone, disc_optimiser, disc_loss_function, batch_size=loader.batch_size)
+                    disc_clone, disc_optimiser, disc_loss_function, batch_size=batch_size)
             cur.wait_stream(graphs.stream)
         else:
             disp_loss, error_loss, disc_loss = train_step(
                 model, left, right, loss_function, model_optimiser, scale, scales, i, disc,
-                disc_clone, disc_optimiser, disc_loss_function, batch_size=loader.batch_size)
+                disc_clone, disc_optimiser, disc_loss_function, batch_size=batch_size)
         if rank == 0:
             running_disp_loss += disp_loss.item()
             running_error_loss += error_loss.item()

@@ -101,9 +101,10 @@ _SIG = {
     'um_bn_fwd_pool_parts_c': (_I, [_L, _L, _I]),
     'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, _L, _P, 's']),
     'um_bn_elu_fwd_slots': (_I, [_I, _L, _I, _P, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P, _P, _P,
-                                 _P, _P, _P, _I, _I, _L, _P, 's']),
+                                 _P, _P, _P, _I, _I, _L, _P, _P, _P, 's']),
     'um_bn_elu_fwd_slots_merge': (_I, [_I, _L, _I, _P, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P,
-                                       _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, 's']),
+                                       _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P,
+                                       _P, 's']),
     'um_bn_elu_bwd_reduce_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
                                         _P, 's']),
     'um_bn_elu_bwd_apply_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
@@ -125,6 +126,9 @@ _SIG = {
     'um_image_to_nhwc': (_I, [_I, _P, _I, _I, _I, _I, _I, _P, 's']),
     'um_axpy': (_I, [_I, _L, _F, _P, _P, 's']),
     'um_sigmoid_scale_bwd': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
+    'um_sigmoid_scale_bwd_split': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
+    'um_head_split_fin': (_I, [_L, _I, _P, _I, _P, _F, _P, _I, 's']),
+    'um_pack_weight_split': (_I, [_P, _I, _I, _I, _I, _P, _P, _I, 's']),
     'um_attn_ws_kstats': (_L, [_I, _I, _I]),
     'um_attn_ws_ctx': (_L, [_I, _I, _I, _I]),
     'um_attn_ws_tiles': (_L, [_I, _I, _I, _I]),

@@ -31,6 +31,7 @@ import torch.distributed as dist
 from . import _lib as L
 from . import overlap as _overlap
 from . import packer as _packer
+from . import rccl as _rccl
 from ._lib import call, ptr, query
 
 
@@ -52,12 +53,23 @@ def _seg_arrays(segs):
 
 
 def _pack(weight: torch.Tensor, Cp: int, dtype: torch.dtype, wf=True, wT=True, ldT=None,
-          segs=None):
+          segs=None, split=False):
     """Repack an NCHW f32 conv weight to [K][R][R][Cp] and [Cp][R][R][ldT];
-    ``segs`` = [(ref_c0, packed_c0, len)] places input-channel ranges."""
+    ``segs`` = [(ref_c0, packed_c0, len)] places input-channel ranges.
+    ``split`` (bf16): 2K rows, the weight then its bf16 rounding residual
+    (um_pack_weight_split)."""
     pk = _packer.active()
     if pk is not None:
-        return pk.pack(weight, Cp, dtype, wf=wf, wT=wT, ldT=ldT, segs=segs)
+        return pk.pack(weight, Cp, dtype, wf=wf, wT=wT, ldT=ldT, segs=segs, split=split)
+    if split:
+        K, Creal, R, _ = weight.shape
+        ldT = ldT or 2 * K
+        w = weight.detach().float().contiguous()
+        f = torch.empty((2 * K, R, R, Cp), dtype=dtype, device=w.device) if wf else None
+        t = (torch.zeros if ldT != 2 * K else torch.empty)((Cp, R, R, ldT), dtype=dtype,
+                                                            device=w.device) if wT else None
+        call('um_pack_weight_split', ptr(w), K, Creal, R, Cp, ptr(f), ptr(t), ldT)
+        return f, t
     K, Creal, R, _ = weight.shape
     ldT = ldT or K
     w = weight.detach()
@@ -133,7 +145,8 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
     else:
         launch = lambda: _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad,  # noqa: E731
                                         pad_mode, dw_ptr, segs)
-    ov.defer((x, dy), launch, out_ptr=dw_ptr, flop=_conv_flops(N, P, Q, Kreal, R, Creal))
+    ov.defer((x, dy), launch, out_ptr=dw_ptr, flop=_conv_flops(N, P, Q, Kreal, R, Creal),
+             out_bytes=dw.numel() * 4)
     return dw
 
 
@@ -242,7 +255,7 @@ def _param_grad(tensors, out, launch):
         launch()
         return out
     out.record_stream(ov.stream)
-    ov.defer(tensors, launch, out_ptr=out.data_ptr())
+    ov.defer(tensors, launch, out_ptr=out.data_ptr(), out_bytes=out.numel() * out.element_size())
     return out
 
 
@@ -292,13 +305,38 @@ _BN_SLOTS = os.environ.get('UMAMD_BN_SLOTS', '1') == '1'
 #  - the pre-BN conv output y stored in the activation dtype (bf16) instead of
 #    f32, as a bf16 autocast conv feeding BatchNorm2d: the conv epilogue still
 #    takes the statistics from its f32 accumulators; the three BN passes and
-#    the conv's store move 2 bytes per element less
-_Y_ACT = os.environ.get('UMAMD_Y_ACT', '1') == '1'
+#    the conv's store move 2 bytes per element less.  OFF by default since
+#    round 4: +2.3 % throughput (790 -> 808 pairs/s, round 3), but the
+#    step-0 error loss at BASELINE config 2 moves 4.7e-3 from the reference
+#    with bf16 y against 1.9e-3 with f32 y (3.6e-3 with the centring below;
+#    tools/bf16_arms.py, profiles/r04/bf16_arms.txt): in the smooth layers the
+#    batch std is ~1/17 of the mean, so the rounding of y is ~17x larger
+#    relative to the normalised x-hat than the rounding of the activations
+_Y_ACT = os.environ.get('UMAMD_Y_ACT', '0') == '1'
 
 
 def _ydtype(dt):
     """storage dtype of the pre-BN conv output for activations of ``dt``"""
     return dt if (_Y_ACT and dt == torch.bfloat16) else torch.float32
+
+
+_Y_CENTER = os.environ.get('UMAMD_Y_CENTER', '1') == '1'
+
+
+def _ycen(bn, K, dev):
+    """The BN layer's centring buffer for its bf16 pre-BN output ([K] f32,
+    persistent on the module, not in its state_dict; see um_bn_elu_fwd_slots):
+    the conv runs with it as its bias, and the BN pass sets it to minus the
+    conv-only batch mean for the next step.  Any value gives the same BN
+    output; a centred y keeps its bf16 rounding error relative to the batch
+    std instead of the mean.  None with UMAMD_Y_CENTER=0."""
+    if not _Y_CENTER:
+        return None
+    t = getattr(bn, '_umamd_ycen', None)
+    if t is None or t.numel() != K or t.device != dev:
+        t = torch.zeros(K, dtype=torch.float32, device=dev)
+        bn._umamd_ycen = t
+    return t
 
 
 def _ydt(a, y):
@@ -488,7 +526,11 @@ class BNSync:
 
     def all_reduce(self, t: torch.Tensor):
         if self.collective:
-            dist.all_reduce(t, group=self.group)
+            c = _rccl.active(self.group, 'bn')  # the captured step's own communicator
+            if c is not None:
+                c.all_reduce(t)
+            else:
+                dist.all_reduce(t, group=self.group)
 
 
 def _bn_forward_coeffs(parts, nparts, K, count, bn, sync: BNSync, training: bool, device):
@@ -555,7 +597,7 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
     -> (outputs tuple, _CBEState).  ``merge`` = (srcs with None for this
     layer's output, widx, mean_weight): also compute that NodeBlock merge
     (fused into the BN apply pass where the statistics slots are used), the
-    result in ``state.merged``.  ``yconv(epi, stats)`` replaces the conv
+    result in ``state.merged``.  ``yconv(epi, stats, bias)`` replaces the conv
     (it returns the f32 pre-BN output; the state then saves no packed
     weights: its backward brings its own conv part, see skip_conv_bn_elu)."""
     ctx = _CBEState()
@@ -584,9 +626,13 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
         nslot = L.STAT_SLOTS * K * 2
         slots_f = _ARENA.take(nslot + 1)
         slots_b = _ARENA.take(nslot + 1)
-        y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
+        # a bf16 y is stored centred: the conv's bias is the layer's ycen
+        # buffer (minus the last step's conv-only mean), see um_bn_elu_fwd_slots
+        ycen = _ycen(bn, K, dev) if _ydtype(x.dtype) != torch.float32 else None
+        cbias = ycen if ycen is not None else bias_f
+        y = _conv_fwd(x, wf, cbias, K, R, spec.stride, spec.pad, spec.pad_mode,
                       out_dtype=_ydtype(x.dtype), epi=L.EPI_STAT_SLOTS, stats=slots_f,
-                      creal=Creal) if yconv is None else yconv(L.EPI_STAT_SLOTS, slots_f)
+                      creal=Creal) if yconv is None else yconv(L.EPI_STAT_SLOTS, slots_f, cbias)
         if sync.collective:  # the conv stored this rank's count after the slots
             sync.all_reduce(slots_f)
             count = -1.0  # read the all-reduced count after the slots
@@ -600,7 +646,7 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
         epi = L.EPI_STATS if training else L.EPI_NONE
         y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
                       out_dtype=_ydtype(x.dtype), epi=epi, stats=parts, creal=Creal) \
-            if yconv is None else yconv(epi, parts)
+            if yconv is None else yconv(epi, parts, bias_f)
         mean, invstd, scale, shift = _bn_forward_coeffs(parts, nparts, K, M, bn, sync,
                                                         training, dev)
     else:  # ConvELUBlock(batch_norm=False): identity normalisation
@@ -608,7 +654,7 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
         training = False
         y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
                       out_dtype=_ydtype(x.dtype), creal=Creal) if yconv is None \
-            else yconv(L.EPI_NONE, None)
+            else yconv(L.EPI_NONE, None, bias_f)
         mean = shift = _const_vec(0.0, K, dev)
         invstd = scale = _const_vec(1.0, K, dev)
     a = torch.empty(y.shape, dtype=x.dtype, device=dev)  # y: pre-BN, f32 or bf16 (_ydtype)
@@ -630,12 +676,13 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
                  ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K, int(spec.elu), n,
                  (ctypes_p * n)(*[t.data_ptr() if t is not None else None for t in msrcs]),
-                 (ctypes_i * n)(*mwidx), ptr(mw), msrcs.index(None), ptr(merged))
+                 (ctypes_i * n)(*mwidx), ptr(mw), msrcs.index(None), ptr(merged), ptr(ycen),
+                 ptr(bias_f))
         else:
             call('um_bn_elu_fwd_slots', _ydt(a, y), M, K, ptr(y), K, ptr(slots_f), count,
                  ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K,
-                 int(spec.elu), P * Q, ptr(pool))
+                 int(spec.elu), P * Q, ptr(pool), ptr(ycen), ptr(bias_f))
     else:
         call('um_bn_elu_fwd', _ydt(a, y), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
              int(spec.elu), P * Q, ptr(pool))
@@ -669,6 +716,9 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
     ctx.se = se
     ctx.saved = (x, wT, y, mean, invstd, scale, shift, gamma, w1, w2)
     return tuple(outs), ctx
+
+
+_SYNCBN_LOCAL = os.environ.get('UMAMD_SYNCBN_LOCAL', '0') == '1'
 
 
 def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=False,
@@ -713,9 +763,13 @@ def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=
              ptr(slots_b))
         local, bcount, bscale = None, float(M), 1.0
         if ctx.sync is not None and ctx.sync.collective:
-            # dgamma/dbeta from this rank's sums (torch SyncBatchNorm),
-            # k1..k3 and the conv-bias gradient from the global ones
-            local = slots_b.clone()  # the reduce kernel stored the count after the slots
+            # k1..k3 from the global sums.  dgamma/dbeta and the conv-bias
+            # gradient: the global sums / world, whose DDP average equals the
+            # average of torch SyncBatchNorm's per-rank sums -- no copy of
+            # this rank's slots before the in-place all-reduce (one launch
+            # per layer less); UMAMD_SYNCBN_LOCAL=1 keeps the per-rank sums
+            if _SYNCBN_LOCAL:
+                local = slots_b.clone()  # the reduce kernel stored the count after the slots
             ctx.sync.all_reduce(slots_b)
             bcount, bscale = -1.0, 1.0 / ctx.sync.world
     elif ctx.has_bn:
@@ -864,11 +918,10 @@ class SkipConvFn(torch.autograd.Function):
         wf_f, wT_f = _pack(weight, Cf, dt, segs=[(0, 0, fin)])
         ydt = _ydtype(dt)
         z = _conv_fwd(gs, wf_s, None, K, 1, 1, 0, L.PAD_ZERO, out_dtype=ydt, creal=skin)
-        bias_f = bias.detach().float().contiguous() if bias is not None else None
 
-        def yconv(epi, stats):
+        def yconv(epi, stats, cbias):
             y = torch.empty((N, H, W, K), dtype=ydt, device=fm.device)
-            call('um_conv2d_fwd_up2', _dt(fm) | (L.Y_ACT if ydt != torch.float32 else 0), N, H, W, Cf, Cf, ptr(fm), ptr(wf_f), ptr(bias_f),
+            call('um_conv2d_fwd_up2', _dt(fm) | (L.Y_ACT if ydt != torch.float32 else 0), N, H, W, Cf, Cf, ptr(fm), ptr(wf_f), ptr(cbias),
                  K, H, W, ptr(y), K, epi, ptr(stats), ptr(z), h, w, K,
                  work=_conv_flops(N, H, W, K, 1, fin))  # the z conv is its own launch
             return y
@@ -1379,17 +1432,42 @@ def concat(sources: Sequence[CatSource], N, H, W, dtype):
 
 
 # ---------------------------------------------------------------- disp head --
+# the heads' weights in split bf16 (hi + lo rows, um_pack_weight_split): the
+# bf16 rounding of these 4-output weights moves the uncertainty sigma of
+# every pixel the same way (a systematic error; the activation roundings
+# average out over the pixels), and the Laplacian NLL e/sigma + log sigma is
+# as sensitive to it as to sigma itself.  Measured at BASELINE config 2
+# (tools/bf16_arms.py, step-0 error loss vs the reference): 1.9e-3 -> 1.2e-3.
+# The 4 outputs pad to 8 GEMM columns anyway, so the split rows are free.
+_SPLIT_HEAD = os.environ.get('UMAMD_SPLIT_HEAD', '1') == '1'
+
+
 class DispHeadFn(torch.autograd.Function):
+    """disp = scale * sigmoid(Conv3x3reflect(x)) (reference
+    model/layers/decoder.py:244-247), all 4 channels."""
+
     @staticmethod
     def forward(ctx, x, weight, bias, scale: float):
         N, H, W, Cp = x.shape
         K, Creal, R, _ = weight.shape
         Kp = ceil8(K)
-        wf, wT = _pack(weight, Cp, x.dtype, ldT=Kp)
-        d = _conv_fwd(x, wf, bias.detach().float().contiguous(), K, R, 1, 1, L.PAD_REFLECT,
-                      out_dtype=torch.float32, epi=L.EPI_SIGMOID_SCALE, epi_scale=scale,
-                      creal=Creal)
+        split = _SPLIT_HEAD and x.dtype == torch.bfloat16 and 2 * K <= Kp
+        bias_f = bias.detach().float().contiguous()
+        if split:
+            wf, wT = _pack(weight, Cp, x.dtype, ldT=Kp, split=True)
+            z = _conv_fwd(x, wf, None, 2 * K, R, 1, 1, L.PAD_REFLECT, out_dtype=torch.float32,
+                          creal=Creal)
+            d = torch.empty((N, H, W, K), dtype=torch.float32, device=x.device)
+            call('um_head_split_fin', N * H * W, K, ptr(z), 2 * K, ptr(bias_f), float(scale),
+                 ptr(d), K)
+            # the GEMM's algorithmic work is the 4-output conv (the split
+            # rows are padding columns of the same MFMA tiles)
+        else:
+            wf, wT = _pack(weight, Cp, x.dtype, ldT=Kp)
+            d = _conv_fwd(x, wf, bias_f, K, R, 1, 1, L.PAD_REFLECT, out_dtype=torch.float32,
+                          epi=L.EPI_SIGMOID_SCALE, epi_scale=scale, creal=Creal)
         ctx.scale = float(scale)
+        ctx.split = split
         _use(ctx, x)
         ctx.save_for_backward(x, wT, d)
         ctx.geom = (K, Kp, Creal, R)
@@ -1403,10 +1481,12 @@ class DispHeadFn(torch.autograd.Function):
         dd = dd.contiguous().float()
         M = N * H * W
         dl = torch.empty((N, H, W, Kp), dtype=x.dtype, device=x.device)
-        call('um_sigmoid_scale_bwd', _dt(dl), M, K, ptr(d), K, ptr(dd), dd.shape[-1], ctx.scale,
-             ptr(dl), Kp)
-        dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)
-        db = _colsum_grad(dl, Kp)[:K]  # channels K..Kp of dl are zero
+        # split: dlogit also in channels K..2K-1, so that the data gradient
+        # over the split rows of wT sums dl (w_hi + w_lo)
+        call('um_sigmoid_scale_bwd_split' if ctx.split else 'um_sigmoid_scale_bwd', _dt(dl), M,
+             K, ptr(d), K, ptr(dd), dd.shape[-1], ctx.scale, ptr(dl), Kp)
+        dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)  # rows K.. unused
+        db = _colsum_grad(dl, Kp)[:K]  # channels K..Kp of dl are zero or a copy
         dx = None
         if ctx.needs_input_grad[0]:
             tgt = _slot(ctx, 0)

@@ -34,6 +34,7 @@ import torch
 from torch import distributed as dist
 
 from . import overlap as _overlap
+from . import rccl as _rccl
 
 
 class GradBuckets:
@@ -116,7 +117,8 @@ class GradBuckets:
         b = self.buckets[bi]
         if any(id(p) not in self.ready for p in b):
             return
-        if self.ov is not None and self.ov.is_pending(p.grad.data_ptr() for p in b):
+        if self.ov is not None and self.ov.is_pending(
+                (p.grad.data_ptr(), p.grad.numel() * p.grad.element_size()) for p in b):
             return  # written by a queued side-stream launch: wait for its flush
         self._launch(bi)
 
@@ -142,7 +144,10 @@ class GradBuckets:
 
     def _reduce(self, dst, grads):
         torch.cat([g.reshape(-1) for g in grads], out=dst)
-        if dist.get_backend(self.group) == 'nccl':
+        c = _rccl.active(self.group, 'grad')  # the captured step's own communicator
+        if c is not None:
+            c.all_reduce(dst, average=True)
+        elif dist.get_backend(self.group) == 'nccl':
             dist.all_reduce(dst, op=dist.ReduceOp.AVG, group=self.group)
         else:
             dist.all_reduce(dst, group=self.group)

@@ -48,7 +48,7 @@ class WgradStream:
         self._queued_flop = 0.0
         self._launch = None
         self._pending = []
-        self._pending_out = set()
+        self._pending_out = []
         self._on_flush = []
 
     def __enter__(self):
@@ -61,24 +61,33 @@ class WgradStream:
         WgradStream._active = self
         return self
 
-    def defer(self, tensors, launch, out_ptr=None, flop=0.0):
+    def defer(self, tensors, launch, out_ptr=None, flop=0.0, out_bytes=1):
         """Queue one weight gradient (``launch`` issues its kernels on the
-        current stream; ``tensors`` are the ones it touches, ``out_ptr`` the
-        address it writes, ``flop`` its work) and flush the queue onto the
+        current stream; ``tensors`` are the ones it touches, ``out_ptr`` /
+        ``out_bytes`` the byte range it writes, ``flop`` its work) and flush
+        the queue onto the
         side stream every ``batch`` entries (or ``flush_flop`` of work): one
         fork per batch instead of one per conv."""
         self._pending.append((tensors, launch))
         self._queued_flop += flop
         if out_ptr is not None:
-            self._pending_out.add(out_ptr)
+            self._pending_out.append((out_ptr, out_ptr + max(int(out_bytes), 1)))
         if len(self._pending) >= self.batch or \
                 (self.flush_flop > 0 and self._queued_flop >= self.flush_flop):
             self._flush()
 
-    def is_pending(self, ptrs) -> bool:
-        """True if any of these addresses is written by a queued launch
-        that has not been flushed onto the side stream yet"""
-        return any(p in self._pending_out for p in ptrs)
+    def is_pending(self, spans) -> bool:
+        """True if any of these (address, bytes) spans overlaps a range
+        written by a queued launch that has not been flushed onto the side
+        stream yet.  Ranges, not base addresses: a gradient may be a view into
+        a larger deferred output (the attention's K/V slices of the fused QKV
+        weight gradient, functional.AttentionFn.backward)."""
+        for p, n in spans:
+            e = p + max(int(n), 1)
+            for a, b in self._pending_out:
+                if p < b and a < e:
+                    return True
+        return False
 
     def on_flush(self, fn):
         """call ``fn()`` after every flush of this context (gradsync: a

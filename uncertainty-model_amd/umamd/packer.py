@@ -35,7 +35,8 @@ class PackDesc(ctypes.Structure):
                 ('K', ctypes.c_int), ('Creal', ctypes.c_int), ('R', ctypes.c_int),
                 ('C', ctypes.c_int), ('ldT', ctypes.c_int), ('block0', ctypes.c_int),
                 ('nseg', ctypes.c_int), ('src0', ctypes.c_int * MAXSEG),
-                ('dst0', ctypes.c_int * MAXSEG), ('len', ctypes.c_int * MAXSEG)]
+                ('dst0', ctypes.c_int * MAXSEG), ('len', ctypes.c_int * MAXSEG),
+                ('split', ctypes.c_int)]
 
 
 def _tiles(K, C, R):
@@ -89,7 +90,7 @@ class WeightPacker:
         for dt, ds in by_dt.items():
             arr = (PackDesc * len(ds))()
             blk = []
-            for i, (w, wf, wT, K, Creal, R, C, ldT, segs, _) in enumerate(ds):
+            for i, (w, wf, wT, K, Creal, R, C, ldT, segs, split, _) in enumerate(ds):
                 e = arr[i]
                 e.w, e.wf, e.wT = w.data_ptr(), wf, wT
                 e.K, e.Creal, e.R, e.C, e.ldT = K, Creal, R, C, ldT
@@ -97,7 +98,8 @@ class WeightPacker:
                 e.nseg = len(segs) if segs else 0
                 for j, (a, b, n) in enumerate(segs or []):
                     e.src0[j], e.dst0[j], e.len[j] = a, b, n
-                blk += [i] * _tiles(K, C, R)
+                e.split = int(split)
+                blk += [i] * _tiles(2 * K if split else K, C, R)
             dev = ds[0][0].device
             raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
             table = raw.to(dev)
@@ -107,26 +109,32 @@ class WeightPacker:
 
     # ---------------------------------------------------------------- sites --
     def pack(self, weight: torch.Tensor, Cp: int, dtype: torch.dtype, wf=True, wT=True,
-             ldT: Optional[int] = None, segs=None):
+             ldT: Optional[int] = None, segs=None, split: bool = False):
+        """``split`` (bf16): 2K packed rows, the weight and its bf16 rounding
+        residual (um_pack_weight_split)"""
         K, Creal, R, _ = weight.shape
-        ldT = ldT or K
+        K2 = 2 * K if split else K
+        ldT = ldT or K2
+        if split and (dtype != torch.bfloat16 or segs):
+            raise ValueError('split packing: bf16 without segments only')
         key = ('w', weight.data_ptr(), tuple(weight.shape), Cp, dtype, ldT,
-               tuple(segs) if segs else None, bool(wf), bool(wT))
+               tuple(segs) if segs else None, bool(wf), bool(wT), bool(split))
         e = self.entries.get(key)
         if e is not None and self.batched and key in self.registered:
             return e
         w = _f32(weight)
         if e is None:
-            f = torch.empty((K, R, R, Cp), dtype=dtype, device=w.device) if wf else None
+            f = torch.empty((K2, R, R, Cp), dtype=dtype, device=w.device) if wf else None
             t = None
             if wT:
-                t = (torch.zeros if ldT != K else torch.empty)((Cp, R, R, ldT), dtype=dtype,
-                                                                device=w.device)
+                t = (torch.zeros if ldT != K2 else torch.empty)((Cp, R, R, ldT), dtype=dtype,
+                                                                 device=w.device)
             e = (f, t)
-            if self._register(weight, w, ptr(f), ptr(t), K, Creal, R, Cp, ldT, segs, dtype):
+            if self._register(weight, w, ptr(f), ptr(t), K, Creal, R, Cp, ldT, segs, dtype,
+                              split):
                 self.registered.add(key)
             self.entries[key] = e
-        _pack_one(w, e[0], e[1], Cp, ldT, segs, dtype)
+        _pack_one(w, e[0], e[1], Cp, ldT, segs, dtype, split)
         return e
 
     def pack_rows(self, weights, C: int, dtype: torch.dtype):
@@ -179,14 +187,14 @@ class WeightPacker:
         torch.cat([_f32(b) for b in biases], out=e)
         return e
 
-    def _register(self, weight, w32, wf, wT, K, Creal, R, C, ldT, segs, dtype):
+    def _register(self, weight, w32, wf, wT, K, Creal, R, C, ldT, segs, dtype, split=False):
         if w32.data_ptr() != weight.data_ptr():
             # the batch reads the parameter memory directly: only f32 contiguous params
             return False
         if R not in (1, 3, 5, 7):  # pack_batch_kernel's compile-time filter sizes
             return False
         self.descs.append((weight, wf, wT, K, Creal, R, C, ldT, list(segs) if segs else None,
-                           weight.data_ptr(), L.dtype_code(dtype)))
+                           bool(split), weight.data_ptr(), L.dtype_code(dtype)))
         self.dirty = True
         return True
 
@@ -198,8 +206,11 @@ def _f32(weight):
     return w
 
 
-def _pack_one(w, f, t, Cp, ldT, segs, dtype):
+def _pack_one(w, f, t, Cp, ldT, segs, dtype, split=False):
     K, Creal, R, _ = w.shape
+    if split:
+        call('um_pack_weight_split', ptr(w), K, Creal, R, Cp, ptr(f), ptr(t), ldT)
+        return
     if segs:
         n = len(segs)
         a0 = (ctypes.c_int * n)(*[a for a, _, _ in segs])
