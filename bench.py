@@ -57,8 +57,8 @@ def parse():
                     help='eager launches instead of the captured HIP graph')
     ap.add_argument('--eager-steps', type=int, default=3,
                     help='N=1: also time this many eagerly launched steps (reported beside)')
-    ap.add_argument('--cpu-steps', type=int, default=2,
-                    help='CPU baseline: best of this many timed steps per shape (BASELINE.md)')
+    ap.add_argument('--cpu-steps', type=int, default=5,
+                    help='CPU baseline: best of this many timed steps at C2 (BASELINE.md: 5)')
     ap.add_argument('--fp32-steps', type=int, default=5,
                     help='N=1: also time the fp32 (parity-mode) captured step, reported beside')
     return ap.parse_args()
@@ -279,11 +279,19 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     out['traffic'] = None
     # HBM bytes per launch of this entry from the committed rocprofv3 PMC
     # passes (tools/pmc_traffic.py: 2*FETCH_SIZE + WRITE_SIZE, separate passes)
+    # -- only while the library loaded here is the one they were taken on
     pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
     if os.path.exists(pmc):
         with open(pmc) as f:
             t = json.load(f)
-        if t.get('entry') == dom:
+        lib = lib_digest()
+        out['traffic_digest'] = t.get('lib_digest')
+        if t.get('entry') != dom:
+            out['traffic_note'] = f'PMC traffic is of {t.get("entry")}, not the dominant entry'
+        elif not t.get('lib_digest') or t.get('lib_digest') != lib:
+            out['traffic_note'] = ('PMC traffic was taken on another library build '
+                                   f'({t.get("lib_digest")} vs loaded {lib}): not reported')
+        else:
             out['traffic'] = round(t['traffic_bytes_per_launch'])
             out['traffic_unit'] = 'bytes/launch (rocprofv3 PMC, ' + t.get('source', '') + ')'
     out['candidates'] = {k: {kk: v[kk] for kk in ('achieved', 'unit', 'frac', 'avg_launch_ms',
@@ -303,6 +311,16 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
                              'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                              'frac': round(ach / HBM_PEAK_GBS, 4)}
     return out
+
+
+def lib_digest():
+    """content digest of the loaded libumamd.so (its build stamp)"""
+    path = os.path.join(REPO, 'uncertainty-model_amd', 'umamd', 'libumamd.so.stamp')
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
 
 
 # --------------------------------------------------------- CPU baseline ----
@@ -353,7 +371,10 @@ def cpu_baseline(config, steps):
                     break
     except OSError:
         pass
-    return {'value': round(c2, 3), 'unit': 'stereo-pairs/sec', 'cores': threads, 'kind': 'port',
+    # cores = the threads actually used (torch intra-op threads); the
+    # machine's CPU count is reported beside it (a job's share is smaller)
+    return {'value': round(c2, 3), 'unit': 'stereo-pairs/sec', 'cores': threads,
+            'threads': threads, 'host_cpu_count': ncpu, 'kind': 'port',
             'sample': f'oracle fp32 train step, C2 B=8 256x512 bayesian, 1 warm-up + best of '
                       f'{steps} ({t2:.2f} s/step) at the best thread count of a C1 sweep; {cpu}',
             'c1_thread_sweep_pairs_per_s': sweep}, ref0
@@ -609,65 +630,97 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     losses = (float(dl.detach()), float(el.detach()))
-
-    loader = None
-    if use_graph and world == 1 and a.loader_steps > 0 and (a.height, a.width) == (256, 512):
-        loader = loader_line(run, a.batch, a.loader_steps)
-
-    # the eager comparison and the roofline pass run on the stream the model
-    # was built on (DDP keeps AccumulateGrad nodes bound to it)
-    with torch.cuda.stream(cap_stream):
-        eager = None
-        if use_graph and world == 1 and a.eager_steps > 0:
-            eager = time_eager(m, lf, opt, left, right, scale, a.batch, a.eager_steps)
-        roof = None
-        if not a.no_roofline:
-            roof = measure_roofline(m, lf, opt, left, right, scale, a.dtype)
-        torch.cuda.synchronize()
-    fp32 = None
-    if world == 1 and a.dtype == 'bf16' and a.fp32_steps > 0:
-        fp32 = time_fp32(cfg, device, left, right, scale, a.batch, 2, a.fp32_steps)
-    cpu, ref0 = None, None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu, ref0 = cpu_baseline(a.config, a.cpu_steps)
-    delta = None
-    if rank == 0 and world == 1 and not a.no_loss_delta and \
-            (a.height, a.width, a.batch, a.loss_type) == (256, 512, 8, 'bayesian'):
-        delta = loss_delta(load_cfg(a.config, 'bayesian'), device, ref0)
-
-    if rank == 0:
-        total = a.batch * world * a.steps
-        out = {
-            'metric': 'stereo-pairs/sec (train step) at 256x512, 1/2/4/8 MI355X; loss delta vs ref',
-            'value': round(total / elapsed, 2),
-            'unit': 'stereo-pairs/sec',
-            'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
-            'ms_per_step': round(elapsed / a.steps * 1e3, 3),
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            'dtype': a.dtype, 'data': 'synthetic U[0,1) stereo pairs (device-resident), '
-                                      'formula-free random init (torch.manual_seed(0))',
-            'config': {'workload': f'depth+uncertainty train step (BASELINE config '
-                                   f'{baseline_config(a, world, cfg)}): '
-                                   f'fwd+4-scale loss+bwd+Adam',
-                       'global_batch': a.batch * world, 'per_gpu_batch': a.batch,
-                       'height': a.height, 'width': a.width, 'loss': a.loss_type,
-                       'parallelism': f'dp{world}' + ('+syncbn' if dp else ''),
-                       'process_group': ({'backend': backend, 'world_size': dist.get_world_size()}
-                                         if dp else None),
-                       'launch': launch,
-                       'graph': f'{a.config} (nodes={cfg["model"]["encoder"].get("nodes")} '
-                                f'stage graphs)'},
-            'eager_launch': eager,
-            'loader_line': loader,
-            'fp32_line': fp32,
-            'final_losses': {'disp': round(losses[0], 5), 'error': round(losses[1], 5)},
-            'loss_delta': delta,
-            'roofline': roof,
-            'cpu_baseline': cpu,
-        }
-        print(json.dumps(out), file=json_out, flush=True)
+    total = a.batch * world * a.steps
+    out = {
+        'metric': 'stereo-pairs/sec (train step) at 256x512, 1/2/4/8 MI355X; loss delta vs ref',
+        'value': round(total / elapsed, 2),
+        'unit': 'stereo-pairs/sec',
+        'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+        'ms_per_step': round(elapsed / a.steps * 1e3, 3),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': a.dtype, 'data': 'synthetic U[0,1) stereo pairs (device-resident), '
+                                  'formula-free random init (torch.manual_seed(0))',
+        'config': {'workload': f'depth+uncertainty train step (BASELINE config '
+                               f'{baseline_config(a, world, cfg)}): '
+                               f'fwd+4-scale loss+bwd+Adam',
+                   'global_batch': a.batch * world, 'per_gpu_batch': a.batch,
+                   'height': a.height, 'width': a.width, 'loss': a.loss_type,
+                   'parallelism': f'dp{world}' + ('+syncbn' if dp else ''),
+                   'process_group': ({'backend': backend, 'world_size': dist.get_world_size()}
+                                     if dp else None),
+                   'launch': launch,
+                   'graph': f'{a.config} (nodes={cfg["model"]["encoder"].get("nodes")} '
+                            f'stage graphs)'},
+        'final_losses': {'disp': round(losses[0], 5), 'error': round(losses[1], 5)},
+    }
+    if world > 1:
+        # N>1: the line goes out right after the timed loop; the reported
+        # legs beside it (eager, roofline, CPU, loss delta) are N=1 legs
+        if rank == 0:
+            out['legs'] = 'N>1: measured value only (the roofline / CPU / loss-delta legs run at N=1)'
+            print(json.dumps(out), file=json_out, flush=True)
+        dist.destroy_process_group()
+        return
+    errors = {}
+    legs = post_timing_legs(a, run, use_graph, m, lf, opt, left, right, scale, cfg, device,
+                            cap_stream, errors)
+    out.update(legs)
+    if errors:
+        out['leg_errors'] = errors
+    print(json.dumps(out), file=json_out, flush=True)
     if dp:
         dist.destroy_process_group()
+
+
+def run_leg(name, fn, errors):
+    """One reported leg after the timed region: a failure is recorded in the
+    line (``leg_errors``) instead of losing the measured value."""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001
+        errors[name] = f'{type(e).__name__}: {e}'[:300]
+        print(f'bench: {name} leg failed: {errors[name]}', file=sys.stderr, flush=True)
+        return None
+
+
+def post_timing_legs(a, run, use_graph, m, lf, opt, left, right, scale, cfg, device, cap_stream,
+                     errors):
+    """The N=1 legs reported beside the measured value (each one guarded)."""
+    res = {}
+    if use_graph and a.loader_steps > 0 and (a.height, a.width) == (256, 512):
+        res['loader_line'] = run_leg('loader_line',
+                                     lambda: loader_line(run, a.batch, a.loader_steps), errors)
+    # the eager comparison and the roofline pass run on the stream the model
+    # was built on (DDP keeps AccumulateGrad nodes bound to it)
+
+    def on_stream(fn):
+        def g():
+            with torch.cuda.stream(cap_stream):
+                r = fn()
+                torch.cuda.synchronize()
+                return r
+        return g
+    if use_graph and a.eager_steps > 0:
+        res['eager_launch'] = run_leg('eager_launch', on_stream(
+            lambda: time_eager(m, lf, opt, left, right, scale, a.batch, a.eager_steps)), errors)
+    if not a.no_roofline:
+        res['roofline'] = run_leg('roofline', on_stream(
+            lambda: measure_roofline(m, lf, opt, left, right, scale, a.dtype)), errors)
+    if a.dtype == 'bf16' and a.fp32_steps > 0:
+        res['fp32_line'] = run_leg('fp32_line', lambda: time_fp32(
+            cfg, device, left, right, scale, a.batch, 2, a.fp32_steps), errors)
+    ref0 = None
+    if not a.no_cpu_baseline:
+        r = run_leg('cpu_baseline', lambda: cpu_baseline(a.config, a.cpu_steps), errors)
+        if r is not None:
+            res['cpu_baseline'], ref0 = r
+        else:
+            res['cpu_baseline'] = None
+    if not a.no_loss_delta and (a.height, a.width, a.batch, a.loss_type) == \
+            (256, 512, 8, 'bayesian'):
+        res['loss_delta'] = run_leg('loss_delta', lambda: loss_delta(
+            load_cfg(a.config, 'bayesian'), device, ref0), errors)
+    return res
 
 
 if __name__ == '__main__':

@@ -186,7 +186,7 @@ def train_step(P: Dict[str, torch.Tensor], left, right, scale, model_cfg, loss_c
         v.requires_grad_(False)
     adam_update(trainable, grads, adam_state, lr)
     return {'disp_loss': float(dl.detach()), 'error_loss': float(el.detach()),
-            'terms': {k: float(v) for k, v in terms.items()},
+            'terms': {k: float(v.detach()) if torch.is_tensor(v) else float(v) for k, v in terms.items()},
             'grads': grads, 'disps': [d.detach() for d in disps]}
 
 

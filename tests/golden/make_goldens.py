@@ -382,6 +382,65 @@ def gen_traj_bf16(ref_model, ref_loss, ref_utils, cfg, steps=10, b=8, h=256, w=5
     save('traj_c2_bf16.npz', **arrays)
 
 
+def train_model_pairs():
+    """7 smooth stereo pairs at 64x128 (a ragged last batch at batch 2)"""
+    left, right, _ = stereo_pair(7, 64, 128, seed=2468)
+    return left, right
+
+
+def gen_train_model(ref_model, ref_loss, ref_utils, cfg):
+    """The reference's own epoch loop, train/train.py:173-267: train_model
+    over a DataLoader of 7 pairs (batch 2, so a ragged last batch), 2 epochs,
+    the disparity scale moving 0.3 -> 0.5 between them (adjust_disparity
+    passed in, as train_model allows), the reference adjust_learning_rate,
+    bayesian loss, fp32, formula weights.  Stores the per-epoch losses per
+    image, and the reference adjust_learning_rate over epochs 0..45 (plain
+    and finetune)."""
+    from torch.utils.data import DataLoader
+    import train.train as ref_train  # noqa: E402
+    sd, _ = _formula_weights(cfg)
+    m = _ref_model(ref_model, cfg)
+    m.load_state_dict(sd)
+    lcfg = json.loads(json.dumps(cfg['loss']))
+    lcfg['error_loss_config']['loss_type'] = 'bayesian'
+    lf = ref_loss.TukraUncertaintyLoss(**lcfg)
+    left, right = train_model_pairs()
+    ds = [{'left': left[i], 'right': right[i]} for i in range(left.shape[0])]
+    loader = DataLoader(ds, batch_size=2, shuffle=False)
+    scales = [0.3, 0.5]
+    losses, _ = ref_train.train_model(m, loader, lf, epochs=2, learning_rate=1e-4,
+                                      adjust_disparity=lambda e: scales[e], no_pbar=True)
+    arrays = {'left': left, 'right': right, 'scales': np.array(scales),
+              'epoch_disp': np.array([l[0] for l in losses]),
+              'epoch_unc': np.array([l[1] for l in losses])}
+    opt = torch.optim.Adam([torch.zeros(1, requires_grad=True)], 1e-4)
+    for ft in (False, True):
+        lrs = []
+        for e in range(46):
+            ref_utils.adjust_learning_rate(opt, e, 1e-4, finetune=ft)
+            lrs.append(opt.param_groups[0]['lr'])
+        arrays['lr_finetune' if ft else 'lr'] = np.array(lrs)
+    print('train_model epochs:', losses, flush=True)
+    # the same loop in float64: the reference's own fp32 noise on these
+    # per-epoch losses (Adam turns summation-order noise in near-zero
+    # gradient components into update sign flips), the scale of the bar
+    torch.set_default_dtype(torch.float64)
+    try:
+        m64 = _ref_model(ref_model, cfg)
+        m64.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in sd.items()})
+        ds64 = [{'left': left[i].double(), 'right': right[i].double()}
+                for i in range(left.shape[0])]
+        losses64, _ = ref_train.train_model(m64, DataLoader(ds64, batch_size=2, shuffle=False),
+                                            lf, epochs=2, learning_rate=1e-4,
+                                            adjust_disparity=lambda e: scales[e], no_pbar=True)
+    finally:
+        torch.set_default_dtype(torch.float32)
+    arrays['epoch_disp_f64'] = np.array([l[0] for l in losses64])
+    arrays['epoch_unc_f64'] = np.array([l[1] for l in losses64])
+    print('train_model epochs (f64):', losses64, flush=True)
+    save('train_model.npz', **arrays)
+
+
 def gen_nodes10(ref_model, cfg10):
     sd, specs = _formula_weights(cfg10)
     m = _ref_model(ref_model, cfg10)
@@ -542,7 +601,7 @@ def main():
     with open(os.path.join(REPO, 'config_nodes10.yml')) as f:
         cfg10 = yaml.safe_load(f)
     which = sys.argv[1:] or ['warp', 'loss', 'model', 'step', 'nodes10', 'c1', 'transforms',
-                             'sparsification', 'adversarial', 'traj']
+                             'sparsification', 'adversarial', 'traj', 'train_model']
     if 'warp' in which:
         gen_warp(ref_utils)
     if 'loss' in which:
@@ -559,6 +618,8 @@ def main():
         gen_traj(ref_model, ref_loss, ref_utils, cfg)
     if 'traj_bf16' in which:  # the reference's own bf16-autocast deviation at config 2
         gen_traj_bf16(ref_model, ref_loss, ref_utils, cfg)
+    if 'train_model' in which:  # the reference's epoch loop (ragged batch, scale change)
+        gen_train_model(ref_model, ref_loss, ref_utils, cfg)
     if 'c1' in which:  # BASELINE config 1: 128x256, batch 2, l1 error loss, one step
         gen_step(ref_model, ref_loss, ref_utils, cfg, 'l1', steps=1, tag='c1_l1', b=2, h=128,
                  w=256, disp_levels=(2, 3))

@@ -55,3 +55,34 @@ def test_bench_parses_gpus_flag():
         sys.argv = old
     assert a.gpus == 8 and a.steps == 3
     assert os.path.exists(os.path.join(REPO, 'tests', 'golden', 'traj_c2.npz'))
+
+
+def test_post_timing_leg_failure_keeps_the_line(monkeypatch):
+    """A leg after the timed region that raises (here the CPU baseline and
+    the eager comparison) is recorded in ``leg_errors``; the other legs and
+    the measured value still go out (bench.main prints the line after
+    post_timing_legs returns)."""
+    import argparse
+    import bench
+
+    def boom(*a, **k):
+        raise RuntimeError('leg exploded')
+    monkeypatch.setattr(bench, 'cpu_baseline', boom)
+    monkeypatch.setattr(bench, 'time_eager', boom)
+    monkeypatch.setattr(bench, 'time_fp32', lambda *a, **k: {'value': 1.0})
+    a = argparse.Namespace(loader_steps=0, eager_steps=3, no_roofline=True, dtype='bf16',
+                           fp32_steps=5, no_cpu_baseline=False, no_loss_delta=True, height=256,
+                           width=512, batch=8, loss_type='bayesian', config='config.yml',
+                           cpu_steps=5)
+
+    class _Stream:  # torch.cuda.stream(...) stand-in on a CPU-only host
+        pass
+    monkeypatch.setattr(bench.torch.cuda, 'stream', lambda s: __import__('contextlib').nullcontext())
+    monkeypatch.setattr(bench.torch.cuda, 'synchronize', lambda: None)
+    errors = {}
+    res = bench.post_timing_legs(a, None, True, None, None, None, None, None, 0.3, None, None,
+                                 _Stream(), errors)
+    assert res['fp32_line'] == {'value': 1.0}
+    assert res['cpu_baseline'] is None and res['eager_launch'] is None
+    assert set(errors) == {'cpu_baseline', 'eager_launch'}
+    assert 'leg exploded' in errors['cpu_baseline']

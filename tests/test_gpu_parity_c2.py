@@ -25,6 +25,7 @@ import pytest
 import torch
 
 from _parity import grad_worst, rel_norm, sketch_worst
+from conftest import GOLDEN
 from test_gpu_model import DEV, _cfg, _model, _z
 
 pytestmark = pytest.mark.gpu
@@ -208,3 +209,48 @@ def test_train_model_graph_replay_matches_eager(monkeypatch):
     for (dg, ug, _), (de, ue, _) in zip(res['graph'], res['eager']):
         assert abs(dg / de - 1) < 5e-3 and abs(ug / ue - 1) < 5e-3, (res['graph'], res['eager'])
     assert np.isfinite(np.array([r[:2] for r in res['graph']])).all()
+
+
+def test_train_model_vs_reference_loop(monkeypatch):
+    """Our train.train.train_model (graph replay for full batches, the
+    ragged last batch eager, the capture redone when the scale moves) against
+    the REFERENCE's own train_model run on the same loader
+    (tests/golden/train_model.npz: reference train/train.py:173-267, 7 pairs
+    at 64x128, batch 2, 2 epochs, disparity scale 0.3 -> 0.5, the reference
+    adjust_learning_rate, bayesian, fp32, formula weights): per-epoch losses
+    per image within max(1e-3, 2x the reference's own fp32 noise on that
+    number): the same reference loop in float64 (epoch_*_f64) moves the
+    epoch-0 uncertainty loss by 2.0e-3 and epoch 1's by 3.3e-3 (Adam turns
+    summation-order noise in near-zero gradient components into update sign
+    flips, and the bayesian e/sigma amplifies them)."""
+    from torch.utils.data import DataLoader
+    from train import train as T
+    from train.loss import TukraUncertaintyLoss
+    z = np.load(os.path.join(GOLDEN, 'train_model.npz'))
+    cfg = _cfg()
+    cfg['loss']['error_loss_config']['loss_type'] = 'bayesian'
+    left, right = torch.from_numpy(z['left']), torch.from_numpy(z['right'])
+    pairs = [{'left': left[i], 'right': right[i]} for i in range(left.shape[0])]
+    loader = DataLoader(pairs, batch_size=2, shuffle=False)
+    m = _model(cfg).train()
+    lf = TukraUncertaintyLoss(**cfg['loss'])
+    seen = []
+    orig = T._GraphSteps.__call__
+
+    def spy(self, l_, r_, scale):
+        out = orig(self, l_, r_, scale)
+        seen.append(out is not None)
+        return out
+    monkeypatch.setattr(T._GraphSteps, '__call__', spy)
+    scales = [float(s) for s in z['scales']]
+    losses, _ = T.train_model(m, loader, lf, 2, 1e-4, adjust_disparity=lambda e: scales[e],
+                              device=DEV, no_pbar=True)
+    assert seen.count(True) == 6 and seen.count(False) == 2, seen  # graph path taken
+    for e, (d, u_, _) in enumerate(losses):
+        for name, got in (('disp', d), ('unc', u_)):
+            ref32, ref64 = float(z[f'epoch_{name}'][e]), float(z[f'epoch_{name}_f64'][e])
+            noise = abs(ref32 / ref64 - 1)  # the reference's own fp32 deviation
+            r = abs(got / ref32 - 1)
+            print(f'epoch {e} {name}: ours {got:.6f} ref fp32 {ref32:.6f} ({r:.2e}) '
+                  f'ref f64 {ref64:.6f} (ours {abs(got / ref64 - 1):.2e}, ref fp32 {noise:.2e})')
+            assert r < max(1e-3, 2 * noise), (e, name, losses, ref32, ref64)

@@ -96,6 +96,15 @@ def _bracketed(disp, counter):
     return per, names
 
 
+def _lib_digest():
+    path = os.path.join(REPO, 'uncertainty-model_amd', 'umamd', 'libumamd.so.stamp')
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
 def parse(a):
     f_per, names = _bracketed(_dispatches(a.fetch_dir), 'FETCH_SIZE')
     w_per, _ = _bracketed(_dispatches(a.write_dir), 'WRITE_SIZE')
@@ -116,6 +125,9 @@ def parse(a):
         'workload': 'one eager bench step (B=8, 256x512, bf16, bayesian) after warm-up',
         'kernels': sorted(names),
         'source': a.tag,
+        # the library these counters were taken on (bench.py reports the
+        # traffic only while the library it loads has the same digest)
+        'lib_digest': _lib_digest(),
     }
     out = a.out or os.path.join(REPO, 'profiles', 'pmc_traffic.json')
     with open(out, 'w') as f:

@@ -53,6 +53,7 @@ class GradBuckets:
         self.ready = set()
         self.launched = set()
         self.raw = []
+        self._events = []  # fork/join events of the current backward (overlap.stream_wait)
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
 
     # ------------------------------------------------------------ layout --
@@ -95,6 +96,7 @@ class GradBuckets:
         self.ready.clear()
         self.launched.clear()
         self.raw = []
+        self._events = []
         self.ov = _overlap.active()
         if self.ov is not None and self.layout is not None:
             self.ov.on_flush(self._poll)
@@ -136,9 +138,9 @@ class GradBuckets:
             self._reduce(dst, grads)
             return
         cur = torch.cuda.current_stream()
-        self.stream.wait_stream(cur)
+        _overlap.stream_wait(self.stream, cur, self._events)
         if self.ov is not None:  # gradients written on the weight-gradient stream
-            self.stream.wait_stream(self.ov.stream)
+            _overlap.stream_wait(self.stream, self.ov.stream, self._events)
         with torch.cuda.stream(self.stream):
             self._reduce(dst, grads)
 
@@ -168,7 +170,7 @@ class GradBuckets:
             if bi not in self.launched:
                 self._launch(bi)
         if self.stream is not None:
-            torch.cuda.current_stream().wait_stream(self.stream)
+            _overlap.stream_wait(torch.cuda.current_stream(), self.stream, self._events)
         for p, h in zip(self.params, self.layout):
             if h:
                 off, n, shape = self.views[id(p)]

@@ -103,7 +103,9 @@ class StereoDraws:
         if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 3:
             raise TypeError(f'StereoDraws: RGB uint8 HWC image expected, got {a.dtype} '
                             f'{a.shape}')
-        return torch.from_numpy(np.ascontiguousarray(a))
+        if not a.flags.writeable or not a.flags.c_contiguous:
+            a = np.array(a, copy=True, order='C')  # np.asarray(PIL image) is read-only
+        return torch.from_numpy(a)
 
     def __call__(self, image_pair):
         prep = np.zeros(8, np.float32)

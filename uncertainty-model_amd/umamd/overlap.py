@@ -50,6 +50,7 @@ class WgradStream:
         self._pending = []
         self._pending_out = []
         self._on_flush = []
+        self._events = []  # fork/join events of the current backward (stream_wait)
 
     def __enter__(self):
         if WgradStream._active is not None:
@@ -58,6 +59,7 @@ class WgradStream:
             raise RuntimeError('WgradStream needs gradients set to None before backward '
                                '(zero_grad(set_to_none=True))')
         self._launch = torch.cuda.current_stream()
+        self._events = []
         WgradStream._active = self
         return self
 
@@ -97,7 +99,7 @@ class WgradStream:
     def _flush(self):
         if not self._pending:
             return
-        self.stream.wait_stream(torch.cuda.current_stream())
+        stream_wait(self.stream, torch.cuda.current_stream(), self._events)
         from . import _lib as L
         from . import functional as F
         with torch.cuda.stream(self.stream):
@@ -129,7 +131,21 @@ class WgradStream:
             self._flush()
         finally:
             self._on_flush = []
-            self._launch.wait_stream(self.stream)
+            stream_wait(self._launch, self.stream, self._events)
+
+
+def stream_wait(dst, src, keep: list):
+    """``dst`` waits for the work queued on ``src`` so far (Stream.wait_stream)
+    with an event object kept alive in ``keep`` until the caller drops it:
+    under HIP graph capture an event that is destroyed while the capture
+    runs and re-created at the same address makes a later wait attach to the
+    wrong captured record (measured on MI355X: with one-parameter gradient
+    buckets, ~200 fork/join pairs in one capture, most of the packed
+    gradients were read before they were written)."""
+    ev = torch.cuda.Event()
+    ev.record(src)
+    dst.wait_event(ev)
+    keep.append(ev)
 
 
 def active() -> Optional[WgradStream]:
