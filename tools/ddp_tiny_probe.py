@@ -68,6 +68,72 @@ def main():
             with torch.cuda.stream(self.stream):
                 torch.cat([g.reshape(-1) for g in grads], out=self.flat[off:off + n])
         GradBuckets._launch = clone
+    if mode in ('evlate', 'fin'):
+        PEND = []
+
+        def late(self, bi):
+            self.launched.add(bi)
+            b = self.buckets[bi]
+            off, n = self.slices[bi]
+            grads = [p.grad for p in b]
+            self.raw += grads
+            ev = None
+            if mode == 'evlate':  # event at hook time, fork at finish
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream())
+            PEND.append((ev, grads, off, n))
+        GradBuckets._launch = late
+        of = GradBuckets.finish
+
+        def fin2(self):
+            cur = torch.cuda.current_stream()
+            for ev, grads, off, n in PEND:
+                if ev is None:
+                    ev = torch.cuda.Event()
+                    ev.record(cur)
+                self.stream.wait_event(ev)
+                self._events.append(ev)
+                with torch.cuda.stream(self.stream):
+                    torch.cat([g_.reshape(-1) for g_ in grads], out=self.flat[off:off + n])
+            PEND.clear()
+            return of(self)
+        GradBuckets.finish = fin2
+    if mode in ('evmid', 'midclone2', 'midcopy'):
+        Q = []
+
+        def mid(self, bi):
+            self.launched.add(bi)
+            b = self.buckets[bi]
+            off, n = self.slices[bi]
+            grads = [p.grad for p in b]
+            self.raw += grads
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            self._events.append(ev)
+            Q.append((ev, grads, off, n))
+            take = Q[:-1] if mode == 'evmid' else Q[:]
+            for e_, gs, o_, n_ in take:
+                self.stream.wait_event(e_)
+                with torch.cuda.stream(self.stream):
+                    if mode == 'midclone2':
+                        gs = [g_.clone() for g_ in gs]
+                        self.raw += gs
+                    if mode == 'midcopy':
+                        self.flat[o_:o_ + n_].copy_(gs[0].reshape(-1))
+                    else:
+                        torch.cat([g_.reshape(-1) for g_ in gs], out=self.flat[o_:o_ + n_])
+            del Q[:len(take)]
+        GradBuckets._launch = mid
+        of2 = GradBuckets.finish
+
+        def fin3(self):
+            for e_, gs, o_, n_ in Q:
+                self.stream.wait_event(e_)
+                with torch.cuda.stream(self.stream):
+                    torch.cat([g_.reshape(-1) for g_ in gs], out=self.flat[o_:o_ + n_])
+            Q.clear()
+            return of2(self)
+        GradBuckets.finish = fin3
     if mode in ('rec', 'hold'):
         HOLD = []
 
@@ -110,7 +176,7 @@ def main():
         return orig_launch(self, bi)
     gb_capturing = [False]
     in_finish = [False]
-    if mode not in ('same', 'clone', 'rec', 'hold'):
+    if mode not in ('same', 'clone', 'rec', 'hold', 'evlate', 'fin', 'evmid', 'midclone2', 'midcopy'):
         GradBuckets._launch = spy
     orig_finish = GradBuckets.finish
 

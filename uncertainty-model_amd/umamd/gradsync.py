@@ -135,17 +135,36 @@ class GradBuckets:
                 raise TypeError('GradBuckets: float32 gradients expected')
         self.raw += grads  # the backward's own gradient tensors stay allocated
         if self.stream is None:
-            self._reduce(dst, grads)
+            self._pack(dst, grads)
+            self._reduce(dst)
             return
+        # The pack runs on a stream that produced (or is ordered after) the
+        # gradients -- the launch stream, or the weight-gradient stream after
+        # it waited for the launch stream -- and only the all-reduce of the
+        # packed slice forks onto the communication stream.  Measured on
+        # MI355X: a pack on the communication stream issued during the
+        # captured backward (autograd's device thread, from these hooks) read
+        # gradient memory before it was written in replay, although its
+        # event dependency was recorded after the producer (one-parameter
+        # buckets: ~150 of 233 gradients wrong; the same wait issued after
+        # the backward, or a pack on the producing stream, was exact:
+        # tools/ddp_tiny_probe.py, tests/test_gpu_graph.py tiny buckets).
         cur = torch.cuda.current_stream()
-        _overlap.stream_wait(self.stream, cur, self._events)
+        src = cur
         if self.ov is not None:  # gradients written on the weight-gradient stream
-            _overlap.stream_wait(self.stream, self.ov.stream, self._events)
+            src = self.ov.stream
+            _overlap.stream_wait(src, cur, self._events)
+        with torch.cuda.stream(src):
+            self._pack(dst, grads)
+        _overlap.stream_wait(self.stream, src, self._events)
         with torch.cuda.stream(self.stream):
-            self._reduce(dst, grads)
+            self._reduce(dst)
 
-    def _reduce(self, dst, grads):
+    @staticmethod
+    def _pack(dst, grads):
         torch.cat([g.reshape(-1) for g in grads], out=dst)
+
+    def _reduce(self, dst):
         c = _rccl.active(self.group, 'grad')  # the captured step's own communicator
         if c is not None:
             c.all_reduce(dst, average=True)
