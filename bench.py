@@ -192,6 +192,27 @@ CONV_ENTRIES = {
 }
 
 
+HEAD_ENTRIES = {'um_head_fwd': 'head_fwd_kernel', 'um_head_dgrad': 'head_dgrad_kernel',
+                'um_head_wgrad': 'head_wgrad_kernel'}
+
+
+def head_min_bytes(name, a):
+    """compulsory HBM bytes of a disparity-head launch (csrc/head.hip):
+    forward reads x (Cp channels) and writes 4 f32; the data gradient reads
+    dl (4 of its 8 channels) and writes dx (read-modify-write when
+    accumulating).  x / dl / dx in the activation dtype."""
+    es = 4 if a[0] == 0 else 2
+    N, H, W = a[1], a[2], a[3]
+    px = N * H * W
+    if name == 'um_head_wgrad':  # reads x and dl (4 of its 8 channels)
+        return px * ((a[4] + 7) // 8 * 8 * es + 4 * es)
+    Cp = a[5]
+    if name == 'um_head_fwd':
+        return px * (Cp * es + 16)
+    acc = a[11]
+    return px * (4 * es + Cp * es * (2 if acc else 1))
+
+
 def conv_min_bytes(name, a):
     """Compulsory HBM bytes of one conv-entry launch (each operand touched
     once): fwd reads x and the packed weights, writes y (f32 pre-BN or T);
@@ -241,7 +262,7 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     the dominant kernel.  Conv work = algorithmic FLOPs with the real channel
     counts (2*N*P*Q*K*R*R*C per pass, attached at each call site)."""
     from umamd import _lib
-    rec = _lib.Recorder(set(CONV_ENTRIES) | set(LOSS_KERNELS))
+    rec = _lib.Recorder(set(CONV_ENTRIES) | set(LOSS_KERNELS) | set(HEAD_ENTRIES))
     with rec:
         step(m, lf, opt, left, right, scale)
     torch.cuda.synchronize()
@@ -250,6 +271,18 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
         groups.setdefault(name, []).append((args, ms, work))
     peak = BF16_PEAK_TFLOPS if dtype == 'bf16' else F32_PEAK_TFLOPS
     table = {}
+    heads = {}
+    for name in HEAD_ENTRIES:
+        items = groups.pop(name, [])
+        if not items:
+            continue
+        tot_ms = sum(ms for _, ms, _ in items)
+        b = sum(head_min_bytes(name, a) for a, _, _ in items)
+        ach = b / (tot_ms * 1e-3) / 1e9
+        heads[name] = {'kernel': HEAD_ENTRIES[name], 'bound': 'hbm', 'launches_per_step': len(items),
+                       'total_ms_per_step': round(tot_ms, 4), 'achieved': round(ach, 1),
+                       'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(ach / HBM_PEAK_GBS, 4),
+                       'per_launch_us': [round(ms * 1e3, 1) for _, ms, _ in items]}
     for name, items in groups.items():
         tot_ms = sum(ms for _, ms, _ in items)
         if name in LOSS_KERNELS:
@@ -298,6 +331,7 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
                                                   'launches_per_step', 'total_ms_per_step')}
                          for k, v in table.items()}
     out['conv1x1'] = conv1x1_report(groups, peak)
+    out['disp_heads'] = heads or None  # the 4-output heads (VALU, HBM-bound)
     if all(k in groups for k in LOSS_KERNELS):
         # the fused loss stack (forward + backward launches) priced as SURVEY
         # 8d does: 56 B/px all-f32 (6 image + 4 prediction reads, 4 gradient

@@ -31,12 +31,15 @@ extern "C" {
 #endif
 
 enum { UM_OK = 0, UM_ERR_ARG = 1, UM_ERR_HIP = 2 };
-enum { UM_F32 = 0, UM_BF16 = 1 };
+enum { UM_F32 = 0, UM_BF16 = 1, UM_F16 = 2 /* pre-BN y storage only (UM_Y_F16) */ };
 /* OR'ed into the dtype of the um_bn_elu_* entries (and um_conv2d_fwd_up2's): the pre-BN conv output y is stored in the activation
  * dtype instead of f32 (the bf16 build's default, as a bf16 autocast conv
  * feeding BatchNorm2d; statistics are still taken in f32 in the conv
  * epilogue).  um_conv2d_fwd_up2: y and the low-resolution map up2. */
 enum { UM_Y_ACT = 0x100 };
+/* dtype flag of the BN entries: the pre-BN y of bf16 activations is stored as
+ * f16 (um_conv2d_fwd with ydtype UM_F16): 2 bytes like UM_Y_ACT's bf16, 8x finer */
+enum { UM_Y_F16 = 0x200 };
 enum { UM_PAD_ZERO = 0, UM_PAD_REFLECT = 1 };
 enum {
   UM_EPI_NONE = 0,           /* y = acc (+ bias)                               */
@@ -373,6 +376,23 @@ int um_sigmoid_scale_bwd(int dtype, long M, int C, const float* d, int ldd, cons
  * channels [2K, ldo) zeroed. */
 int um_head_split_fin(long M, int K, const float* z, int ldz, const float* bias, float scale,
                       float* d, int ldd, hipStream_t stream);
+/* The 4-output heads as VALU kernels (csrc/head.hip; reference
+ * model/layers/decoder.py:244-247): 3x3 conv with ReflectionPad2d(1), f32
+ * weights in the reference layout w [4][Creal][3][3], f32 accumulation.
+ * um_head_fwd: d [N*H*W][4] f32 = scale * sigmoid(conv(x) + bias), x NHWC
+ * [N][H][W] with ldx >= Cp, Cp % 32 == 0 (zero-padded channels beyond Creal).
+ * um_head_dgrad: dx[m][c] (+)= sum over the reflect-padded 3x3 transpose of
+ * dl [N*H*W][ldl] (channels 0..3 = d(loss)/d(logit)) with w; dtype of x / dx
+ * and dl. */
+int um_head_fwd(int dtype, int N, int H, int W, int Creal, int Cp, int ldx, const void* x,
+                const float* w, const float* bias, float scale, float* d, hipStream_t stream);
+int um_head_dgrad(int dtype, int N, int H, int W, int Creal, int Cp, const void* dl, int ldl,
+                  const float* w, void* dx, int ldx, int accumulate, hipStream_t stream);
+/* weight and bias gradient of the head: dw [4][Creal][3][3] += sum_q dl[q][k]
+ * x[reflect(q + t)][c], db[4] += sum_q dl[q][k] (db nullable); dw / db must be
+ * zeroed by the caller (f32 atomics, one per value and workgroup). */
+int um_head_wgrad(int dtype, int N, int H, int W, int Creal, int ldx, const void* x,
+                  const void* dl, int ldl, float* dw, float* db, hipStream_t stream);
 int um_sigmoid_scale_bwd_split(int dtype, long M, int C, const float* d, int ldd, const float* dd,
                                int lddd, float scale, void* dlogit, int ldo, hipStream_t stream);
 

@@ -757,13 +757,16 @@ def test_dgrad_stride2_classes(case, cls4):
     assert _rel(_nchw(dx), ref) < 1e-2
 
 
-@pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 16), (256, 4, 8)])
-def test_disp_head_split(C, H, W, monkeypatch):
-    """The bf16 disparity/uncertainty head with split-bf16 weights
+@pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 16), (256, 4, 8), (96, 3, 5)])
+@pytest.mark.parametrize('path', ['valu', 'split'])
+def test_disp_head_split(C, H, W, path, monkeypatch):
+    """The bf16 disparity/uncertainty head, either as the VALU kernels
+    (csrc/head.hip: f32 weights, um_head_fwd / um_head_dgrad, the reflect
+    transpose incl. 3-pixel edges) or as the GEMM with split-bf16 weights
     (um_pack_weight_split: hi + lo rows in the padding columns of the
-    4-output GEMM) against an f64 reference with the UNROUNDED f32 weights:
-    the forward is f32-accurate (the plain bf16 head is off by the weight
-    rounding), and the backward sums both halves of the weight."""
+    4-output GEMM), against an f64 reference with the UNROUNDED f32 weights:
+    the forward is f32-accurate (the plain bf16 GEMM head is off by the
+    weight rounding), and the backward sees the f32 weight."""
     import umamd.functional as U
     N, K, scale = 2, 4, 0.3
     x = F.elu(torch.randn(N, C, H, W)).to(torch.bfloat16).float()
@@ -783,7 +786,8 @@ def test_disp_head_split(C, H, W, monkeypatch):
         return d.detach(), xr.grad, wr.grad
 
     def run(split):
-        monkeypatch.setattr(U, '_SPLIT_HEAD', split)
+        monkeypatch.setattr(U, '_SPLIT_HEAD', split and path == 'split')
+        monkeypatch.setattr(U, '_VALU_HEAD', split and path == 'valu')
         xd = _nhwc(x).to(torch.bfloat16)
         Cp = (C + 7) // 8 * 8
         if Cp != C:
@@ -804,3 +808,54 @@ def test_disp_head_split(C, H, W, monkeypatch):
     assert _rel(dx_s, dx_ref) <= 1e-2, _rel(dx_s, dx_ref)
     assert _rel(dw_s, dw_ref) <= 1e-2, _rel(dw_s, dw_ref)
     assert _rel(dx_s, dx_ref) <= _rel(dx_p, dx_ref) * 1.5 + 1e-4
+
+
+@pytest.mark.parametrize('case', [CONV_CASES[1], CONV_CASES[3], CONV_CASES[7], CONV_CASES[4]])
+@pytest.mark.parametrize('ymode', ['f16', 'bf16'])
+def test_conv_bn_elu_y16_centred(case, ymode, monkeypatch):
+    """bf16 activations with the pre-BN y stored in 16 bits (UM_Y_F16 /
+    UM_Y_ACT) and centred by the layer's ycen buffer: two training steps on
+    the same input (the second conv runs with ycen = -(conv-only mean of the
+    first), um_bn_elu_fwd_slots): outputs, gradients and the running
+    statistics after both updates (true means, not the centred ones) against
+    the fp32 CPU reference."""
+    from umamd import functional as U
+    from umamd._lib import PAD_REFLECT, PAD_ZERO
+    monkeypatch.setattr(U, '_Y_F16', ymode == 'f16')
+    monkeypatch.setattr(U, '_Y_ACT', ymode == 'bf16')
+    monkeypatch.setattr(U, '_Y_CENTER', True)
+    Cin, Cout, k, stride, mode, H, W = case
+    N, pad = 2, (k - 1) // 2
+    conv, bn = nn.Conv2d(Cin, Cout, k, stride), nn.BatchNorm2d(Cout)
+    with torch.no_grad():
+        conv.bias.uniform_(2.0, 4.0)  # a large mean: what the centring is for
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(N, Cin, H, W) + 1.0
+    cr, br = nn.Conv2d(Cin, Cout, k, stride), nn.BatchNorm2d(Cout)
+    cr.load_state_dict(conv.state_dict())
+    br.load_state_dict(bn.state_dict())
+    cd, bd = conv.to(DEV), bn.to(DEV)
+    xq = _nhwc(x).to(torch.bfloat16)
+    xs = _nchw(xq)  # the reference sees the same bf16-rounded input
+    for step in range(2):
+        xr = xs.clone().requires_grad_(True)
+        xp = F.pad(xr, (pad,) * 4, mode='reflect' if mode == 'reflect' else 'constant')
+        yr = F.elu(br(cr(xp)))
+        g = torch.randn_like(yr)
+        cr.zero_grad()
+        br.zero_grad()
+        (yr * g).sum().backward()
+        xd = xq.clone().requires_grad_(True)
+        cd.zero_grad()
+        bd.zero_grad()
+        with U.stat_scope(U.StatArena(), DEV):
+            yd = U.conv_bn_elu(xd, cd, bd, pad, PAD_REFLECT if mode == 'reflect' else PAD_ZERO)
+        (yd.float() * _nhwc(g)).sum().backward()
+        assert _rel(_nchw(yd), yr) < 5e-2, step
+        assert _rel(_nchw(xd.grad), xr.grad) < 2.5e-1, step
+        assert _rel(cd.weight.grad, cr.weight.grad) < 2.5e-1, step
+        assert _rel(bd.weight.grad, br.weight.grad) < 2.5e-1, step
+    assert getattr(bd, '_umamd_ycen', None) is not None
+    assert _rel(bd.running_mean, br.running_mean) < 1e-3
+    assert _rel(bd.running_var, br.running_var) < 2e-2

@@ -654,14 +654,16 @@ static int bn_fwd_launch(int dtype, long M, int C, const void* y, int ldy, const
   const dim3 g(ceil_div(M, rows), sl.ns);
   const size_t shm = (pool_parts ? 256 * 8 * sizeof(float) : 0) +
                      (fin.slots ? 2 * (size_t)sl.cs * sizeof(float) : 0);
-  const bool yact = dtype & UM_Y_ACT;
-  dtype &= ~UM_Y_ACT;
+  const bool yact = dtype & UM_Y_ACT, yf16 = dtype & UM_Y_F16;
+  dtype &= ~(UM_Y_ACT | UM_Y_F16);
 #define UM_BN_FWD(T_, MG_, TY_)                                                            \
   hipLaunchKernelGGL((bn_elu_fwd_kernel<T_, MG_, TY_>), g, dim3(256), shm, st, (const TY_*)y, \
                      ldy, M, C, scale, shift, (T_*)a, lda, apply_elu, rows, pool_parts, fin,   \
                      sl.cs, mo)
   if (dtype == UM_BF16 && yact) {
     if (mo.n) UM_BN_FWD(bf16_t, true, bf16_t); else UM_BN_FWD(bf16_t, false, bf16_t);
+  } else if (dtype == UM_BF16 && yf16) {
+    if (mo.n) UM_BN_FWD(bf16_t, true, f16_t); else UM_BN_FWD(bf16_t, false, f16_t);
   } else if (dtype == UM_BF16) {
     if (mo.n) UM_BN_FWD(bf16_t, true, float); else UM_BN_FWD(bf16_t, false, float);
   } else {
@@ -750,6 +752,7 @@ static int bwd_reduce_launch(int dtype, long M, int C, long HW, const void* da, 
                      (const T_*)da, ldda, (const TY_*)y, ldy, M, C, HW, mean, invstd, scale, \
                      shift, add_nc, apply_elu, parts, rows, fin, slots, sl.cs)
   if (dtype == (UM_BF16 | UM_Y_ACT)) UM_BN_RED(bf16_t, bf16_t);
+  else if (dtype == (UM_BF16 | UM_Y_F16)) UM_BN_RED(bf16_t, f16_t);
   else if (dtype == UM_BF16) UM_BN_RED(bf16_t, float);
   else UM_BN_RED(float, float);
 #undef UM_BN_RED
@@ -828,6 +831,7 @@ static int bwd_apply_launch(int dtype, long M, int C, long HW, const void* da, i
                      shift, add_nc, apply_elu, k1, k2, k3, (T_*)dy, lddy, sum_parts, rows, fin, \
                      sl.cs)
   if (dtype == (UM_BF16 | UM_Y_ACT)) UM_BN_APPLY(bf16_t, bf16_t);
+  else if (dtype == (UM_BF16 | UM_Y_F16)) UM_BN_APPLY(bf16_t, f16_t);
   else if (dtype == UM_BF16) UM_BN_APPLY(bf16_t, float);
   else UM_BN_APPLY(float, float);
 #undef UM_BN_APPLY

@@ -1059,7 +1059,8 @@ static int conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void
   UM_CHECK_ARG((epilogue != UM_EPI_STATS && epilogue != UM_EPI_STAT_SLOTS) || stats != nullptr,
                "um_conv2d_fwd: stats buffer missing");
   UM_CHECK_ARG(epilogue != UM_EPI_RESIDUAL || residual != nullptr, "um_conv2d_fwd: residual missing");
-  UM_CHECK_ARG(ydtype == dtype || ydtype == UM_F32, "um_conv2d_fwd: ydtype must be dtype or f32");
+  UM_CHECK_ARG(ydtype == dtype || ydtype == UM_F32 || (ydtype == UM_F16 && dtype == UM_BF16),
+               "um_conv2d_fwd: ydtype must be dtype, f32, or f16 with bf16 activations");
   umamd::IgArgs a{};
   a.a = x; a.ah = H; a.aw = W; a.ach = C; a.lda = ldx;
   a.on = N; a.oh = P; a.ow = Q;
@@ -1070,6 +1071,7 @@ static int conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void
   a.b = wf; a.ldb = (long)R * R * C;
   a.NC = K; a.M = N * P * Q;
   a.bias = bias; a.out = y; a.ld_out = ldy; a.out_f32 = (ydtype == UM_F32);
+  a.out_f16 = (ydtype == UM_F16);
   a.epilogue = epilogue == UM_EPI_STAT_SLOTS ? UM_EPI_STATS : epilogue;
   a.stat_slots = epilogue == UM_EPI_STAT_SLOTS;
   a.accumulate = accumulate; a.epi_scale = epi_scale;

@@ -36,6 +36,7 @@ struct IgArgs {
   const float* bias;
   void* out;
   int ld_out, out_f32, epilogue, accumulate;
+  int out_f16;      // y stored as f16 (UM_Y_F16; out_f32 == 0)
   float epi_scale;
   const void* residual;
   int ldr;

@@ -262,7 +262,8 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
     }
     return;
   }
-  const bool stageable = sOut != nullptr && !a.out_f32 && a.NC % 8 == 0 && a.ld_out % 8 == 0;
+  const bool stageable = sOut != nullptr && !a.out_f32 && !a.out_f16 && a.NC % 8 == 0 &&
+                         a.ld_out % 8 == 0;
   // accumulate + statistics slots (the decoder skip conv's feature-map half
   // onto up2(z)): the statistics of the SUM are taken in the 16-byte row
   // store (WN == 1: one wave per row of sStat) instead of a 2-byte
@@ -294,6 +295,10 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
           float* o = reinterpret_cast<float*>(a.out) + off;
           if (a.accumulate) v += *o;
           *o = v;
+        } else if (a.out_f16) {
+          f16_t* o = reinterpret_cast<f16_t*>(a.out) + off;
+          if (a.accumulate) v += to_f32(*o);
+          *o = from_f32<f16_t>(v);
         } else if (staged) {  // accumulate (if any) happens at the row store
           sOut[(m - bm) * BN + (n - bn)] = from_f32<T>(v);
         } else {
@@ -851,6 +856,10 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const fl
           float* o = reinterpret_cast<float*>(a.out) + off;
           if (a.accumulate) v[e] += *o;
           *o = v[e];
+        } else if (a.out_f16) {
+          f16_t* o = reinterpret_cast<f16_t*>(a.out) + off;
+          if (a.accumulate) v[e] += to_f32(*o);
+          *o = from_f32<f16_t>(v[e]);
         } else {
           T* o = reinterpret_cast<T*>(a.out) + off;
           if (a.accumulate) v[e] += to_f32(*o);

@@ -14,10 +14,11 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libumamd.so')
 
-UM_F32, UM_BF16 = 0, 1
+UM_F32, UM_BF16, UM_F16 = 0, 1, 2
 # OR'ed into the dtype of the um_bn_elu_* entries / um_conv2d_fwd_up2: the
 # pre-BN y is stored in the activation dtype (include/umamd.h)
 Y_ACT = 0x100
+Y_F16 = 0x200
 PAD_ZERO, PAD_REFLECT = 0, 1
 EPI_NONE, EPI_STATS, EPI_SIGMOID_SCALE, EPI_RESIDUAL, EPI_STAT_SLOTS = 0, 1, 2, 3, 4
 STAT_SLOTS = 16  # UM_STAT_SLOTS (include/umamd.h)
@@ -128,6 +129,9 @@ _SIG = {
     'um_sigmoid_scale_bwd': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
     'um_sigmoid_scale_bwd_split': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
     'um_head_split_fin': (_I, [_L, _I, _P, _I, _P, _F, _P, _I, 's']),
+    'um_head_fwd': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, 's']),
+    'um_head_dgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, 's']),
+    'um_head_wgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, 's']),
     'um_pack_weight_split': (_I, [_P, _I, _I, _I, _I, _P, _P, _I, 's']),
     'um_attn_ws_kstats': (_L, [_I, _I, _I]),
     'um_attn_ws_ctx': (_L, [_I, _I, _I, _I]),
@@ -289,4 +293,6 @@ def dtype_code(dt: torch.dtype) -> int:
         return UM_F32
     if dt == torch.bfloat16:
         return UM_BF16
+    if dt == torch.float16:  # the pre-BN y storage of UM_Y_F16 only
+        return UM_F16
     raise UmamdError(f'unsupported activation dtype {dt}')

@@ -313,10 +313,15 @@ _BN_SLOTS = os.environ.get('UMAMD_BN_SLOTS', '1') == '1'
 #    batch std is ~1/17 of the mean, so the rounding of y is ~17x larger
 #    relative to the normalised x-hat than the rounding of the activations
 _Y_ACT = os.environ.get('UMAMD_Y_ACT', '0') == '1'
+#  - ... or in f16 (UM_Y_F16): 2 bytes like bf16 y with 3 more mantissa bits;
+#    with the centring below the values are O(batch std), far inside f16's range
+_Y_F16 = os.environ.get('UMAMD_Y_F16', '0') == '1'
 
 
 def _ydtype(dt):
     """storage dtype of the pre-BN conv output for activations of ``dt``"""
+    if dt == torch.bfloat16 and _Y_F16:
+        return torch.float16
     return dt if (_Y_ACT and dt == torch.bfloat16) else torch.float32
 
 
@@ -341,7 +346,9 @@ def _ycen(bn, K, dev):
 
 def _ydt(a, y):
     """dtype code of a BN entry: activations ``a`` (a / da), plus UM_Y_ACT
-    when the pre-BN ``y`` is stored in their dtype rather than f32"""
+    when the pre-BN ``y`` is stored in their dtype, UM_Y_F16 when in f16"""
+    if y.dtype == torch.float16:
+        return _dt(a) | L.Y_F16
     return _dt(a) | (L.Y_ACT if y.dtype != torch.float32 else 0)
 
 
@@ -917,6 +924,8 @@ class SkipConvFn(torch.autograd.Function):
         wf_s, wT_s = _pack(weight, Cg, dt, segs=[(fin, 0, skin)])
         wf_f, wT_f = _pack(weight, Cf, dt, segs=[(0, 0, fin)])
         ydt = _ydtype(dt)
+        if ydt == torch.float16:  # the upsample pass into y has no f16 path
+            ydt = torch.float32
         z = _conv_fwd(gs, wf_s, None, K, 1, 1, 0, L.PAD_ZERO, out_dtype=ydt, creal=skin)
 
         def yconv(epi, stats, cbias):
@@ -1442,6 +1451,11 @@ def concat(sources: Sequence[CatSource], N, H, W, dtype):
 _SPLIT_HEAD = os.environ.get('UMAMD_SPLIT_HEAD', '1') == '1'
 
 
+# the 4-output heads as VALU kernels (csrc/head.hip: f32 weights, no
+# packing, no MFMA padding columns); UMAMD_VALU_HEAD=0 keeps the GEMM path
+_VALU_HEAD = os.environ.get('UMAMD_VALU_HEAD', '0') == '1'
+
+
 class DispHeadFn(torch.autograd.Function):
     """disp = scale * sigmoid(Conv3x3reflect(x)) (reference
     model/layers/decoder.py:244-247), all 4 channels."""
@@ -1451,8 +1465,21 @@ class DispHeadFn(torch.autograd.Function):
         N, H, W, Cp = x.shape
         K, Creal, R, _ = weight.shape
         Kp = ceil8(K)
-        split = _SPLIT_HEAD and x.dtype == torch.bfloat16 and 2 * K <= Kp
         bias_f = bias.detach().float().contiguous()
+        valu = _VALU_HEAD and K == 4 and R == 3 and Cp % 32 == 0 and H >= 2 and W >= 2 \
+            and x.stride(-1) == 1
+        ctx.valu = valu
+        if valu:
+            w32 = weight.detach().float().contiguous()
+            d = torch.empty((N, H, W, K), dtype=torch.float32, device=x.device)
+            call('um_head_fwd', _dt(x), N, H, W, Creal, Cp, x.stride(2), ptr(x), ptr(w32),
+                 ptr(bias_f), float(scale), ptr(d), work=_conv_flops(N, H, W, K, R, Creal))
+            ctx.scale, ctx.split = float(scale), False
+            _use(ctx, x)
+            ctx.save_for_backward(x, w32, d)
+            ctx.geom = (K, Kp, Creal, R)
+            return d
+        split = _SPLIT_HEAD and x.dtype == torch.bfloat16 and 2 * K <= Kp
         if split:
             wf, wT = _pack(weight, Cp, x.dtype, ldT=Kp, split=True)
             z = _conv_fwd(x, wf, None, 2 * K, R, 1, 1, L.PAD_REFLECT, out_dtype=torch.float32,
@@ -1485,15 +1512,49 @@ class DispHeadFn(torch.autograd.Function):
         # over the split rows of wT sums dl (w_hi + w_lo)
         call('um_sigmoid_scale_bwd_split' if ctx.split else 'um_sigmoid_scale_bwd', _dt(dl), M,
              K, ptr(d), K, ptr(dd), dd.shape[-1], ctx.scale, ptr(dl), Kp)
-        dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)  # rows K.. unused
-        db = _colsum_grad(dl, Kp)[:K]  # channels K..Kp of dl are zero or a copy
+        if ctx.valu:
+            dW, db = _head_wgrad(x, dl, Kp, Creal)
+        else:
+            dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)  # rows K.. unused
+            db = _colsum_grad(dl, Kp)[:K]  # channels K..Kp of dl are zero or a copy
         dx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and ctx.valu:
+            tgt = _slot(ctx, 0)
+            dxt = tgt if tgt is not None else torch.empty_like(x)
+            call('um_head_dgrad', _dt(x), N, H, W, Creal, Cp, ptr(dl), Kp, ptr(wT), ptr(dxt),
+                 dxt.stride(2), int(tgt is not None),
+                 work=_conv_flops(N, H, W, K, R, Creal))
+            dx = _give(ctx, 0, dxt)
+        elif ctx.needs_input_grad[0]:
             tgt = _slot(ctx, 0)
             dx = _give(ctx, 0, _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT,
                                            dx=tgt, accumulate=tgt is not None, creal=Creal,
                                            kreal=K))
         return dx, dW, db, None
+
+
+def _head_wgrad(x, dl, ldl, Creal):
+    """The head's weight and bias gradients in one VALU launch
+    (um_head_wgrad) into one zeroed f32 buffer [4*Creal*9 + 4] (dW, db views):
+    under overlap.WgradStream it is queued on the weight-gradient side stream
+    like the conv weight gradients (by address: see _conv_wgrad)."""
+    N, H, W, _ = x.shape
+    n = 4 * Creal * 9
+    buf = torch.zeros((n + 4,), dtype=torch.float32, device=x.device)
+    dW, db = buf[:n].view(4, Creal, 3, 3), buf[n:]
+    bp = buf.data_ptr()
+    args = (_dt(x), N, H, W, Creal, x.stride(2), x.data_ptr(), dl.data_ptr(), ldl, bp, bp + 4 * n)
+
+    def launch():
+        call('um_head_wgrad', *args, work=_conv_flops(N, H, W, 4, 3, Creal))
+    ov = _overlap.active()
+    if ov is None:
+        launch()
+    else:
+        buf.record_stream(ov.stream)
+        ov.defer((x, dl), launch, out_ptr=bp, flop=_conv_flops(N, H, W, 4, 3, Creal),
+                 out_bytes=4 * (n + 4))
+    return dW, db
 
 
 def disp_head(x, conv, scale):
