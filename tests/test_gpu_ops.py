@@ -61,6 +61,10 @@ HALO_CASES = [
     (40, 48, 3, 1, 'reflect', 8, 32),
     (64, 16, 3, 1, 'zero', 16, 32),
     (8, 32, 3, 1, 'reflect', 8, 64),
+    # one-chunk 3x3 (32 input channels): resident weights when halo_res_kb
+    # allows (forward and data gradient)
+    (32, 32, 3, 1, 'zero', 16, 64),
+    (32, 64, 3, 1, 'reflect', 8, 64),
     # wider outputs (halo_max_nc): 96- and 128-wide 3x3 column blocks, column
     # grids of 96 / 64 (5x5, 7x7) blocks
     (168, 128, 3, 1, 'reflect', 8, 32),
@@ -72,18 +76,38 @@ HALO_CASES = [
 
 
 @pytest.mark.parametrize('case', HALO_CASES)
-@pytest.mark.parametrize('pf2', [0, 1])
-def test_conv_bn_elu_halo(case, pf2):
-    """the halo kernel forced on; pf2: weight tap rows loaded two rows ahead
-    (knob halo_pf2), forward and data gradient"""
+@pytest.mark.parametrize('pf2,res', [(0, 0), (1, 0), (0, 48)])
+@pytest.mark.parametrize('hgrid', [0, 1, 3])
+def test_conv_bn_elu_halo(case, pf2, res, hgrid):
+    """the halo kernel forced on; weight modes: tap rows streamed (res 0),
+    two rows ahead (pf2, knob halo_pf2), or -- 3x3 whose weights fit res KB
+    (knob halo_res_kb) -- resident in LDS for persistent workgroups; hgrid >
+    0: at most that many workgroups per column block, so each takes several
+    tiles and prefetches the next one's halo (knob halo_grid); forward, BN
+    statistics and data gradient"""
     from umamd._lib import lib
-    old = lib().um_set_tuning(b'halo_min_tiles', 1)
-    old_p = lib().um_set_tuning(b'halo_pf2', pf2)
+    knobs = {b'halo_min_tiles': 1, b'halo_pf2': pf2, b'halo_res_kb': res, b'halo_grid': hgrid}
+    old = {k: lib().um_set_tuning(k, v) for k, v in knobs.items()}
     try:
         test_conv_bn_elu(case, torch.bfloat16)
     finally:
+        for k, v in old.items():
+            lib().um_set_tuning(k, v)
+
+
+@pytest.mark.parametrize('case', HALO_CASES)
+def test_conv_bn_elu_halo_persist_slots(case):
+    """persistent halo workgroups (2 per column block) with the BN statistics
+    in f64 slots: each tile adds its own slot rows"""
+    from umamd import functional as U
+    from umamd._lib import lib
+    old = lib().um_set_tuning(b'halo_min_tiles', 1)
+    old_g = lib().um_set_tuning(b'halo_grid', 2)
+    try:
+        test_conv_bn_elu(case, torch.bfloat16, arena=U.StatArena())
+    finally:
         lib().um_set_tuning(b'halo_min_tiles', old)
-        lib().um_set_tuning(b'halo_pf2', old_p)
+        lib().um_set_tuning(b'halo_grid', old_g)
 
 
 @pytest.mark.parametrize('case', CONV_CASES)
@@ -650,14 +674,15 @@ def test_dgrad_reflect(dtype, case):
 
 # 64x64 LDS-DMA main loop with 3 stages (several blocks per CU) and with 6
 # stages (grids of <= glds_deep_blocks blocks, one 96 KB block per CU), split
-# and unsplit, row- and column-major tile order, forward and data gradient,
-# against f64 torch on the same bf16 operands
+# and unsplit (the split-K finished by each tile's last split in the launch,
+# splitk_fix 1, or by the epilogue kernel, 0), row- and column-major tile
+# order, forward and data gradient, against f64 torch on the same bf16 operands
 @pytest.mark.parametrize('case', [(256, 256, 3, 2, 16, 32), (128, 128, 3, 8, 16, 32),
                                   (512, 512, 3, 2, 8, 16), (128, 192, 1, 4, 16, 32)])
 @pytest.mark.parametrize('deep', [3, 6])
-@pytest.mark.parametrize('split_below', [0, 256])
+@pytest.mark.parametrize('split_below,splitk_fix', [(0, 1), (256, 0), (256, 1)])
 @pytest.mark.parametrize('xcd_col', [0, 2])
-def test_glds_stage_depth(case, deep, split_below, xcd_col):
+def test_glds_stage_depth(case, deep, split_below, splitk_fix, xcd_col):
     from umamd import functional as U
     from umamd._lib import PAD_ZERO, lib
     C, K, R, N, H, W = case
@@ -672,7 +697,7 @@ def test_glds_stage_depth(case, deep, split_below, xcd_col):
     ref_dx = torch.nn.grad.conv2d_input((N, C, H, W), wq, dyq, padding=pad)
     wf, wT = U._pack(w.to(DEV), C, dtype)
     knobs = {b'glds_deep': deep, b'glds_deep_blocks': 1024, b'glds_split_below': split_below,
-             b'halo': 0, b'xcd_col': xcd_col}
+             b'halo': 0, b'xcd_col': xcd_col, b'splitk_fix': splitk_fix}
     old = {k: lib().um_set_tuning(k, v) for k, v in knobs.items()}
     try:
         y = U._conv_fwd(_nhwc(x).to(dtype), wf, None, K, R, 1, pad, PAD_ZERO,

@@ -273,25 +273,6 @@ struct BwdFin {
   float *dgamma, *dbeta, *dbias, *k1, *k2, *k3;
 };
 
-// returns true in the block that must continue (the last arriver)
-__device__ __forceinline__ bool ticket_last(unsigned int* ctr, unsigned int expected, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = t == expected - 1;
-    if (*flag) {
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
 // sum rows [r0, r0+n) of a [rows][W] array (float or double) into out[W]
 // (double), 256 threads: W/lanes columns x row lanes, combined in LDS
 template <typename S>

@@ -214,6 +214,30 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Arrival on an agent-scope counter shared by `expected` workgroups (the
+// producer/consumer recipe of MI355X_MICROARCH.md "Workgroup dispatch":
+// every wave drains its stores, the workgroup barrier, lane 0 releases, then
+// the relaxed add).  Returns true in the workgroup that arrived last, after
+// its acquire, so it may read what the others stored; that workgroup resets
+// the counter to 0 for the next use.  `flag`: an LDS int.
+__device__ __forceinline__ bool ticket_last(unsigned int* ctr, unsigned int expected, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = t == expected - 1;
+    if (*flag) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
 // ------------------------------------------------- BN statistics slots --
 // Per-channel (sum, sum of squares) accumulated straight into f64 "slots"
 // [UM_STAT_SLOTS][C][2] (zeroed by the caller) by no-return f64 atomics: the

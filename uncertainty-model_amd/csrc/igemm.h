@@ -45,6 +45,9 @@ struct IgArgs {
   int stat_slots;   // UM_EPI_STAT_SLOTS: stats is double[UM_STAT_SLOTS][NC][2]
   int colmajor;     // tile order, set by igemm_run (knob xcd_col)
   int tappack;      // 4 taps x 8 channels per k-step (ach == 8), set by igemm_run
+  // split-K finished inside the launch (knob splitk_fix): 0 = the separate
+  // epilogue kernel; k > 0 = arrival counters of region k-1 (igemm.hip)
+  int splitk_fix;
 };
 
 // rows per BN partial-statistics row of a stats epilogue (M, NC of the GEMM)
@@ -71,6 +74,12 @@ int igemm_pad_dgrad();
 
 // halo conv weight rows two rows ahead (knob "halo_pf2", UMAMD_HALO_PF2)
 int igemm_halo_pf2();
+// halo conv grid: persistent workgroups per resident slot (knob
+// "halo_persist", 0 = one tile per workgroup) and a grid cap ("halo_grid")
+int igemm_halo_persist();
+int igemm_halo_grid();
+// resident-weight LDS budget (KB) of the 3x3 halo convs ("halo_res_kb", 0 = off)
+int igemm_halo_res_kb();
 
 // fill the border-list fields of a (oh, ow, fold_pad set) and return the
 // number of listed pixels per image

@@ -423,9 +423,15 @@ class GradSlots:
     buffer and hands that to autograd; every later one ACCUMULATES into the
     same buffer (GEMM / concat-adjoint accumulate epilogues) and returns None,
     so autograd sums nothing -- it would launch one elementwise add per extra
-    consumer (12 bf16 adds per step).  Consumers outside a model forward
-    (the loss, user code) are not registered and go through autograd as
-    usual, which stays correct: autograd adds their gradient to the buffer's.
+    consumer (12 bf16 adds per step).
+    Limitation: a tensor with two or more registered consumers must have NO
+    unregistered one (the loss, user code).  Autograd would sum that
+    consumer's gradient with the first registered one's into a new buffer
+    (or into that buffer in place, by its own choice), so a later registered
+    consumer's accumulate could land in a tensor autograd no longer passes
+    on: its term would be lost.  In the model every pooled tensor is
+    consumed only inside the forward (the disparities, which the loss reads,
+    have a single registered use and are never pooled).
     UMAMD_GRAD_SLOTS=0 turns it off."""
 
     def __init__(self):
