@@ -632,7 +632,10 @@ def test_dgrad_odd_tiles(dtype, case):
     (320, 256, 3, 2, 8, 16, False),   # split-K
     (88, 64, 3, 2, 8, 64, True),      # split form on the 96-wide halo blocks
 ])
-def test_dgrad_reflect(dtype, case):
+@pytest.mark.parametrize('border_valu', [0, 2])
+def test_dgrad_reflect(dtype, case, border_valu):
+    """border_valu: the split form's reflect fold as the VALU border pass
+    (2: every shape) or as the register GEMM's border-list mode (0)"""
     from umamd import functional as U
     from umamd._lib import PAD_REFLECT, lib
     C, K, R, N, H, W, accumulate = case
@@ -657,6 +660,7 @@ def test_dgrad_reflect(dtype, case):
         old = lib().um_set_tuning(b'halo_min_tiles', hmin)
         old_s = lib().um_set_tuning(b'fold_split_nc', snc)
         old_p = lib().um_set_tuning(b'pad_dgrad', pd)
+        old_b = lib().um_set_tuning(b'border_valu', border_valu)
         try:
             dx = _nhwc(dx0).to(dtype).contiguous() if accumulate else None
             out = U._conv_dgrad(_nhwc(dy).to(dtype), wT, (N, H, W, C), K, R, 1, pad, PAD_REFLECT,
@@ -666,6 +670,7 @@ def test_dgrad_reflect(dtype, case):
             lib().um_set_tuning(b'halo_min_tiles', old)
             lib().um_set_tuning(b'fold_split_nc', old_s)
             lib().um_set_tuning(b'pad_dgrad', old_p)
+            lib().um_set_tuning(b'border_valu', old_b)
         err = _rel(_nchw(out), ref)
         print(f'dgrad_reflect {case} {dtype} halo_min_tiles={hmin} fold_split_nc={snc} '
               f'pad_dgrad={pd}: rel {err:.3e}')

@@ -771,6 +771,70 @@ __global__ void __launch_bounds__(256) colsum_fin_batch_kernel(CsBatch b) {
 // Reflect-pad data gradient, padded form: dxp[n][Y][X] (the gradient of the
 // reflect-padded input, (H+2p) x (W+2p), from a zero-pad transposed conv
 // on the fast GEMM paths) folded onto dx: x_pad[Y] = x[refl(Y - p)], so
+// The reflect fold of a split-form data gradient as a VALU pass over the
+// border list (umamd::border_pixel): border pixel (n, i, j) of dx adds, for
+// every tap (r, s), the dy sources that reach it only through the reflect
+// pad -- rows -i - p' + r (1 <= i <= pad) and 2(H-1) - i - p' + r
+// (H-1-pad <= i <= H-2), columns likewise, p' = a.pad = R-1-pad, every
+// (row, column) pair but the plain one -- times the flipped tap's weights.
+// The same sums as the register GEMM's border mode (igemm.hip gather, IG_FOLD
+// + border), without its per-k-step gather chain: thread per (border pixel,
+// 8 dx channels), all of a pair's dy chunks and weight rows loaded before
+// they are summed.
+template <typename T>
+__global__ void __launch_bounds__(256) reflect_border_kernel(umamd::IgArgs a) {
+  const int cg = a.NC / 8;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)a.M * cg) return;
+  const int m = (int)(gid / cg), c0 = (int)(gid - (long)m * cg) * 8;
+  int n, oy, ox;
+  umamd::border_pixel(a, m, n, oy, ox);
+  const T* __restrict__ dy = reinterpret_cast<const T*>(a.a) + (long)n * a.ah * a.aw * a.lda;
+  const T* __restrict__ wT = reinterpret_cast<const T*>(a.b);
+  const int H = a.oh, W = a.ow, fp = a.fold_pad, R = a.R, K = a.ach;
+  const bool lo_y = oy >= 1 && oy <= fp, hi_y = oy >= H - 1 - fp && oy <= H - 2;
+  const bool lo_x = ox >= 1 && ox <= fp, hi_x = ox >= W - 1 - fp && ox <= W - 2;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = 0; r < R; ++r) {
+    const int yy = oy - a.pad + r;
+    int ys[3], ny = 0;
+    const bool iny = yy >= 0 && yy < a.ah;
+    if (iny) ys[ny++] = yy;
+    if (lo_y) { const int t = -oy - a.pad + r; if (t >= 0 && t < a.ah) ys[ny++] = t; }
+    if (hi_y) { const int t = 2 * (H - 1) - oy - a.pad + r; if (t >= 0 && t < a.ah) ys[ny++] = t; }
+    for (int s = 0; s < R; ++s) {
+      const int xx = ox - a.pad + s;
+      int xs[3], nx = 0;
+      const bool inx = xx >= 0 && xx < a.aw;
+      if (inx) xs[nx++] = xx;
+      if (lo_x) { const int t = -ox - a.pad + s; if (t >= 0 && t < a.aw) xs[nx++] = t; }
+      if (hi_x) { const int t = 2 * (W - 1) - ox - a.pad + s; if (t >= 0 && t < a.aw) xs[nx++] = t; }
+      const int btap = (R - 1 - r) * R + (R - 1 - s);
+      for (int u = 0; u < ny; ++u)
+        for (int q = 0; q < nx; ++q) {
+          if (u == 0 && q == 0 && iny && inx) continue;  // the zero-pad pass summed it
+          const T* src = dy + ((long)ys[u] * a.aw + xs[q]) * a.lda;
+          for (int k0 = 0; k0 < K; k0 += 8) {
+            float dv[8], wv[8][8];
+            load8(src + k0, dv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) load8(wT + (long)(c0 + e) * a.ldb + (long)btap * K + k0, wv[e]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+#pragma unroll
+              for (int kk = 0; kk < 8; ++kk) acc[e] += dv[kk] * wv[e][kk];
+          }
+        }
+    }
+  }
+  T* o = reinterpret_cast<T*>(a.out) + (((long)n * H + oy) * W + ox) * a.ld_out + c0;
+  float t[8];
+  load8(o, t);  // the zero-pad pass wrote these pixels: always accumulate
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] += acc[e];
+  store8(o, t);
+}
+
 // dx[i] sums dxp[i + p], dxp[p - i] (1 <= i <= p) and dxp[2(H-1) + p - i]
 // (H-1-p <= i <= H-2), separably in y and x.  Thread per (pixel, 8 channels).
 template <typename T>
@@ -1144,6 +1208,21 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
     a.fold_pad = pad;
     a.accumulate = 1;
     a.M = N * umamd::igemm_border_list(a);
+    // 8-channel dy (the disparity heads): the border list as a VALU pass,
+    // else as a register-path GEMM (igemm.hip).  Micro-benchmark on MI355X
+    // (tools/border_micro.sh r04aa): 256x512 C32 K8 80.9 -> 77.2 us, 128x256
+    // C64 K8 59.5 -> 55.5; at K = 32 / 64 the GEMM stays ahead (144 vs 163,
+    // 59 vs 83 us).  Knob border_valu: 0 never, 1 K <= 8, 2 always
+    const int bv = umamd::igemm_border_valu();
+    if ((bv == 2 || (bv == 1 && K <= 8)) && C % 8 == 0 && K % 8 == 0 && ldx % 8 == 0 && a.M > 0) {
+      const long threads = (long)a.M * (C / 8);
+      if (dtype == UM_BF16)
+        hipLaunchKernelGGL(reflect_border_kernel<bf16_t>, dim3(ceil_div(threads, 256)), dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL(reflect_border_kernel<float>, dim3(ceil_div(threads, 256)), dim3(256), 0, st, a);
+      UM_LAUNCH_CHECK();
+      return UM_OK;
+    }
     return umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
   }
   // stride 2 (zero padding): four parity classes (ay, ax) of dx pixels, each

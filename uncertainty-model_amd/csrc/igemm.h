@@ -50,6 +50,32 @@ struct IgArgs {
   int splitk_fix;
 };
 
+__device__ __forceinline__ int pick4(const int (&v)[4], int i) {
+  return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
+}
+
+// border-list mode: listed pixel m -> (n, y, x); rows rr[] (ascending) are
+// listed whole, the other rows at the columns rc[]
+__device__ __forceinline__ void border_pixel(const IgArgs& a, int m, int& n, int& y, int& x) {
+  const int W = a.ow, full = a.nrr * W;
+  const int per = full + (a.oh - a.nrr) * a.nrc;
+  n = m / per;
+  int k = m - n * per;
+  if (k < full) {
+    const int i = k / W;
+    y = pick4(a.rr, i);
+    x = k - i * W;
+    return;
+  }
+  k -= full;
+  const int idx = k / a.nrc;
+  x = pick4(a.rc, k - idx * a.nrc);
+  y = idx;  // the idx-th row not in rr[]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < a.nrr && pick4(a.rr, j) <= y) ++y;
+}
+
 // rows per BN partial-statistics row of a stats epilogue (M, NC of the GEMM)
 int igemm_stats_rows(int M, int NC);
 
@@ -80,6 +106,8 @@ int igemm_halo_persist();
 int igemm_halo_grid();
 // resident-weight LDS budget (KB) of the 3x3 halo convs ("halo_res_kb", 0 = off)
 int igemm_halo_res_kb();
+// reflect fold of the split-form data gradient as a VALU pass ("border_valu")
+int igemm_border_valu();
 
 // fill the border-list fields of a (oh, ow, fold_pad set) and return the
 // number of listed pixels per image

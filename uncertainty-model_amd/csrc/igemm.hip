@@ -112,32 +112,6 @@ struct ARow {
   bool ok;
 };
 
-__device__ __forceinline__ int pick4(const int (&v)[4], int i) {
-  return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
-}
-
-// border-list mode: listed pixel m -> (n, y, x); rows rr[] (ascending) are
-// listed whole, the other rows at the columns rc[]
-__device__ __forceinline__ void border_pixel(const IgArgs& a, int m, int& n, int& y, int& x) {
-  const int W = a.ow, full = a.nrr * W;
-  const int per = full + (a.oh - a.nrr) * a.nrc;
-  n = m / per;
-  int k = m - n * per;
-  if (k < full) {
-    const int i = k / W;
-    y = pick4(a.rr, i);
-    x = k - i * W;
-    return;
-  }
-  k -= full;
-  const int idx = k / a.nrc;
-  x = pick4(a.rc, k - idx * a.nrc);
-  y = idx;  // the idx-th row not in rr[]
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (j < a.nrr && pick4(a.rr, j) <= y) ++y;
-}
-
 // MODE: 0 plain rows, 1 parity class rows (stride-2 data gradient), 2 the
 // border list of the reflect fold (IgArgs::border)
 template <int MODE>
@@ -990,6 +964,7 @@ struct Knobs {
   int halo_max_nc;
   int halo_pf2;
   int halo_persist, halo_grid, halo_res_kb;
+  int border_valu;
   int splitk_fix;
   Knobs() {
     auto env = [](const char* n, int d) {
@@ -1057,6 +1032,9 @@ struct Knobs {
     // 3x3 halo convs keep all their tap weights in LDS (per workgroup, for
     // all its tiles) when they need at most this many KB; 0 = stream rows
     halo_res_kb = env("UMAMD_HALO_RES_KB", 48);
+    // reflect fold of the split-form data gradient: a VALU pass over the
+    // border list (conv.hip reflect_border_kernel) instead of the GEMM
+    border_valu = env("UMAMD_BORDER_VALU", 1);
     // split-K of the LDS-DMA tiles finished by each tile's last split in the
     // launch instead of a splitk_epilogue_kernel launch (partials of a group
     // of splits loaded at once).  Bench step A/B on MI355X (tools/gpu_ab.sh
@@ -1245,6 +1223,7 @@ int igemm_halo_pf2() { return knobs().halo_pf2; }
 int igemm_halo_persist() { return knobs().halo_persist; }
 int igemm_halo_grid() { return knobs().halo_grid; }
 int igemm_halo_res_kb() { return knobs().halo_res_kb; }
+int igemm_border_valu() { return knobs().border_valu; }
 
 int igemm_border_list(IgArgs& a) {
   const int H = a.oh, W = a.ow, p = a.fold_pad;
@@ -1371,6 +1350,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "halo_persist")) f = &k.halo_persist;
   else if (!strcmp(key, "halo_grid")) f = &k.halo_grid;
   else if (!strcmp(key, "halo_res_kb")) f = &k.halo_res_kb;
+  else if (!strcmp(key, "border_valu")) f = &k.border_valu;
   else if (!strcmp(key, "splitk_fix")) f = &k.splitk_fix;
   if (!f) return -1;
   const int old = *f;

@@ -37,6 +37,7 @@ stream (``stream=``).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -96,6 +97,16 @@ class CapturedTrainStep:
             self.overlap = overlap.WgradStream(p for p in model.parameters() if p.requires_grad)
         self.left = left.detach().clone().contiguous()
         self.right = right.detach().clone().contiguous()
+        # UMAMD_LOSS_OVERLAP=1: the fused loss forward (the loss values) on a
+        # side stream beside the backward (umamd.lossfn.forward_on_side_stream).
+        # Off: bench step A/B on MI355X 763 with vs 766 pairs/s without
+        # (profiles/r04/loss_overlap_arms.txt) -- the loss tiles contend with
+        # the backward's first kernels instead of filling idle CUs
+        self._loss_stream = None
+        if os.environ.get('UMAMD_LOSS_OVERLAP', '0') != '0':
+            self._loss_stream = torch.cuda.Stream(device=self.left.device)
+        self._one = torch.ones((), dtype=torch.float32, device=self.left.device)
+        self._loss_events = []
         cur = torch.cuda.current_stream()
         side = stream if stream is not None else torch.cuda.Stream()
         if side != cur:
@@ -180,18 +191,33 @@ class CapturedTrainStep:
                 recon = u.reconstruct_pyramid(disparities, pyramid)
         else:
             recon = u.reconstruct_pyramid(disparities, pyramid)
-        disp_loss, error_loss = self.loss_function(pyramid, disparities, recon, 0, None)
+        side = self._loss_stream if isinstance(self.loss_function, TukraUncertaintyLoss) else None
+        events = []
+        with (LF.forward_on_side_stream(side, events) if side is not None
+              else contextlib.nullcontext()):
+            disp_loss, error_loss = self.loss_function(pyramid, disparities, recon, 0, None)
+
+        def backward():
+            if side is not None:
+                # d(disp + error)/d(each) = 1 without reading the values (a sum
+                # would wait for the loss forward on the side stream)
+                torch.autograd.backward([disp_loss, error_loss], [self._one, self._one])
+            else:
+                (disp_loss + error_loss).backward()
         if self.overlap is None:
             if self._buckets is not None:
                 self._buckets.arm()
-            (disp_loss + error_loss).backward()
+            backward()
         else:
             with self.overlap:
                 if self._buckets is not None:
                     self._buckets.arm()  # buckets launch from the backward's hooks
-                (disp_loss + error_loss).backward()
+                backward()
         if self._buckets is not None:
             self._reduce_grads()
+        if side is not None:  # the loss values join the step
+            overlap.stream_wait(torch.cuda.current_stream(), side, events)
+            self._loss_events = events  # alive until the next capture or step
         return disp_loss, error_loss
 
     @property

@@ -36,6 +36,26 @@ LOSS_TYPES = {'l1': 0, 'bayesian': 1, 'log_bayesian': 2}
 MAX_LEVELS = 6
 
 _defer = [False]
+# (stream, events) while forward_on_side_stream is active
+_side = [None, None]
+
+
+@contextlib.contextmanager
+def forward_on_side_stream(stream, events: list):
+    """Inside this context TukraLossFn's forward kernel -- the loss VALUES,
+    which no gradient needs -- runs on ``stream`` (after it waits for the
+    current stream), so it overlaps the backward pass that follows on the
+    current stream: um_loss_bwd re-derives everything it needs.  The caller
+    joins ``stream`` back before anything reads the losses (train.graph's
+    captured step, which also backpropagates with explicit unit gradients
+    instead of reading the values in a sum).  ``events``: the fork/join
+    events, kept alive by the caller (overlap.stream_wait)."""
+    prev = list(_side)
+    _side[0], _side[1] = stream, events
+    try:
+        yield stream
+    finally:
+        _side[0], _side[1] = prev
 
 
 @contextlib.contextmanager
@@ -238,15 +258,29 @@ class TukraLossFn(torch.autograd.Function):
                          device=dev)
         emap = torch.empty((N, 2, H >> (n - 1), W >> (n - 1)), dtype=torch.float32, device=dev)
         out = torch.empty(6, dtype=torch.float32, device=dev)
-        call('um_loss_fwd', n, N, H, W, _parr(pyr), _parr(preds), cfg['alpha'],
-             cfg['loss_type'], cfg['esw'], cfg['ecw'], cfg['w_wssim'], cfg['w_cons'],
-             cfg['w_smooth'], cfg['w_err'], ptr(ws), ptr(emap), rarr, ptr(out))
+        dl = torch.empty((), dtype=torch.float32, device=dev)
+        el = torch.empty_like(dl)
+
+        def launch():
+            call('um_loss_fwd', n, N, H, W, _parr(pyr), _parr(preds), cfg['alpha'],
+                 cfg['loss_type'], cfg['esw'], cfg['ecw'], cfg['w_wssim'], cfg['w_cons'],
+                 cfg['w_smooth'], cfg['w_err'], ptr(ws), ptr(emap), rarr, ptr(out))
+            dl.copy_(out[0])
+            el.copy_(out[1])
+        side, events = _side
+        if side is None:
+            launch()
+        else:
+            from .overlap import stream_wait
+            stream_wait(side, torch.cuda.current_stream(), events)
+            for t in (ws, emap, out, dl, el, *preds, *pyr, *(recon_out or ())):
+                t.record_stream(side)
+            with torch.cuda.stream(side):
+                launch()
         ctx.cfg = cfg
         ctx.n = n
         ctx.geom = (N, H, W)
         ctx.save_for_backward(*preds, *pyr)
-        dl = out[0].clone()
-        el = out[1].clone()
         ctx.mark_non_differentiable(out, emap)
         return dl, el, out, emap
 
