@@ -679,15 +679,14 @@ def test_dgrad_reflect(dtype, case, border_valu):
 
 # 64x64 LDS-DMA main loop with 3 stages (several blocks per CU) and with 6
 # stages (grids of <= glds_deep_blocks blocks, one 96 KB block per CU), split
-# and unsplit (the split-K finished by each tile's last split in the launch,
-# splitk_fix 1, or by the epilogue kernel, 0), row- and column-major tile
-# order, forward and data gradient, against f64 torch on the same bf16 operands
+# and unsplit, row- and column-major tile order, forward and data gradient,
+# against f64 torch on the same bf16 operands
 @pytest.mark.parametrize('case', [(256, 256, 3, 2, 16, 32), (128, 128, 3, 8, 16, 32),
                                   (512, 512, 3, 2, 8, 16), (128, 192, 1, 4, 16, 32)])
 @pytest.mark.parametrize('deep', [3, 6])
-@pytest.mark.parametrize('split_below,splitk_fix', [(0, 1), (256, 0), (256, 1)])
+@pytest.mark.parametrize('split_below', [0, 256])
 @pytest.mark.parametrize('xcd_col', [0, 2])
-def test_glds_stage_depth(case, deep, split_below, splitk_fix, xcd_col):
+def test_glds_stage_depth(case, deep, split_below, xcd_col):
     from umamd import functional as U
     from umamd._lib import PAD_ZERO, lib
     C, K, R, N, H, W = case
@@ -702,7 +701,7 @@ def test_glds_stage_depth(case, deep, split_below, splitk_fix, xcd_col):
     ref_dx = torch.nn.grad.conv2d_input((N, C, H, W), wq, dyq, padding=pad)
     wf, wT = U._pack(w.to(DEV), C, dtype)
     knobs = {b'glds_deep': deep, b'glds_deep_blocks': 1024, b'glds_split_below': split_below,
-             b'halo': 0, b'xcd_col': xcd_col, b'splitk_fix': splitk_fix}
+             b'halo': 0, b'xcd_col': xcd_col}
     old = {k: lib().um_set_tuning(k, v) for k, v in knobs.items()}
     try:
         y = U._conv_fwd(_nhwc(x).to(dtype), wf, None, K, R, 1, pad, PAD_ZERO,

@@ -45,9 +45,6 @@ struct IgArgs {
   int stat_slots;   // UM_EPI_STAT_SLOTS: stats is double[UM_STAT_SLOTS][NC][2]
   int colmajor;     // tile order, set by igemm_run (knob xcd_col)
   int tappack;      // 4 taps x 8 channels per k-step (ach == 8), set by igemm_run
-  // split-K finished inside the launch (knob splitk_fix): 0 = the separate
-  // epilogue kernel; k > 0 = arrival counters of region k-1 (igemm.hip)
-  int splitk_fix;
 };
 
 __device__ __forceinline__ int pick4(const int (&v)[4], int i) {

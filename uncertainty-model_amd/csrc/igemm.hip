@@ -601,65 +601,6 @@ __device__ __forceinline__ void igemm_tile(const IgArgs& a, float* __restrict__ 
 // barriers are raw s_barrier, so the DMA stays in flight across them.
 __device__ __attribute__((aligned(16))) unsigned int g_zero_page[4];
 
-// Split-K arrival counters (ticket_last, self-resetting): SPLITK_REGIONS
-// regions of SPLITK_TILES, one counter per output tile; the host hands each
-// split launch the next region in turn, so launches that could overlap (the
-// weight-gradient side stream runs no split igemm) would not share counters.
-constexpr int SPLITK_REGIONS = 64, SPLITK_TILES = 1024;
-__device__ unsigned int g_splitk_tk[SPLITK_REGIONS * SPLITK_TILES];
-
-// acc (MFMA layout of an igemm_epilogue tile) = the sum of the `splits`
-// partial tiles in ws, in split order.  The loads of ZG splits are issued
-// before any is summed (one memory round trip per group, not per split:
-// round 2's in-GEMM finish read its partials one split after another).
-template <int BM, int BN, int WM, int WN>
-__device__ __forceinline__ void splitk_sum(const IgArgs& a, const float* __restrict__ ws,
-                                           f32x4_t (&acc)[BM / WM / 16][BN / WN / 16], int bm,
-                                           int bn, int splits) {
-  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-  constexpr int ZG = TM * TN <= 2 ? 8 : 4;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int col_l = lane & 15, row_g = (lane >> 4) * 4;
-  const long zs = (long)a.M * a.NC;
-  // this lane's element offsets (-1: outside the GEMM)
-  long off[TM][TN][4];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const int n = bn + wn * (BN / WN) + j * 16 + col_l;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = bm + wm * (BM / WM) + i * 16 + row_g + q;
-        off[i][j][q] = (n < a.NC && m < a.M) ? (long)m * a.NC + n : -1;
-      }
-    }
-  for (int z0 = 0; z0 < splits; z0 += ZG) {
-    float v[ZG][TM][TN][4];
-#pragma unroll
-    for (int u = 0; u < ZG; ++u)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const long o = off[i][j][q];
-            v[u][i][j][q] = (z0 + u < splits && o >= 0) ? ws[(z0 + u) * zs + o] : 0.f;
-          }
-#pragma unroll
-    for (int u = 0; u < ZG; ++u)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[i][j][q] += v[u][i][j][q];
-  }
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -840,22 +781,6 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
   __syncthreads();
   constexpr int STAT_ELEMS = (WM * BN * 2 * 4 + 15) / 16 * 8;  // bf16 elements, 16-B aligned
   static_assert(STAT_ELEMS + BM * BN <= NST * STAGE, "staged epilogue fits the staging LDS");
-  if constexpr (SPLIT) {
-    if (a.splitk_fix > 0) {
-      // every split stores its partial tile; the tile's last arriver sums
-      // the partials (fixed split order: deterministic) and runs the plain
-      // epilogue -- no split-K epilogue launch
-      __shared__ int last;
-      igemm_epilogue<bf16_t, BM, BN, WM, WN, true, MODE>(a, ws, acc, bm, bn, nullptr, nullptr);
-      unsigned int* ctr = g_splitk_tk + (long)(a.splitk_fix - 1) * SPLITK_TILES + blockIdx.x;
-      if (!ticket_last(ctr, gridDim.z, &last)) return;
-      splitk_sum<BM, BN, WM, WN>(a, ws, acc, bm, bn, gridDim.z);
-      igemm_epilogue<bf16_t, BM, BN, WM, WN, false, MODE>(a, ws, acc, bm, bn,
-                                                         reinterpret_cast<float*>(smem),
-                                                         smem + STAT_ELEMS);
-      return;
-    }
-  }
   igemm_epilogue<bf16_t, BM, BN, WM, WN, SPLIT, MODE>(a, ws, acc, bm, bn,
                                                      reinterpret_cast<float*>(smem),
                                                      smem + STAT_ELEMS);
@@ -965,7 +890,6 @@ struct Knobs {
   int halo_pf2;
   int halo_persist, halo_grid, halo_res_kb;
   int border_valu;
-  int splitk_fix;
   Knobs() {
     auto env = [](const char* n, int d) {
       const char* v = getenv(n);
@@ -1035,14 +959,6 @@ struct Knobs {
     // reflect fold of the split-form data gradient: a VALU pass over the
     // border list (conv.hip reflect_border_kernel) instead of the GEMM
     border_valu = env("UMAMD_BORDER_VALU", 1);
-    // split-K of the LDS-DMA tiles finished by each tile's last split in the
-    // launch instead of a splitk_epilogue_kernel launch (partials of a group
-    // of splits loaded at once).  Bench step A/B on MI355X (tools/gpu_ab.sh
-    // r04u): 752-756 with vs 763 pairs/s without -- every split's agent-scope
-    // release of its partial tile and the last split's acquire + re-read cost
-    // more than the epilogue launch, as in round 2 (MI355X_MICROARCH.md
-    // "splitk-seam"): off
-    splitk_fix = env("UMAMD_IG_SPLITK_FIX", 0);
   }
 };
 Knobs& knobs() {
@@ -1125,12 +1041,7 @@ int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
       const long blocks = (long)ntm * ntn * p.splits;
       const bool deep = BM == 64 && w8 && knobs().glds_deep > 3 && blocks <= knobs().glds_deep_blocks;
       constexpr int DEEP = BM == 64 ? 6 : 3;  // 96 KB of stages: 64x64 tiles only
-      // split-K finished in the launch (the tile's last split runs the epilogue)
-      IgArgs g = a;
-      if (p.splits > 1 && knobs().splitk_fix && ntm * ntn <= SPLITK_TILES) {
-        static unsigned int region = 0;
-        g.splitk_fix = 1 + (int)(region++ % SPLITK_REGIONS);
-      }
+      const IgArgs& g = a;
       const dim3 grid(ntm * ntn, 1, p.splits);
       if (deep && p.splits > 1)
         hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 8, true, MODE, DEEP>), grid, dim3(512), 0, st, g,
@@ -1150,7 +1061,7 @@ int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
       else
         hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, false, MODE, 3>), grid, dim3(256), 0, st, g, ws,
                            p.steps, p.per, ntn);
-      if (p.splits > 1 && g.splitk_fix == 0)
+      if (p.splits > 1)
         hipLaunchKernelGGL((splitk_epilogue_kernel<T, MODE>),
                            dim3(ceil_div(a.M, a.stats_rows), ceil_div(a.NC, EPI_COLS)), dim3(256), 0,
                            st, a, (const float*)ws, p.splits);
@@ -1351,7 +1262,6 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "halo_grid")) f = &k.halo_grid;
   else if (!strcmp(key, "halo_res_kb")) f = &k.halo_res_kb;
   else if (!strcmp(key, "border_valu")) f = &k.border_valu;
-  else if (!strcmp(key, "splitk_fix")) f = &k.splitk_fix;
   if (!f) return -1;
   const int old = *f;
   *f = value;
