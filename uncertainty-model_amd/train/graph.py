@@ -75,8 +75,13 @@ class CapturedTrainStep:
         self._buckets = None
         if self.group is not None:
             # bucketed all-reduce overlapped with the backward (umamd.gradsync);
-            # UMAMD_GRAD_BUCKET_MB sizes the buckets, 0 = one all-reduce at the end
-            mb = float(os.environ.get('UMAMD_GRAD_BUCKET_MB', '16'))
+            # UMAMD_GRAD_BUCKET_MB sizes the buckets, 0 = one all-reduce at the
+            # end.  A one-rank group has no peer to overlap with: there the
+            # buckets' packs and per-bucket collectives only cost (one-rank
+            # SyncBN step on MI355X: 750 bucketed vs 795 pairs/s with one
+            # all-reduce, dp1 805), so the default is one all-reduce
+            default_mb = '16' if self.world > 1 else '0'
+            mb = float(os.environ.get('UMAMD_GRAD_BUCKET_MB', default_mb))
             self._buckets = GradBuckets(model.parameters(), self.group, self.world,
                                         cap_mb=mb if mb > 0 else 1e9)
         # RCCL collectives of the step (SyncBN, gradient buckets) through the
