@@ -144,8 +144,12 @@ def test_config2_trajectory_vs_reference():
     bayesian error loss falls 28.7 -> 9.6 in 10 steps, and Adam's first
     updates are lr * sign(g), so elements whose gradient is at summation-noise
     level move either way: two eager runs of our own path drift 1e-3..4e-3 by
-    steps 5-8 (test_gpu_graph), so later steps are held to 2e-2.  bf16: step 0
-    within the bf16 bar (1e-2 disp, 3e-2 error)."""
+    steps 5-8 (test_gpu_graph), so later steps are held to 2e-2.
+    bf16 (the bench's dtype): step 0 within 1e-3 (disparity loss) and 2e-3
+    (error loss; DESIGN §2: 1.25e-3 measured), and over the 10 steps within
+    1e-2 AND no further from the reference's fp32 trajectory than the
+    reference itself under torch.autocast('cpu', bf16) is (traj_c2_bf16.npz:
+    3.9e-3 at step 0, 1.6e-2 over 10 steps on the error loss)."""
     z = _z('traj_c2.npz')
     n = sum(1 for k in z.files if k.startswith('disp_loss_'))
     ref = [(float(z[f'disp_loss_{i}']), float(z[f'error_loss_{i}'])) for i in range(n)]
@@ -154,9 +158,17 @@ def test_config2_trajectory_vs_reference():
     print('fp32 trajectory rel deltas', [(round(x, 6), round(y, 6)) for x, y in rel])
     assert rel[0][0] < 1e-3 and rel[0][1] < 1e-3, rel[0]
     assert max(max(r) for r in rel) < 2e-2, rel
-    g16 = _trajectory('bf16', 1)
-    assert abs(g16[0][0] / ref[0][0] - 1) < 1e-2 and abs(g16[0][1] / ref[0][1] - 1) < 3e-2, \
-        (g16, ref[0])
+    g16 = _trajectory('bf16', n)
+    r16 = [(abs(a[0] / b[0] - 1), abs(a[1] / b[1] - 1)) for a, b in zip(g16, ref)]
+    zb = _z('traj_c2_bf16.npz')
+    refb = [(float(zb[f'disp_loss_{i}']), float(zb[f'error_loss_{i}'])) for i in range(n)]
+    rb = [(abs(a[0] / b[0] - 1), abs(a[1] / b[1] - 1)) for a, b in zip(refb, ref)]
+    print('bf16 trajectory rel deltas', [(round(x, 6), round(y, 6)) for x, y in r16])
+    print('reference bf16-autocast rel deltas', [(round(x, 6), round(y, 6)) for x, y in rb])
+    assert r16[0][0] < 1e-3 and r16[0][1] < 2e-3, r16[0]
+    for j in range(2):
+        worst, worst_ref = max(r[j] for r in r16), max(r[j] for r in rb)
+        assert worst < 1e-2 and worst <= worst_ref, (j, worst, worst_ref)
 
 
 def test_train_model_graph_replay_matches_eager(monkeypatch):
