@@ -361,6 +361,17 @@ int um_merge_parts(long count);
 int um_merge_bwd(int dtype, int nsrc, const void* const* srcs, void* const* dsrcs,
                  const int* accumulate, const int* widx, const float* w, const float* coefs,
                  long count, const void* dm, float* parts, hipStream_t stream);
+/* um_merge_bwd that also takes the BN-ELU backward statistics of source fsrc,
+ * whose gradient dsrcs[fsrc] it completes (the same sums as
+ * um_bn_elu_bwd_reduce_slots over that gradient as stored, into `slots`):
+ * reference model/layers/encoder.py:115-124 (merge) + 42-44 (BN+ELU).
+ * dtype: activation dtype | UM_Y_ACT / UM_Y_F16 (the pre-BN y's type);
+ * C / 8 must divide 256 */
+int um_merge_bwd_bn(int dtype, int nsrc, const void* const* srcs, void* const* dsrcs,
+                    const int* accumulate, const int* widx, const float* w, const float* coefs,
+                    long count, const void* dm, float* parts, int fsrc, const void* y, int C,
+                    const float* mean, const float* invstd, const float* scale,
+                    const float* shift, int apply_elu, double* slots, hipStream_t stream);
 int um_merge_wgrad(const float* parts, int nparts, int nsrc, const int* widx,
                    const float* w, float* dw, int nw, int accumulate, hipStream_t stream);
 int um_image_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp,

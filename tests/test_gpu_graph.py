@@ -344,6 +344,55 @@ def test_fused_merge_matches_separate_merge(dtype):
 
 
 @pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_merge_bn_reduce_matches_separate_reduce(dtype):
+    """A GraphBlock node's BN-backward sums taken by the merge backward that
+    completes its gradient (um_merge_bwd_bn) against the separate
+    um_bn_elu_bwd_reduce_slots launch: the same sums over the same stored
+    gradient, in another partial-sum order -> equal disparities, gradients
+    within f32 summation noise."""
+    from umamd import functional as U
+    cfg = _cfg('config.yml')
+    left, _ = _uniform_pair(2, 64, 128, seed=7)
+    left = left.to(DEV)
+    res = []
+    old = U._MERGE_BN_REDUCE
+    calls = []
+    orig = U._merge_bn_target
+
+    def spy(*args):
+        r = orig(*args)
+        calls.append(r is not None)
+        return r
+    U._merge_bn_target = spy
+    try:
+        for flag in (True, False):
+            U._MERGE_BN_REDUCE = flag
+            m = _model(cfg, dtype).train()
+            d = m(left, 0.3)
+            (sum((t.float() ** 2).mean() for t in d)).backward()
+            torch.cuda.synchronize()
+            res.append(([t.detach().clone() for t in d],
+                        {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+    finally:
+        U._MERGE_BN_REDUCE = old
+        U._merge_bn_target = orig
+    assert sum(calls) >= 10, calls  # nodes 1-3 of each of the 5 stages
+    (d1, g1), (d0, g0) = res
+    for a, b in zip(d1, d0):
+        assert torch.equal(a, b)
+    # the conv weights, as test_grad_slots_match_autograd_sums: the biases in
+    # front of a training-mode BN have a gradient that is zero up to summation
+    # noise (closed form, sum of x-hat = 0), and the merge weights' gradients
+    # are stage-wide dot products of near-cancelling terms (fp32 1.2e-4; in
+    # bf16 one rounding flip of dy moves them by O(1) of their size)
+    tol = 1e-4 if dtype == 'fp32' else 5e-2
+    keys = [k for k in g0 if k.endswith('.weight') and g0[k].dim() == 4]
+    worst = max((float((g1[k] - g0[k]).norm() / g0[k].norm()), k) for k in keys)
+    print('merge-BN reduce worst rel', worst)
+    assert worst[0] < tol, worst
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
 def test_grad_slots_match_autograd_sums(dtype):
     """Fan-out input gradients accumulated into one shared buffer by the
     registered consumers (umamd.functional.GradSlots) against autograd

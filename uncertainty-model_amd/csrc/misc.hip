@@ -89,6 +89,101 @@ __global__ void merge_bwd_kernel(MergeArgs a, int nsrc, const float* __restrict_
   }
 }
 
+// merge_bwd_kernel + the BN-ELU backward statistics of source `fsrc`, whose
+// gradient this merge completes (its last consumer in the backward order,
+// umamd.functional.GraphBlockFn): the sums bn_elu_bwd_reduce would take over
+// that gradient -- sum dz and sum dz*xhat per channel, dz = da * ELU'(y*scale
+// + shift), xhat = (y - mean) * invstd, over the da as stored (T-rounded) --
+// go into the layer's f64 statistics slots here, so the reduce launch and its
+// re-read of da are skipped.  C / 8 divides the block size: every thread of
+// the grid-stride loop keeps one 8-channel group.
+template <typename T, typename TY>
+__global__ void __launch_bounds__(256) merge_bwd_bn_kernel(
+    MergeArgs a, int nsrc, const float* __restrict__ w, long n8, const T* __restrict__ dm,
+    float* __restrict__ parts, int fsrc, const TY* __restrict__ y, int C,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ scale, const float* __restrict__ shift, int apply_elu,
+    double* __restrict__ slots, long M) {
+  __shared__ float sred[4][64 * 8][2];
+  float coef[MAX_SRC], dot[MAX_SRC];
+  for (int i = 0; i < nsrc; ++i) {
+    coef[i] = w ? sigmoidf_(w[a.widx[i]]) : a.coef[i];
+    dot[i] = 0.f;
+  }
+  const int cg = C / 8, g = threadIdx.x % cg;
+  float mu[8], is[8], sc[8], sh[8], bs[8], bx[8];
+  load8(mean + g * 8, mu);
+  load8(invstd + g * 8, is);
+  load8(scale + g * 8, sc);
+  load8(shift + g * 8, sh);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { bs[e] = 0.f; bx[e] = 0.f; }
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8;
+       i += (long)gridDim.x * blockDim.x) {
+    float gv[8], v[8], o[8];
+    load8(dm + i * 8, gv);
+    for (int s = 0; s < nsrc; ++s) {
+      if (parts) {
+        load8(reinterpret_cast<const T*>(a.src[s]) + i * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dot[s] += gv[e] * v[e];
+      }
+      if (a.dsrc[s]) {
+        T* d = reinterpret_cast<T*>(a.dsrc[s]) + i * 8;
+        if (a.acc[s]) load8(d, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (a.acc[s] ? o[e] : 0.f) + coef[s] * gv[e];
+        store8(d, o);
+        if (s == fsrc) {
+          float r[8], yv[8];
+          load8_rounded(o, r, d);
+          load8(y + i * 8, yv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float dz = r[e];
+            if (apply_elu) {
+              const float z = yv[e] * sc[e] + sh[e];
+              dz = z > 0.f ? dz : dz * __expf(z);
+            }
+            bs[e] += dz;
+            bx[e] += dz * (yv[e] - mu[e]) * is[e];
+          }
+        }
+      }
+    }
+  }
+  if (parts) {
+    __shared__ float red[4];
+    for (int s = 0; s < nsrc; ++s) {
+      float t = wave_sum(dot[s]);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+      __syncthreads();
+      if (threadIdx.x == 0) parts[(long)blockIdx.x * nsrc + s] = red[0] + red[1] + red[2] + red[3];
+      __syncthreads();
+    }
+  }
+  // lanes of a wave with the same channel group: lane % cg
+  for (int off = cg; off < 64; off <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bs[e] += __shfl_xor(bs[e], off, 64);
+      bx[e] += __shfl_xor(bx[e], off, 64);
+    }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane < cg)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sred[wave][lane * 8 + e][0] = bs[e];
+      sred[wave][lane * 8 + e][1] = bx[e];
+    }
+  __syncthreads();
+  stat_slots_count(slots, C, M);
+  stat_slots_add_row(slots, blockIdx.x, C, 0, C, [&](int k) {
+    const int c = k >> 1, j = k & 1;
+    return sred[0][c][j] + sred[1][c][j] + sred[2][c][j] + sred[3][c][j];
+  });
+}
+
 __global__ void merge_wgrad_kernel(const float* __restrict__ parts, int nparts, int nsrc,
                                    MergeArgs a, const float* __restrict__ w, float* dw,
                                    int nw, int accumulate) {
@@ -279,6 +374,38 @@ int um_merge_bwd(int dtype, int nsrc, const void* const* srcs, void* const* dsrc
   else
     hipLaunchKernelGGL(merge_bwd_kernel<float>, dim3(grid_for(n8)), dim3(256), 0, st, a, nsrc, w,
                        n8, (const float*)dm, parts);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+int um_merge_bwd_bn(int dtype, int nsrc, const void* const* srcs, void* const* dsrcs,
+                    const int* accumulate, const int* widx, const float* w, const float* coefs,
+                    long count, const void* dm, float* parts, int fsrc, const void* y, int C,
+                    const float* mean, const float* invstd, const float* scale,
+                    const float* shift, int apply_elu, double* slots, hipStream_t st) {
+  UM_CHECK_ARG(nsrc >= 1 && nsrc <= MAX_SRC && fsrc >= 0 && fsrc < nsrc, "um_merge_bwd_bn: nsrc %d fsrc %d",
+               nsrc, fsrc);
+  UM_CHECK_ARG(C >= 8 && C <= 512 && C % 8 == 0 && 256 % (C / 8) == 0 && count % C == 0,
+               "um_merge_bwd_bn: C %d (C/8 must divide 256)", C);
+  UM_CHECK_ARG(dsrcs[fsrc] != nullptr && y != nullptr && slots != nullptr, "um_merge_bwd_bn: operands");
+  MergeArgs a{};
+  for (int i = 0; i < nsrc; ++i) {
+    a.src[i] = srcs ? srcs[i] : nullptr;
+    a.dsrc[i] = dsrcs[i];
+    a.acc[i] = accumulate[i];
+    a.widx[i] = widx ? widx[i] : 0;
+    a.coef[i] = coefs ? coefs[i] : 1.f;
+  }
+  const long n8 = count / 8, M = count / C;
+#define UM_MBB(T_, TY_)                                                                           \
+  hipLaunchKernelGGL((merge_bwd_bn_kernel<T_, TY_>), dim3(grid_for(n8)), dim3(256), 0, st, a, nsrc, w, \
+                     n8, (const T_*)dm, parts, fsrc, (const TY_*)y, C, mean, invstd, scale, shift,   \
+                     apply_elu, slots, M)
+  if (dtype == (UM_BF16 | UM_Y_ACT)) UM_MBB(bf16_t, bf16_t);
+  else if (dtype == (UM_BF16 | UM_Y_F16)) UM_MBB(bf16_t, f16_t);
+  else if (dtype == UM_BF16) UM_MBB(bf16_t, float);
+  else UM_MBB(float, float);
+#undef UM_MBB
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

@@ -602,7 +602,7 @@ class ConvSpec:
 class _CBEState:
     """What a conv+BN+ELU forward keeps for its backward (the autograd ctx
     of ConvBNELUFn, or one node of a GraphBlockFn)."""
-    __slots__ = ('spec', 'sync', 'slots_b', 'has_bn', 'geom', 'se', 'saved', 'merged')
+    __slots__ = ('spec', 'sync', 'slots_b', 'has_bn', 'geom', 'se', 'saved', 'merged', 'prereduced')
 
 
 def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, yconv=None):
@@ -614,6 +614,7 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
     (it returns the f32 pre-BN output; the state then saves no packed
     weights: its backward brings its own conv part, see skip_conv_bn_elu)."""
     ctx = _CBEState()
+    ctx.prereduced = False  # GraphBlockFn: the merge backward took the BN-backward sums
     L.require_device(x)
     N, H, W, Cp = x.shape
     K, Creal, R, _ = weight.shape
@@ -771,9 +772,10 @@ def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=
         if gamma is not None:
             dgamma = torch.empty(K, dtype=torch.float32, device=dev)
             dbeta = torch.empty(K, dtype=torch.float32, device=dev)
-        call('um_bn_elu_bwd_reduce_slots', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K,
-             ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
-             ptr(slots_b))
+        if not ctx.prereduced:  # else um_merge_bwd_bn summed them (GraphBlockFn)
+            call('um_bn_elu_bwd_reduce_slots', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K,
+                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
+                 ptr(slots_b))
         local, bcount, bscale = None, float(M), 1.0
         if ctx.sync is not None and ctx.sync.collective:
             # k1..k3 from the global sums.  dgamma/dbeta and the conv-bias
@@ -1138,6 +1140,14 @@ class GraphSpec:
         for s, preds in enumerate(self.nodes):
             if len(preds) > 1 and len(preds) <= 8 and max(preds) < s:
                 self.merge_after.setdefault(max(preds), s)
+        # node p -> its lowest-id successor: in the reverse-id backward that
+        # successor's input gradient is the last one added to p's, so a merge
+        # backward there completes p's gradient (um_merge_bwd_bn)
+        self.last_consumer = {}
+        for s, preds in enumerate(self.nodes):
+            for p in preds:
+                if p not in self.last_consumer or s < self.last_consumer[p]:
+                    self.last_consumer[p] = s
 
 
 def _merge_launch(srcs, w, widx, coefs, out):
@@ -1248,9 +1258,22 @@ class GraphBlockFn(torch.autograd.Function):
                 parts = torch.empty((nparts, k), dtype=torch.float32, device=dm.device) \
                     if need_w else None
                 idx = (ctypes_i * k)(*gs.widx[j])
-                call('um_merge_bwd', _dt(dm), k, (ctypes_p * k)(*[a[p].data_ptr() for p in preds]),
-                     (ctypes_p * k)(*[da[p].data_ptr() for p in preds]), (ctypes_i * k)(*acc), idx,
-                     ptr(mw), None, dm.numel(), ptr(dm), ptr(parts))
+                srcs = (ctypes_p * k)(*[a[p].data_ptr() for p in preds])
+                dsrcs = (ctypes_p * k)(*[da[p].data_ptr() for p in preds])
+                fs = _merge_bn_target(gs, j, preds, states, a)
+                if fs is not None:
+                    # this merge completes pred fs's gradient: take its BN-backward
+                    # sums here (its reduce launch and re-read of da are skipped)
+                    sp = states[preds[fs]]
+                    y_p, mean_p, invstd_p, scale_p, shift_p = sp.saved[2:7]
+                    call('um_merge_bwd_bn', _ydt(a[preds[fs]], y_p), k, srcs, dsrcs,
+                         (ctypes_i * k)(*acc), idx, ptr(mw), None, dm.numel(), ptr(dm),
+                         ptr(parts), fs, ptr(y_p), y_p.shape[-1], ptr(mean_p), ptr(invstd_p),
+                         ptr(scale_p), ptr(shift_p), int(sp.spec.elu), ptr(sp.slots_b))
+                    sp.prereduced = True
+                else:
+                    call('um_merge_bwd', _dt(dm), k, srcs, dsrcs, (ctypes_i * k)(*acc), idx,
+                         ptr(mw), None, dm.numel(), ptr(dm), ptr(parts))
                 if need_w:
                     dmw = torch.empty(mw.shape, dtype=torch.float32, device=dm.device)
                     if _MWG_BATCH and _overlap.active() is not None and k <= L.MWG_SRC:
@@ -1273,6 +1296,32 @@ class GraphBlockFn(torch.autograd.Function):
         ctx.a = ctx.states = None
         grads = [gr if p is not None else None for gr, p in zip(grads, gs.params)]
         return (None, _give(ctx, 0, dx_stage), *grads)
+
+
+# a GraphBlock node's BN-backward statistics taken by the merge backward that
+# completes its gradient (um_merge_bwd_bn); UMAMD_MERGE_BN_REDUCE=0 keeps the
+# separate reduce launch
+_MERGE_BN_REDUCE = os.environ.get('UMAMD_MERGE_BN_REDUCE', '1') == '1'
+
+
+def _merge_bn_target(gs, j, preds, states, a):
+    """index (into preds) of the predecessor whose gradient node j's merge
+    backward completes and whose BN backward can take its sums there, or None"""
+    if not _MERGE_BN_REDUCE:
+        return None
+    for q, p in enumerate(preds):
+        if gs.last_consumer.get(p) != j or p in gs.out_nodes:
+            continue
+        st = states[p]
+        if st is None or not st.has_bn or st.slots_b is None or st.se is not None:
+            continue
+        if st.sync is not None and st.sync.collective:
+            continue
+        C = a[p].shape[-1]
+        if st.saved[2].shape[-1] != C or C % 8 or C > 512 or 256 % (C // 8):
+            continue
+        return q
+    return None
 
 
 def graph_block(x, block):
