@@ -367,6 +367,8 @@ int um_merge_bwd(int dtype, int nsrc, const void* const* srcs, void* const* dsrc
  * reference model/layers/encoder.py:115-124 (merge) + 42-44 (BN+ELU).
  * dtype: activation dtype | UM_Y_ACT / UM_Y_F16 (the pre-BN y's type);
  * C / 8 must divide 256 */
+/* partial rows of um_merge_bwd_bn's merge-weight dot products (its grid) */
+int um_merge_bn_parts(long count);
 int um_merge_bwd_bn(int dtype, int nsrc, const void* const* srcs, void* const* dsrcs,
                     const int* accumulate, const int* widx, const float* w, const float* coefs,
                     long count, const void* dm, float* parts, int fsrc, const void* y, int C,

@@ -22,6 +22,16 @@ struct MergeArgs {
   float coef[MAX_SRC];  // used when w == null (constant coefficients)
 };
 
+// merge_bwd_bn: at most 512 workgroups (each adds 2*C f64 statistics to one
+// of 16 slot rows: 4096 workgroups of the 256x512 stage meant 256 adders per
+// address), the grid-stride loop covers the rest
+inline int merge_bn_grid(long n8) {
+  long b = (n8 + 255) / 256;
+  if (b > 512) b = 512;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
 inline int grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -353,6 +363,7 @@ int um_merge_fwd(int dtype, int nsrc, const void* const* srcs, const int* widx,
 }
 
 int um_merge_parts(long count) { return grid_for(count / 8); }
+int um_merge_bn_parts(long count) { return merge_bn_grid(count / 8); }
 
 int um_merge_bwd(int dtype, int nsrc, const void* const* srcs, void* const* dsrcs,
                  const int* accumulate, const int* widx, const float* w, const float* coefs,
@@ -398,7 +409,7 @@ int um_merge_bwd_bn(int dtype, int nsrc, const void* const* srcs, void* const* d
   }
   const long n8 = count / 8, M = count / C;
 #define UM_MBB(T_, TY_)                                                                           \
-  hipLaunchKernelGGL((merge_bwd_bn_kernel<T_, TY_>), dim3(grid_for(n8)), dim3(256), 0, st, a, nsrc, w, \
+  hipLaunchKernelGGL((merge_bwd_bn_kernel<T_, TY_>), dim3(merge_bn_grid(n8)), dim3(256), 0, st, a, nsrc, w, \
                      n8, (const T_*)dm, parts, fsrc, (const TY_*)y, C, mean, invstd, scale, shift,   \
                      apply_elu, slots, M)
   if (dtype == (UM_BF16 | UM_Y_ACT)) UM_MBB(bf16_t, bf16_t);

@@ -122,6 +122,7 @@ _SIG = {
     'um_merge_fwd': (_I, [_I, _I, _P, _P, _P, _P, _L, _P, 's']),
     'um_merge_parts': (_I, [_L]),
     'um_merge_bwd': (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _L, _P, _P, 's']),
+    'um_merge_bn_parts': (_I, [_L]),
     'um_merge_bwd_bn': (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _L, _P, _P, _I, _P, _I, _P, _P, _P,
                              _P, _I, _P, 's']),
     'um_merge_wgrad': (_I, [_P, _I, _I, _P, _P, _P, _I, _I, 's']),

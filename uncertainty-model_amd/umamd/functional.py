@@ -1254,13 +1254,13 @@ class GraphBlockFn(torch.autograd.Function):
                         da[p] = torch.empty_like(a[p])
                 mw = gs.params[o + 4]
                 need_w = ctx.needs_input_grad[2 + o + 4]
-                nparts = query('um_merge_parts', dm.numel())
+                fs = _merge_bn_target(gs, j, preds, states, a)
+                nparts = query('um_merge_parts' if fs is None else 'um_merge_bn_parts', dm.numel())
                 parts = torch.empty((nparts, k), dtype=torch.float32, device=dm.device) \
                     if need_w else None
                 idx = (ctypes_i * k)(*gs.widx[j])
                 srcs = (ctypes_p * k)(*[a[p].data_ptr() for p in preds])
                 dsrcs = (ctypes_p * k)(*[da[p].data_ptr() for p in preds])
-                fs = _merge_bn_target(gs, j, preds, states, a)
                 if fs is not None:
                     # this merge completes pred fs's gradient: take its BN-backward
                     # sums here (its reduce launch and re-read of da are skipped)
