@@ -136,3 +136,88 @@ def test_loss_full_size_properties():
     for a, b in zip(g1, g2):
         assert torch.isfinite(a).all()
         assert _rel(2.0 * a, b) < 1e-6
+
+
+def _smooth_preds(N, H, W, seed, noisy_right=False):
+    """disparities that vary by well under a pixel of shift between
+    neighbours (the row-owned scatter's increasing-tap path); with
+    noisy_right the right half of every row is per-pixel noise (the atomic
+    fallback path) in the same launch"""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for i in range(4):
+        h, w = H >> i, W >> i
+        yy = torch.linspace(0, 1, h).view(1, 1, h, 1)
+        xx = torch.linspace(0, 1, w).view(1, 1, 1, w)
+        base = 0.05 + 0.1 * torch.rand(N, 4, 1, 1, generator=g)
+        p = base + 0.02 * torch.sin(6.0 * xx + 3.0 * yy + torch.rand(N, 4, 1, 1, generator=g))
+        if noisy_right:
+            p = p.expand(N, 4, h, w).clone()
+            p[..., w // 2:] = 0.02 + 0.2 * torch.rand(N, 4, h, w - w // 2, generator=g)
+        out.append(p.expand(N, 4, h, w).contiguous())
+    return out
+
+
+def _loss_grads(imgs, preds, cfg):
+    import train.utils as u
+    from train.loss import TukraUncertaintyLoss
+    from umamd import lossfn as LF
+    lf = TukraUncertaintyLoss(**cfg)
+    pyr = u.scale_pyramid(imgs.to(DEV), 4)
+    pd = [p.to(DEV).requires_grad_(True) for p in preds]
+    with LF.deferred_recon():
+        rec = u.reconstruct_pyramid(pd, pyr)
+    dl, el = lf(pyr, pd, rec, 0, None)
+    (dl + 0.5 * el).backward()
+    return dl, el, [p.grad.detach().clone() for p in pd]
+
+
+@pytest.mark.parametrize('shape', [(2, 64, 128), (1, 40, 72), (2, 32, 200)])
+@pytest.mark.parametrize('noisy_right', [False, True])
+def test_row_scatter_vs_oracle(shape, noisy_right):
+    """loss backward with the row-owned consistency scatter (increasing taps:
+    plain read-modify-writes; otherwise the atomic fallback) against the f64
+    oracle, ragged widths (72, 200: a partial 64-source step per row)"""
+    from umamd._lib import lib
+    N, H, W = shape
+    g = torch.Generator().manual_seed(11)
+    imgs = torch.rand(N, 6, H, W, generator=g)
+    preds = _smooth_preds(N, H, W, 12, noisy_right)
+    cfg = _cfg()
+    old = lib().um_set_tuning(b'loss_scatter', 1)
+    try:
+        dl, el, gr = _loss_grads(imgs, preds, cfg)
+    finally:
+        lib().um_set_tuning(b'loss_scatter', old)
+    pyr_c = OL.scale_pyramid(imgs.double(), 4)
+    pc = [p.double().requires_grad_(True) for p in preds]
+    rc = OL.reconstruct_pyramid(pc, pyr_c)
+    dlc, elc, _ = OL.total_loss(pyr_c, pc, rc, dict(cfg))
+    assert abs(float(dl) / float(dlc) - 1) < 1e-4
+    assert abs(float(el) / float(elc) - 1) < 1e-4
+    (dlc + 0.5 * elc).backward()
+    for i in range(4):
+        ref = pc[i].grad
+        err = float((gr[i].double().cpu() - ref).norm() / ref.norm())
+        assert err < 4e-3, (i, err)  # warp cell flips (SURVEY F9)
+
+
+@pytest.mark.parametrize('noisy_right', [False, True])
+def test_row_scatter_matches_atomic_scatter_full_size(noisy_right):
+    """BASELINE config-2 shape: the row-owned scatter and the LDS-atomic
+    strip kernel give the same gradients up to the summation order"""
+    from umamd._lib import lib
+    g = torch.Generator().manual_seed(21)
+    imgs = torch.rand(8, 6, 256, 512, generator=g)
+    preds = _smooth_preds(8, 256, 512, 22, noisy_right)
+    cfg = _cfg()
+    res = {}
+    for mode in (0, 1):
+        old = lib().um_set_tuning(b'loss_scatter', mode)
+        try:
+            res[mode] = _loss_grads(imgs, preds, cfg)
+        finally:
+            lib().um_set_tuning(b'loss_scatter', old)
+    assert float(res[0][0]) == float(res[1][0]) and float(res[0][1]) == float(res[1][1])
+    for a, b in zip(res[0][2], res[1][2]):
+        assert _rel(b, a) < 1e-5

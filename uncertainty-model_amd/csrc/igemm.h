@@ -105,6 +105,9 @@ int igemm_halo_grid();
 int igemm_halo_res_kb();
 // reflect fold of the split-form data gradient as a VALU pass ("border_valu")
 int igemm_border_valu();
+// loss backward consistency scatter: 1 row-owned waves, 0 LDS-atomic strips
+// (knob "loss_scatter", UMAMD_LOSS_SCATTER; loss.hip)
+int knob_loss_scatter();
 
 // fill the border-list fields of a (oh, ow, fold_pad set) and return the
 // number of listed pixels per image

@@ -890,6 +890,7 @@ struct Knobs {
   int halo_pf2;
   int halo_persist, halo_grid, halo_res_kb;
   int border_valu;
+  int loss_scatter;
   Knobs() {
     auto env = [](const char* n, int d) {
       const char* v = getenv(n);
@@ -959,6 +960,10 @@ struct Knobs {
     // reflect fold of the split-form data gradient: a VALU pass over the
     // border list (conv.hip reflect_border_kernel) instead of the GEMM
     border_valu = env("UMAMD_BORDER_VALU", 1);
+    // consistency-gradient scatter of the loss backward: 1/2/4 row-owned waves
+    // without LDS atomics (steps per iteration), 0 the atomic strip kernel
+    // (loss.hip; the row form is within noise at the step level)
+    loss_scatter = env("UMAMD_LOSS_SCATTER", 0);
   }
 };
 Knobs& knobs() {
@@ -1135,6 +1140,7 @@ int igemm_halo_persist() { return knobs().halo_persist; }
 int igemm_halo_grid() { return knobs().halo_grid; }
 int igemm_halo_res_kb() { return knobs().halo_res_kb; }
 int igemm_border_valu() { return knobs().border_valu; }
+int knob_loss_scatter() { return knobs().loss_scatter; }
 
 int igemm_border_list(IgArgs& a) {
   const int H = a.oh, W = a.ow, p = a.fold_pad;
@@ -1262,6 +1268,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "halo_grid")) f = &k.halo_grid;
   else if (!strcmp(key, "halo_res_kb")) f = &k.halo_res_kb;
   else if (!strcmp(key, "border_valu")) f = &k.border_valu;
+  else if (!strcmp(key, "loss_scatter")) f = &k.loss_scatter;
   if (!f) return -1;
   const int old = *f;
   *f = value;
