@@ -377,6 +377,27 @@ def _cpu_step_rate(cfg, H, W, batch, steps, seed=1234):
     return batch / best, best, (r0['disp_loss'], r0['error_loss'])
 
 
+def physical_cores():
+    """(physical cores among the CPUs this process may run on, physical
+    cores of the machine) from /sys topology: (package, core) pairs; (0, 0)
+    when the topology is not readable."""
+    def core_of(c):
+        base = f'/sys/devices/system/cpu/cpu{c}/topology/'
+        with open(base + 'physical_package_id') as f:
+            pkg = f.read().strip()
+        with open(base + 'core_id') as f:
+            return pkg, f.read().strip()
+    try:
+        allowed = os.sched_getaffinity(0)
+        online = [int(d[3:]) for d in os.listdir('/sys/devices/system/cpu')
+                  if d.startswith('cpu') and d[3:].isdigit()]
+        host = {core_of(c) for c in online}
+        mine = {core_of(c) for c in allowed}
+        return len(mine), len(host)
+    except (OSError, ValueError):
+        return 0, 0
+
+
 def cpu_baseline(config, steps):
     """The oracle's CPU train step (plain-PyTorch restatement of the
     reference, pinned to its goldens) on the host cores, BASELINE.md
@@ -405,10 +426,14 @@ def cpu_baseline(config, steps):
                     break
     except OSError:
         pass
-    # cores = the threads actually used (torch intra-op threads); the
-    # machine's CPU count is reported beside it (a job's share is smaller)
-    return {'value': round(c2, 3), 'unit': 'stereo-pairs/sec', 'cores': threads,
-            'threads': threads, 'host_cpu_count': ncpu, 'kind': 'port',
+    # cores = physical cores the timed run used: its intra-op threads, capped
+    # by the physical cores of the CPUs this process may run on (SMT
+    # siblings count once); the machine's totals are reported beside it
+    phys, host_phys = physical_cores()
+    return {'value': round(c2, 3), 'unit': 'stereo-pairs/sec',
+            'cores': min(threads, phys) if phys else threads,
+            'threads': threads, 'host_cpu_count': ncpu, 'affinity_physical_cores': phys,
+            'host_physical_cores': host_phys, 'kind': 'port',
             'sample': f'oracle fp32 train step, C2 B=8 256x512 bayesian, 1 warm-up + best of '
                       f'{steps} ({t2:.2f} s/step) at the best thread count of a C1 sweep; {cpu}',
             'c1_thread_sweep_pairs_per_s': sweep}, ref0

@@ -31,15 +31,12 @@ extern "C" {
 #endif
 
 enum { UM_OK = 0, UM_ERR_ARG = 1, UM_ERR_HIP = 2 };
-enum { UM_F32 = 0, UM_BF16 = 1, UM_F16 = 2 /* pre-BN y storage only (UM_Y_F16) */ };
+enum { UM_F32 = 0, UM_BF16 = 1 };
 /* OR'ed into the dtype of the um_bn_elu_* entries (and um_conv2d_fwd_up2's): the pre-BN conv output y is stored in the activation
  * dtype instead of f32 (the bf16 build's default, as a bf16 autocast conv
  * feeding BatchNorm2d; statistics are still taken in f32 in the conv
  * epilogue).  um_conv2d_fwd_up2: y and the low-resolution map up2. */
 enum { UM_Y_ACT = 0x100 };
-/* dtype flag of the BN entries: the pre-BN y of bf16 activations is stored as
- * f16 (um_conv2d_fwd with ydtype UM_F16): 2 bytes like UM_Y_ACT's bf16, 8x finer */
-enum { UM_Y_F16 = 0x200 };
 enum { UM_PAD_ZERO = 0, UM_PAD_REFLECT = 1 };
 enum {
   UM_EPI_NONE = 0,           /* y = acc (+ bias)                               */
@@ -128,19 +125,6 @@ int um_conv_wgrad_reduce(const float* slabs, int splits, int K, int Kreal, int R
 int um_conv_wgrad_reduce_seg(const float* slabs, int splits, int K, int Kreal, int R, int C,
                              int Creal, float* dw, int accumulate, int nseg, const int* src0,
                              const int* dst0, const int* len, hipStream_t stream);
-/* Several weight gradients' slab reductions (um_conv_wgrad_reduce_seg each)
- * in ONE launch: the weight-gradient side stream reduces a whole batch of
- * queued convs at once (reference: the dW of every nn.Conv2d in
- * train/train.py:126's backward).  descs is a HOST array of n <= UM_WRED_MAX
- * entries; it is passed by value to the kernel (graph-capture safe). */
-#define UM_WRED_MAX 24
-typedef struct {
-  const float* slabs;  /* [splits][K][R][R][C] f32 */
-  float* dw;           /* [Kreal][Creal][R][R] f32 */
-  int splits, K, Kreal, R, C, Creal, accumulate;
-  int nseg, src0[4], dst0[4], len[4];
-} um_wred_desc;
-int um_conv_wgrad_reduce_batch(const um_wred_desc* descs, int n, hipStream_t stream);
 int um_pack_weight_seg(int dtype, const float* w, int K, int Creal, int R, int C, void* wf,
                        void* wT, int ldT, int nseg, const int* src0, const int* dst0,
                        const int* len, hipStream_t stream);
@@ -264,13 +248,7 @@ int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const 
                         float momentum, float* running_mean, float* running_var,
                         long long* num_batches_tracked, float* mean, float* invstd, float* scale,
                         float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
-                        float* ycen, const float* conv_bias, hipStream_t stream);
-/* ycen (optional, [C] f32, persistent per layer): the bf16 pre-BN output is
- * stored centred.  The conv ran with bias = ycen instead of conv_bias, so y
- * holds y_true - conv_bias + ycen; mean/invstd/scale/shift describe that y
- * (the BN output is unchanged), the running mean gets the true mean, and
- * ycen is updated to minus this step's conv-only mean for the next step.
- * Null: y is the conv's output with its own bias. */
+                        hipStream_t stream);
 /* um_bn_elu_fwd_slots plus the NodeBlock merge of the next graph node
  * (reference model/layers/encoder.py:115-124): merged = sum_i
  * sigmoid(w[widx[i]]) * src_i over nsrc (2..8) sources [M][lda] of the
@@ -283,8 +261,7 @@ int um_bn_elu_fwd_slots_merge(int dtype, long M, int C, const void* y, int ldy,
                               float* running_var, long long* num_batches_tracked, float* mean,
                               float* invstd, float* scale, float* shift, void* a, int lda,
                               int apply_elu, int nsrc, const void* const* srcs, const int* widx,
-                              const float* w, int self, void* merged, float* ycen,
-                              const float* conv_bias, hipStream_t stream);
+                              const float* w, int self, void* merged, hipStream_t stream);
 /* backward sums (sum dz, sum dz*xhat) added into zeroed f64 slots
  * [UM_STAT_SLOTS][C][2] instead of partial rows */
 int um_bn_elu_bwd_reduce_slots(int dtype, long M, int C, long HW, const void* da, int ldda,
@@ -313,17 +290,6 @@ int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int 
 /* dbias as in um_bn_bwd_stats_coeffs from the all-reduced sums, times
  * dbias_scale (SyncBN: 1/world, so that the data-parallel gradient average
  * over ranks gives the global sum's average, as the reference's DDP does) */
-/* single-process BN backward in ONE launch: um_bn_elu_bwd_reduce whose last
- * blocks (two-level ticket tree, f64) finish k1..k3, dgamma, dbeta and the
- * closed-form conv-bias gradient (as um_bn_bwd_stats_coeffs); fin_ws:
- * um_bn_bwd_fin_ws(M, C) bytes */
-long um_bn_bwd_fin_ws(long M, int C);
-int um_bn_elu_bwd_reduce_coeffs(int dtype, long M, int C, long HW, const void* da, int ldda,
-                                const void* y, int ldy, const float* mean, const float* invstd,
-                                const float* scale, const float* shift, const float* add_nc,
-                                int apply_elu, float* parts, double* fin_ws, const float* gamma,
-                                float* dgamma, float* dbeta, float* dbias, float* k1, float* k2,
-                                float* k3, hipStream_t stream);
 int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamma,
                      const float* invstd, const double* stats_local, float* dgamma,
                      float* dbeta, float* dbias, float dbias_scale, int accumulate, float* k1,
@@ -365,7 +331,7 @@ int um_merge_bwd(int dtype, int nsrc, const void* const* srcs, void* const* dsrc
  * whose gradient dsrcs[fsrc] it completes (the same sums as
  * um_bn_elu_bwd_reduce_slots over that gradient as stored, into `slots`):
  * reference model/layers/encoder.py:115-124 (merge) + 42-44 (BN+ELU).
- * dtype: activation dtype | UM_Y_ACT / UM_Y_F16 (the pre-BN y's type);
+ * dtype: activation dtype | UM_Y_ACT (the pre-BN y's type);
  * C / 8 must divide 256 */
 /* partial rows of um_merge_bwd_bn's merge-weight dot products (its grid) */
 int um_merge_bn_parts(long count);
@@ -389,23 +355,6 @@ int um_sigmoid_scale_bwd(int dtype, long M, int C, const float* d, int ldd, cons
  * channels [2K, ldo) zeroed. */
 int um_head_split_fin(long M, int K, const float* z, int ldz, const float* bias, float scale,
                       float* d, int ldd, hipStream_t stream);
-/* The 4-output heads as VALU kernels (csrc/head.hip; reference
- * model/layers/decoder.py:244-247): 3x3 conv with ReflectionPad2d(1), f32
- * weights in the reference layout w [4][Creal][3][3], f32 accumulation.
- * um_head_fwd: d [N*H*W][4] f32 = scale * sigmoid(conv(x) + bias), x NHWC
- * [N][H][W] with ldx >= Cp, Cp % 32 == 0 (zero-padded channels beyond Creal).
- * um_head_dgrad: dx[m][c] (+)= sum over the reflect-padded 3x3 transpose of
- * dl [N*H*W][ldl] (channels 0..3 = d(loss)/d(logit)) with w; dtype of x / dx
- * and dl. */
-int um_head_fwd(int dtype, int N, int H, int W, int Creal, int Cp, int ldx, const void* x,
-                const float* w, const float* bias, float scale, float* d, hipStream_t stream);
-int um_head_dgrad(int dtype, int N, int H, int W, int Creal, int Cp, const void* dl, int ldl,
-                  const float* w, void* dx, int ldx, int accumulate, hipStream_t stream);
-/* weight and bias gradient of the head: dw [4][Creal][3][3] += sum_q dl[q][k]
- * x[reflect(q + t)][c], db[4] += sum_q dl[q][k] (db nullable); dw / db must be
- * zeroed by the caller (f32 atomics, one per value and workgroup). */
-int um_head_wgrad(int dtype, int N, int H, int W, int Creal, int ldx, const void* x,
-                  const void* dl, int ldl, float* dw, float* db, hipStream_t stream);
 int um_sigmoid_scale_bwd_split(int dtype, long M, int C, const float* d, int ldd, const float* dd,
                                int lddd, float scale, void* dlogit, int ldo, hipStream_t stream);
 

@@ -4,6 +4,9 @@ tests/test_ddp_cpu.py and tests/test_gpu_ddp.py; not collected by pytest).
 mode 'cpu'    : gloo, CPU only -- host logic of the DP wrapper: SyncBN
                 conversion, BNSync world detection, f64 stats all-reduce, DDP
                 construction and gradient averaging hooks on plain tensors.
+mode 'order'  : gloo, CPU -- the captured step's collective order (SyncBN +
+                gradient buckets through one ordered communicator) recorded
+                on every rank (umamd.rccl).
 mode 'single' : one process, full batch on cuda:0, one train step.
 mode 'ddp'    : gloo ranks sharing cuda:0, each on its batch shard, one
                 DDP+SyncBN train step (SURVEY 8c golden (v): SyncBN identity).
@@ -108,6 +111,106 @@ def run_cpu(rank, world, out):
                os.path.join(out, f'cpu_{rank}.pt'))
 
 
+class _RecordingComm:
+    """Stand-in for umamd.rccl.Comm on gloo/CPU: the same collective-chain
+    bookkeeping (umamd.rccl._Order, with fake streams) and a log of every
+    collective; the values go through the gloo group."""
+
+    def __init__(self, group):
+        from umamd import rccl
+        self.group = group
+        self.ranks = dist.get_process_group_ranks(group)
+        self.stream = 'launch'  # the issuing stream of the next collective
+        self.order = rccl._Order(record=lambda s: ('event', s), wait=lambda s, ev: None)
+        self.seq = []
+
+    def all_reduce(self, t, average=False):
+        self.order.before(self.stream)
+        self.seq.append((self.stream, tuple(t.shape), str(t.dtype), bool(average)))
+        dist.all_reduce(t, group=self.group)
+        if average:
+            t.mul_(1.0 / dist.get_world_size(self.group))
+
+
+def run_order(rank, world, out):
+    """The captured step's collective sequence (SyncBN statistics on the
+    launch stream, gradient buckets on the communication stream, tiny
+    buckets) recorded on both ranks: the same order everywhere, and a wait
+    on the previous collective's stream at every switch (umamd.rccl)."""
+    from umamd import rccl
+    from umamd.functional import BNSync
+    from umamd.gradsync import GradBuckets
+    rec = _RecordingComm(dist.group.WORLD)
+    bn = torch.nn.SyncBatchNorm(4)
+    sync = BNSync(bn)
+    assert sync.collective
+
+    class SyncLayer(torch.autograd.Function):
+        """a SyncBN-like layer: all-reduce in forward and in backward"""
+        @staticmethod
+        def forward(ctx, x, i):
+            st = torch.full((4 + i,), float(rank + 1), dtype=torch.float64)
+            sync.all_reduce(st)
+            assert torch.all(st == 3.0)
+            ctx.i = i
+            return x * 1.0
+
+        @staticmethod
+        def backward(ctx, g):
+            st = torch.full((8 + ctx.i,), float(rank + 1), dtype=torch.float64)
+            sync.all_reduce(st)
+            assert torch.all(st == 3.0)
+            return g, None
+
+    torch.manual_seed(0)
+    layers = torch.nn.ModuleList([torch.nn.Linear(8, 8) for _ in range(6)])
+    gb = GradBuckets(layers.parameters(), dist.group.WORLD, world, cap_mb=300 / 2 ** 20)
+    orig = gb._reduce
+
+    def on_comm_stream(dst):
+        prev, rec.stream = rec.stream, 'comm'
+        try:
+            orig(dst)
+        finally:
+            rec.stream = prev
+    gb._reduce = on_comm_stream
+    x = torch.ones(2, 8) * (rank + 1)
+    seqs = []
+    with rccl.use(rec):
+        for it in range(2):  # step 1 learns the layout, step 2 launches from hooks
+            rec.seq = []
+            rec.order.reset()
+            for p in layers.parameters():
+                p.grad = None
+            gb.arm()
+            h = x
+            for i, lin in enumerate(layers):
+                h = SyncLayer.apply(lin(h), i)
+            h.sum().backward()
+            gb.finish()
+            seqs.append(list(rec.seq))
+            log = list(rec.order.log)
+    # every switch of issuing stream waits on the previous one
+    prev = None
+    for i, e in enumerate(log):
+        if e[0] == 'coll':
+            if prev is not None and prev != e[1]:
+                assert log[i - 1] == ('wait', e[1], prev), (i, log[i - 1], e)
+            prev = e[1]
+    kinds = [s for s, *_ in seqs[1]]
+    assert 'comm' in kinds and kinds.count('launch') == 12, kinds
+    # the buckets launch during the backward: comm collectives between the
+    # launch-stream (SyncBN backward) ones
+    first_comm = kinds.index('comm')
+    assert 'launch' in kinds[first_comm:], kinds
+    allseq = [None] * world
+    dist.all_gather_object(allseq, seqs)
+    assert all(s == allseq[0] for s in allseq), 'collective order differs between ranks'
+    torch.save({'seq': [[list(map(str, e)) for e in s] for s in seqs],
+                'grads': [p.grad.clone() for p in layers.parameters()]},
+               os.path.join(out, f'order_{rank}.pt'))
+
+
 def run_step(mode, rank, world, out):
     from train.loss import TukraUncertaintyLoss
     from train.parallel import data_parallel, unwrap
@@ -142,10 +245,12 @@ def main():
     mode, out = sys.argv[1], sys.argv[2]
     rank = int(os.environ.get('RANK', '0'))
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    if mode in ('cpu', 'ddp', 'ddp_uneven'):
+    if mode in ('cpu', 'order', 'ddp', 'ddp_uneven'):
         dist.init_process_group('gloo', init_method='env://', rank=rank, world_size=world)
     if mode == 'cpu':
         run_cpu(rank, world, out)
+    elif mode == 'order':
+        run_order(rank, world, out)
     else:
         run_step(mode, rank, world, out)
     if dist.is_initialized():

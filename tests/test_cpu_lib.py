@@ -125,3 +125,32 @@ def test_schedules_match_oracle():
     from oracle import loss as OL
     for e in range(60):
         assert float(u.adjust_disparity(e)) == pytest.approx(OL.adjust_disparity(e))
+
+
+def test_build_stamp_is_path_independent(tmp_path):
+    """The library stamp hashes sources, headers and the flags with the
+    include directories relative to the repository: a copy of the tree at
+    another path (the GPU box's snapshot) computes the same digest, so it
+    loads the shipped libumamd.so instead of rebuilding it."""
+    import glob
+    import importlib.util
+    import shutil
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(repo, 'uncertainty-model_amd')
+    dst = tmp_path / 'elsewhere' / 'repo'
+    (dst / 'uncertainty-model_amd' / 'csrc').mkdir(parents=True)
+    (dst / 'uncertainty-model_amd' / 'umamd').mkdir(parents=True)
+    shutil.copytree(os.path.join(repo, 'include'), dst / 'include')
+    for f in glob.glob(os.path.join(pkg, 'csrc', '*')):
+        if os.path.isfile(f):
+            shutil.copy(f, dst / 'uncertainty-model_amd' / 'csrc')
+    shutil.copy(os.path.join(pkg, 'umamd', '_build.py'), dst / 'uncertainty-model_amd' / 'umamd')
+
+    def digest(path):
+        spec = importlib.util.spec_from_file_location(f'_b{abs(hash(path))}', path)
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        return m._digest()
+    here = digest(os.path.join(pkg, 'umamd', '_build.py'))
+    there = digest(str(dst / 'uncertainty-model_amd' / 'umamd' / '_build.py'))
+    assert here == there

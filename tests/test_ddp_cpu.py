@@ -72,3 +72,16 @@ def test_dp_wrapper_gloo_world2(tmp_path):
     for x in r:
         for a, b in zip(x['bucket_grads'], g3):
             assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)
+
+
+def test_collective_order_same_on_ranks_world2(tmp_path):
+    """umamd.rccl: SyncBN all-reduces (launch stream) and gradient-bucket
+    all-reduces (communication stream, one-parameter-sized buckets) go
+    through ONE communicator in one chain: identical sequence on both ranks
+    (asserted inside the workers), a wait at every stream switch, and the
+    averaged gradients of the plain backward."""
+    launch('order', 2, str(tmp_path))
+    r = [torch.load(tmp_path / f'order_{i}.pt', weights_only=True) for i in range(2)]
+    assert r[0]['seq'] == r[1]['seq']
+    for a, b in zip(r[0]['grads'], r[1]['grads']):
+        assert torch.equal(a, b)

@@ -434,3 +434,48 @@ def test_grad_slots_match_autograd_sums(dtype):
         # (merge weights: ~1e-5 true value, summation-order noise of the same size)
         assert d <= tol * float(g0[k].norm()) + g0[k].numel() ** 0.5 * atol_of(k), \
             (k, d, float(g0[k].norm()))
+
+
+def test_grad_slots_guard_unregistered_consumer(monkeypatch):
+    """GradSlots' guard: an activation with two registered (umamd) consumers
+    AND a consumer outside them (here a plain torch sum) would lose gradient
+    terms silently; the pooled tensor's gradient hook raises instead and
+    turns pooling off, and the next step (autograd's own sums) gives the
+    gradient of the reference composition."""
+    import torch.nn as nn
+    from umamd import functional as U
+    from umamd._lib import PAD_ZERO
+    monkeypatch.setattr(U.GradSlots, 'broken', False)
+    torch.manual_seed(0)
+    c1, b1 = nn.Conv2d(16, 16, 3).to(DEV), nn.BatchNorm2d(16).to(DEV)
+    c2, b2 = nn.Conv2d(16, 16, 3).to(DEV), nn.BatchNorm2d(16).to(DEV)
+    x0 = torch.randn(2, 8, 16, 16, device=DEV)
+
+    def step():
+        x = x0.clone().requires_grad_(True)
+        with U.stat_scope(U.StatArena(), DEV), U.grad_slots():
+            y1 = U.conv_bn_elu(x, c1, b1, 1, PAD_ZERO)
+            y2 = U.conv_bn_elu(x, c2, b2, 1, PAD_ZERO)  # x: two registered uses
+        loss = y1.sum() + 2 * y2.sum() + 3 * (x * x).sum()  # + an unregistered use
+        loss.backward()
+        torch.cuda.synchronize()
+        return x.grad
+
+    with pytest.raises(RuntimeError, match='GradSlots'):
+        step()
+    assert U.GradSlots.broken
+    got = step()  # pooling off: autograd sums every consumer
+    monkeypatch.setattr(U, '_GRAD_SLOTS', False)
+    ref = step()
+    assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6)
+    # and without the outside consumer the pooled path is silent and exact
+    monkeypatch.setattr(U.GradSlots, 'broken', False)
+    monkeypatch.setattr(U, '_GRAD_SLOTS', True)
+    x = x0.clone().requires_grad_(True)
+    with U.stat_scope(U.StatArena(), DEV), U.grad_slots():
+        y1 = U.conv_bn_elu(x, c1, b1, 1, PAD_ZERO)
+        y2 = U.conv_bn_elu(x, c2, b2, 1, PAD_ZERO)
+    (y1.sum() + 2 * y2.sum()).backward()
+    torch.cuda.synchronize()
+    assert not U.GradSlots.broken
+    assert x.grad is not None and torch.isfinite(x.grad).all()

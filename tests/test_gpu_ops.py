@@ -430,37 +430,6 @@ def test_wgrad(case):
     assert err < 1e-4, err
 
 
-# the side stream's batched slab reduction (one um_conv_wgrad_reduce_batch per
-# WgradStream flush) against the per-conv reduction: same slabs, same
-# summation order -> bit-identical dW, incl. a segment-mapped (concat) input
-# and more convs than one launch takes (UM_WRED_MAX)
-def test_wgrad_reduce_batch_matches_per_conv(monkeypatch):
-    from umamd import functional as U
-    from umamd import overlap
-    monkeypatch.setattr(U, '_WRED_BATCH', True)  # off by default (measured slower)
-    from umamd._lib import PAD_REFLECT, PAD_ZERO, WRED_MAX
-    g = torch.Generator().manual_seed(3)
-    cases = [(32, 32, 7, 1, PAD_ZERO, 12, 64, None), (64, 128, 3, 1, PAD_REFLECT, 6, 32, None),
-             (256, 512, 3, 1, PAD_ZERO, 4, 8, None), (32, 96, 1, 1, PAD_ZERO, 12, 40, None),
-             (24, 32, 3, 1, PAD_REFLECT, 8, 32, [(0, 0, 5), (5, 8, 11)])]
-    cases = (cases * ((WRED_MAX + 8) // len(cases) + 1))[:WRED_MAX + 6]
-    ins, refs = [], []
-    for C, K, R, st, pm, H, W, segs in cases:
-        N, pad = 2, (R - 1) // 2
-        x = (torch.rand(N, H, W, C, generator=g) - 0.5).to(torch.bfloat16).to(DEV)
-        dy = torch.randn(N, H, W, K, generator=g).to(torch.bfloat16).to(DEV)
-        creal = 16 if segs else C
-        ins.append((x, dy, K, creal, R, st, pad, pm, segs))
-        refs.append(U._conv_wgrad(x, dy, K, K, creal, R, st, pad, pm, segs=segs))
-    grads = [torch.empty_like(r) for r in refs]
-    with overlap.WgradStream(batch=len(cases)):
-        for (x, dy, K, creal, R, st, pad, pm, segs), dw in zip(ins, grads):
-            U._conv_wgrad(x, dy, K, K, creal, R, st, pad, pm, dw=dw, segs=segs)
-    torch.cuda.synchronize()
-    for r, got in zip(refs, grads):
-        assert torch.equal(r, got)
-
-
 # slab reduction of the large 3x3..7x7 weights (>= 256K elements: the LDS-
 # transposed kernel with contiguous dW stores) against torch, with padded
 # K / C, a segment map (concat input) and accumulate
@@ -787,12 +756,9 @@ def test_dgrad_stride2_classes(case, cls4):
 
 
 @pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 16), (256, 4, 8), (96, 3, 5)])
-@pytest.mark.parametrize('path', ['valu', 'split'])
-def test_disp_head_split(C, H, W, path, monkeypatch):
-    """The bf16 disparity/uncertainty head, either as the VALU kernels
-    (csrc/head.hip: f32 weights, um_head_fwd / um_head_dgrad, the reflect
-    transpose incl. 3-pixel edges) or as the GEMM with split-bf16 weights
-    (um_pack_weight_split: hi + lo rows in the padding columns of the
+def test_disp_head_split(C, H, W, monkeypatch):
+    """The bf16 disparity/uncertainty head as the GEMM with split-bf16
+    weights (um_pack_weight_split: hi + lo rows in the padding columns of the
     4-output GEMM), against an f64 reference with the UNROUNDED f32 weights:
     the forward is f32-accurate (the plain bf16 GEMM head is off by the
     weight rounding), and the backward sees the f32 weight."""
@@ -815,8 +781,7 @@ def test_disp_head_split(C, H, W, path, monkeypatch):
         return d.detach(), xr.grad, wr.grad
 
     def run(split):
-        monkeypatch.setattr(U, '_SPLIT_HEAD', split and path == 'split')
-        monkeypatch.setattr(U, '_VALU_HEAD', split and path == 'valu')
+        monkeypatch.setattr(U, '_SPLIT_HEAD', split)
         xd = _nhwc(x).to(torch.bfloat16)
         Cp = (C + 7) // 8 * 8
         if Cp != C:
@@ -840,24 +805,19 @@ def test_disp_head_split(C, H, W, path, monkeypatch):
 
 
 @pytest.mark.parametrize('case', [CONV_CASES[1], CONV_CASES[3], CONV_CASES[7], CONV_CASES[4]])
-@pytest.mark.parametrize('ymode', ['f16', 'bf16'])
-def test_conv_bn_elu_y16_centred(case, ymode, monkeypatch):
-    """bf16 activations with the pre-BN y stored in 16 bits (UM_Y_F16 /
-    UM_Y_ACT) and centred by the layer's ycen buffer: two training steps on
-    the same input (the second conv runs with ycen = -(conv-only mean of the
-    first), um_bn_elu_fwd_slots): outputs, gradients and the running
-    statistics after both updates (true means, not the centred ones) against
-    the fp32 CPU reference."""
+def test_conv_bn_elu_ybf16(case, monkeypatch):
+    """bf16 activations with the pre-BN y stored in bf16 (UM_Y_ACT, the
+    UMAMD_Y_ACT=1 build): two training steps on the same input, outputs,
+    gradients and the running statistics after both updates against the
+    fp32 CPU reference."""
     from umamd import functional as U
     from umamd._lib import PAD_REFLECT, PAD_ZERO
-    monkeypatch.setattr(U, '_Y_F16', ymode == 'f16')
-    monkeypatch.setattr(U, '_Y_ACT', ymode == 'bf16')
-    monkeypatch.setattr(U, '_Y_CENTER', True)
+    monkeypatch.setattr(U, '_Y_ACT', True)
     Cin, Cout, k, stride, mode, H, W = case
     N, pad = 2, (k - 1) // 2
     conv, bn = nn.Conv2d(Cin, Cout, k, stride), nn.BatchNorm2d(Cout)
     with torch.no_grad():
-        conv.bias.uniform_(2.0, 4.0)  # a large mean: what the centring is for
+        conv.bias.uniform_(2.0, 4.0)  # a large mean: the bf16 y's worst case
         bn.weight.uniform_(0.5, 1.5)
         bn.bias.uniform_(-0.2, 0.2)
     x = torch.randn(N, Cin, H, W) + 1.0
@@ -885,6 +845,5 @@ def test_conv_bn_elu_y16_centred(case, ymode, monkeypatch):
         assert _rel(_nchw(xd.grad), xr.grad) < 2.5e-1, step
         assert _rel(cd.weight.grad, cr.weight.grad) < 2.5e-1, step
         assert _rel(bd.weight.grad, br.weight.grad) < 2.5e-1, step
-    assert getattr(bd, '_umamd_ycen', None) is not None
     assert _rel(bd.running_mean, br.running_mean) < 1e-3
     assert _rel(bd.running_var, br.running_var) < 2e-2

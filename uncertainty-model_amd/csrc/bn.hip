@@ -67,17 +67,6 @@ struct FwdFin {
   float *running_mean, *running_var;
   long long* nbt;
   float *mean, *invstd, *scale, *shift;
-  // centred pre-BN output (bf16 y): the conv ran with bias ycen instead of
-  // its own bias, so the slots hold the statistics of y' = y - bias + ycen.
-  // The BN output is the same (it is invariant to a per-channel shift of its
-  // input); mean/invstd/scale/shift are those of y' (what the backward
-  // recomputes xhat from), the running mean gets the true mean
-  // mean' - ycen + bias, and ycen becomes nb - mean' (minus the conv-only mean:
-  // the next step's y' is centred on this step's mean before its bf16
-  // rounding, which otherwise costs |mean| * 2^-9 against a batch std that is
-  // ~1/17 of the mean in smooth layers)
-  float* ycen;
-  const float* bias;
 };
 
 // s_sc / s_sh hold channels [c0, c0 + n) (this block's slice) at [c - c0]
@@ -100,12 +89,7 @@ __device__ __forceinline__ void fwd_fin_coeffs(const FwdFin& f, int C, int c0, i
       f.invstd[c] = invstd;
       f.scale[c] = sc;
       f.shift[c] = sh;
-      float tmean = (float)mean;  // the true mean of this layer's y
-      if (f.ycen != nullptr) {
-        const float nb = f.ycen[c];
-        tmean = (float)mean - nb + (f.bias ? f.bias[c] : 0.f);
-        f.ycen[c] = nb - (float)mean;
-      }
+      const float tmean = (float)mean;
       if (f.running_mean != nullptr) {
         const double unb = count > 1 ? var * count / (count - 1) : var;
         f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * tmean;
@@ -229,13 +213,10 @@ __global__ void __launch_bounds__(256) bn_elu_fwd_kernel(
 }
 
 // rows per backward block: the row-chunk sizing of common.h (about 512
-// blocks, 16..max rows) with the cap as a knob (UMAMD_BN_BWD_ROWS_MAX,
+// blocks, 16..max rows) with the cap as a tuning key (bn_bwd_rows_max,
 // default 1024 = rows_per_part)
 static int bn_bwd_rows(long M) {
-  static const int cap = [] {
-    const char* e = getenv("UMAMD_BN_BWD_ROWS_MAX");
-    return e ? atoi(e) : 1024;
-  }();
+  static const int cap = (int)umamd::tuning_env("bn_bwd_rows_max", 1024);
   const long r = (M + 511) / 512;
   int p = 16;
   while (p < r && p < cap) p <<= 1;
@@ -254,83 +235,6 @@ inline int fwd_rows(long M, long HW) {
   return (int)r;
 }
 
-// Optional in-kernel finish of the backward reduction (single-process BN):
-// the partial rows are combined by a two-level last-arriver tree -- the last
-// block of each group of FIN_GROUP rows sums them into an f64 level-2 row,
-// the last group to finish sums those and writes the coefficients -- so the
-// coefficients need no separate reduction launch.  Agent-scope release /
-// acquire around each ticket (the publish recipe of reduce.hip).
-constexpr int FIN_GROUP = 32;
-constexpr int FIN_MAX_GROUPS = 1024;
-__device__ unsigned int g_fin_t1[FIN_MAX_GROUPS];
-__device__ unsigned int g_fin_t2;
-
-struct BwdFin {
-  double* lvl2;  // [groups][C][2]; null: no finish
-  double count;
-  const float* gamma;
-  const float* invstd;
-  float *dgamma, *dbeta, *dbias, *k1, *k2, *k3;
-};
-
-// sum rows [r0, r0+n) of a [rows][W] array (float or double) into out[W]
-// (double), 256 threads: W/lanes columns x row lanes, combined in LDS
-template <typename S>
-__device__ __forceinline__ void sum_rows(const S* __restrict__ src, int r0, int n, int W,
-                                         double* __restrict__ out, double* red) {
-  const int CU = W < 256 ? W : 256;
-  const int L = 256 / CU;
-  const int u = threadIdx.x % CU, l = threadIdx.x / CU;
-  for (int w0 = 0; w0 < W; w0 += CU) {
-    const int w = w0 + u;
-    double s = 0.0;
-    if (l < L && w < W) {
-      int r = l;
-      for (; r + 3 * L < n; r += 4 * L) {
-        const double a0 = src[(long)(r0 + r) * W + w], a1 = src[(long)(r0 + r + L) * W + w];
-        const double a2 = src[(long)(r0 + r + 2 * L) * W + w];
-        const double a3 = src[(long)(r0 + r + 3 * L) * W + w];
-        s += (a0 + a1) + (a2 + a3);
-      }
-      for (; r < n; r += L) s += src[(long)(r0 + r) * W + w];
-    }
-    red[threadIdx.x] = s;
-    __syncthreads();
-    if (l == 0 && w < W) {
-      for (int q = 1; q < L; ++q) s += red[q * CU + u];
-      out[w] = s;
-    }
-    __syncthreads();
-  }
-}
-
-__device__ void bwd_finish(const float* __restrict__ parts, int nb, int C, const BwdFin& f) {
-  __shared__ double red[256];
-  __shared__ int flag;
-  const int W = 2 * C;
-  const int g = blockIdx.x / FIN_GROUP;
-  const int g0 = g * FIN_GROUP, gn = min(FIN_GROUP, nb - g0);
-  const int ng = (nb + FIN_GROUP - 1) / FIN_GROUP;
-  if (!ticket_last(&g_fin_t1[g], gn, &flag)) return;
-  sum_rows<float>(parts, g0, gn, W, f.lvl2 + (long)g * W, red);
-  if (!ticket_last(&g_fin_t2, ng, &flag)) return;
-  double* tot = f.lvl2 + (long)ng * W;  // one spare row after the groups
-  sum_rows<double>(f.lvl2, 0, ng, W, tot, red);
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const double s0 = tot[2 * c], s1 = tot[2 * c + 1];
-    const float gm = f.gamma ? f.gamma[c] : 1.f;
-    const float a1 = gm * f.invstd[c], a2 = (float)(s0 / f.count);
-    f.k1[c] = a1;
-    f.k2[c] = a2;
-    f.k3[c] = (float)(s1 / f.count);
-    if (f.dgamma) f.dgamma[c] = (float)s1;
-    if (f.dbeta) f.dbeta[c] = (float)s0;
-    // conv-bias gradient sum_m dy = k1 (s0 - n k2 - k3 sum xhat), sum xhat = 0
-    if (f.dbias) f.dbias[c] = a1 * (float)(s0 - f.count * (double)a2);
-  }
-}
-
 // Backward reduce: dz = (da + add[n][c]) * ELU'(z), z = y*scale + shift,
 // xhat = (y - mean) * invstd; partial sums per block [blk][C][2].
 template <typename T, typename TY>
@@ -339,7 +243,7 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
     long HW, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ add_nc, int apply_elu, float* __restrict__ parts,
-    int rows_per_block, BwdFin fin, double* __restrict__ slots, int cs) {
+    int rows_per_block, double* __restrict__ slots, int cs) {
   extern __shared__ float red[];  // [256][16]
   const int cb = blockIdx.y * cs;  // channel slice (see bn_elu_fwd_kernel)
   const int cg = cs / 8;
@@ -400,7 +304,6 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
       }
     }
   }
-  if (fin.lvl2 != nullptr) bwd_finish(parts, gridDim.x, C, fin);
 }
 
 __global__ void bwd_coeffs_kernel(const double* __restrict__ st, double count, int C,
@@ -578,17 +481,14 @@ int um_bn_coeffs(const double* stats, double count, int C, const float* gamma, c
 
 namespace {
 // Channel-slice plan of the three BN passes: small layers (M * C up to 8M
-// elements) with C >= 128 take 64-channel slices (UMAMD_BN_SLICE = 0 turns
+// elements) with C >= 128 take 64-channel slices (tuning key bn_slice = 0 turns
 // it off) and rows such that the grid has ~512 blocks (>= 32 rows: the 32
 // row lanes of a 64-channel block).
 struct Slices {
   int cs, ns;
 };
 Slices bn_slices(long M, int C) {
-  static const int on = [] {
-    const char* e = getenv("UMAMD_BN_SLICE");
-    return e ? atoi(e) : 1;
-  }();
+  static const int on = (int)umamd::tuning_env("bn_slice", 1);
   if (!on || C < 128 || C % 64 || M * C > (8l << 20)) return {C, 1};
   return {64, C / 64};
 }
@@ -635,16 +535,14 @@ static int bn_fwd_launch(int dtype, long M, int C, const void* y, int ldy, const
   const dim3 g(ceil_div(M, rows), sl.ns);
   const size_t shm = (pool_parts ? 256 * 8 * sizeof(float) : 0) +
                      (fin.slots ? 2 * (size_t)sl.cs * sizeof(float) : 0);
-  const bool yact = dtype & UM_Y_ACT, yf16 = dtype & UM_Y_F16;
-  dtype &= ~(UM_Y_ACT | UM_Y_F16);
+  const bool yact = dtype & UM_Y_ACT;
+  dtype &= ~UM_Y_ACT;
 #define UM_BN_FWD(T_, MG_, TY_)                                                            \
   hipLaunchKernelGGL((bn_elu_fwd_kernel<T_, MG_, TY_>), g, dim3(256), shm, st, (const TY_*)y, \
                      ldy, M, C, scale, shift, (T_*)a, lda, apply_elu, rows, pool_parts, fin,   \
                      sl.cs, mo)
   if (dtype == UM_BF16 && yact) {
     if (mo.n) UM_BN_FWD(bf16_t, true, bf16_t); else UM_BN_FWD(bf16_t, false, bf16_t);
-  } else if (dtype == UM_BF16 && yf16) {
-    if (mo.n) UM_BN_FWD(bf16_t, true, f16_t); else UM_BN_FWD(bf16_t, false, f16_t);
   } else if (dtype == UM_BF16) {
     if (mo.n) UM_BN_FWD(bf16_t, true, float); else UM_BN_FWD(bf16_t, false, float);
   } else {
@@ -667,11 +565,10 @@ int um_bn_elu_fwd_slots(int dtype, long M, int C, const void* y, int ldy, const 
                         float momentum, float* running_mean, float* running_var,
                         long long* num_batches_tracked, float* mean, float* invstd, float* scale,
                         float* shift, void* a, int lda, int apply_elu, long HW, float* pool_parts,
-                        float* ycen, const float* conv_bias, hipStream_t st) {
+                        hipStream_t st) {
   UM_CHECK_ARG(slots != nullptr && mean && invstd && scale && shift,
                "um_bn_elu_fwd_slots: slots / coefficient outputs");
   FwdFin fin{};
-  fin.ycen = ycen; fin.bias = conv_bias;
   fin.slots = slots; fin.count = count; fin.gamma = gamma; fin.beta = beta;
   fin.eps = eps; fin.momentum = momentum;
   fin.running_mean = running_mean; fin.running_var = running_var; fin.nbt = num_batches_tracked;
@@ -686,8 +583,7 @@ int um_bn_elu_fwd_slots_merge(int dtype, long M, int C, const void* y, int ldy,
                               float* running_var, long long* num_batches_tracked, float* mean,
                               float* invstd, float* scale, float* shift, void* a, int lda,
                               int apply_elu, int nsrc, const void* const* srcs, const int* widx,
-                              const float* w, int self, void* merged, float* ycen,
-                              const float* conv_bias, hipStream_t st) {
+                              const float* w, int self, void* merged, hipStream_t st) {
   UM_CHECK_ARG(slots != nullptr && mean && invstd && scale && shift,
                "um_bn_elu_fwd_slots_merge: slots / coefficient outputs");
   UM_CHECK_ARG(nsrc >= 2 && nsrc <= FMERGE_MAX && self >= 0 && self < nsrc && srcs && widx &&
@@ -698,7 +594,6 @@ int um_bn_elu_fwd_slots_merge(int dtype, long M, int C, const void* y, int ldy,
   fin.eps = eps; fin.momentum = momentum;
   fin.running_mean = running_mean; fin.running_var = running_var; fin.nbt = num_batches_tracked;
   fin.mean = mean; fin.invstd = invstd; fin.scale = scale; fin.shift = shift;
-  fin.ycen = ycen; fin.bias = conv_bias;
   MergeOut mo{};
   mo.n = nsrc;
   mo.self = self;
@@ -718,12 +613,11 @@ int um_bn_bwd_parts(long M) { return ceil_div(M, bn_bwd_rows(M)); }
 static int bwd_reduce_launch(int dtype, long M, int C, long HW, const void* da, int ldda,
                              const void* y, int ldy, const float* mean, const float* invstd,
                              const float* scale, const float* shift, const float* add_nc,
-                             int apply_elu, float* parts, const BwdFin& fin, double* slots,
+                             int apply_elu, float* parts, double* slots,
                              hipStream_t st) {
   UM_CHECK_ARG(C % 8 == 0, "um_bn_elu_bwd_reduce: C %% 8");
   // channel slices only where the statistics go to slots (the partial rows
-  // of the other paths are sized by um_bn_bwd_parts, and the fused finish
-  // counts row blocks)
+  // of the other paths are sized by um_bn_bwd_parts)
   const Slices sl = slots != nullptr ? bn_slices(M, C) : Slices{C, 1};
   const int rows = sl.ns > 1 ? bwd_rows_c(M, C) : bn_bwd_rows(M);
   const dim3 blocks(ceil_div(M, rows), sl.ns);
@@ -731,9 +625,8 @@ static int bwd_reduce_launch(int dtype, long M, int C, long HW, const void* da, 
 #define UM_BN_RED(T_, TY_)                                                                   \
   hipLaunchKernelGGL((bn_elu_bwd_reduce_kernel<T_, TY_>), blocks, dim3(256), shm, st,        \
                      (const T_*)da, ldda, (const TY_*)y, ldy, M, C, HW, mean, invstd, scale, \
-                     shift, add_nc, apply_elu, parts, rows, fin, slots, sl.cs)
+                     shift, add_nc, apply_elu, parts, rows, slots, sl.cs)
   if (dtype == (UM_BF16 | UM_Y_ACT)) UM_BN_RED(bf16_t, bf16_t);
-  else if (dtype == (UM_BF16 | UM_Y_F16)) UM_BN_RED(bf16_t, f16_t);
   else if (dtype == UM_BF16) UM_BN_RED(bf16_t, float);
   else UM_BN_RED(float, float);
 #undef UM_BN_RED
@@ -745,9 +638,8 @@ int um_bn_elu_bwd_reduce(int dtype, long M, int C, long HW, const void* da, int 
                          const void* y, int ldy, const float* mean, const float* invstd,
                          const float* scale, const float* shift, const float* add_nc,
                          int apply_elu, float* parts, hipStream_t st) {
-  BwdFin fin{};
   return bwd_reduce_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
-                           apply_elu, parts, fin, nullptr, st);
+                           apply_elu, parts, nullptr, st);
 }
 
 int um_bn_elu_bwd_reduce_slots(int dtype, long M, int C, long HW, const void* da, int ldda,
@@ -755,33 +647,8 @@ int um_bn_elu_bwd_reduce_slots(int dtype, long M, int C, long HW, const void* da
                                const float* scale, const float* shift, const float* add_nc,
                                int apply_elu, double* slots, hipStream_t st) {
   UM_CHECK_ARG(slots != nullptr, "um_bn_elu_bwd_reduce_slots: slots");
-  BwdFin fin{};
   return bwd_reduce_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
-                           apply_elu, nullptr, fin, slots, st);
-}
-
-long um_bn_bwd_fin_ws(long M, int C) {
-  const int ng = (um_bn_bwd_parts(M) + FIN_GROUP - 1) / FIN_GROUP;
-  return (long)(ng + 1) * 2 * C * sizeof(double);
-}
-
-int um_bn_elu_bwd_reduce_coeffs(int dtype, long M, int C, long HW, const void* da, int ldda,
-                                const void* y, int ldy, const float* mean, const float* invstd,
-                                const float* scale, const float* shift, const float* add_nc,
-                                int apply_elu, float* parts, double* fin_ws, const float* gamma,
-                                float* dgamma, float* dbeta, float* dbias, float* k1, float* k2,
-                                float* k3, hipStream_t st) {
-  const int ng = (um_bn_bwd_parts(M) + FIN_GROUP - 1) / FIN_GROUP;
-  UM_CHECK_ARG(fin_ws != nullptr && ng <= FIN_MAX_GROUPS, "um_bn_elu_bwd_reduce_coeffs: ws/groups");
-  BwdFin fin{};
-  fin.lvl2 = fin_ws;
-  fin.count = (double)M;
-  fin.gamma = gamma;
-  fin.invstd = invstd;
-  fin.dgamma = dgamma; fin.dbeta = dbeta; fin.dbias = dbias;
-  fin.k1 = k1; fin.k2 = k2; fin.k3 = k3;
-  return bwd_reduce_launch(dtype, M, C, HW, da, ldda, y, ldy, mean, invstd, scale, shift, add_nc,
-                           apply_elu, parts, fin, nullptr, st);
+                           apply_elu, nullptr, slots, st);
 }
 
 int um_bn_bwd_coeffs(const double* stats, double count, int C, const float* gamma,
@@ -812,7 +679,6 @@ static int bwd_apply_launch(int dtype, long M, int C, long HW, const void* da, i
                      shift, add_nc, apply_elu, k1, k2, k3, (T_*)dy, lddy, sum_parts, rows, fin, \
                      sl.cs)
   if (dtype == (UM_BF16 | UM_Y_ACT)) UM_BN_APPLY(bf16_t, bf16_t);
-  else if (dtype == (UM_BF16 | UM_Y_F16)) UM_BN_APPLY(bf16_t, f16_t);
   else if (dtype == UM_BF16) UM_BN_APPLY(bf16_t, float);
   else UM_BN_APPLY(float, float);
 #undef UM_BN_APPLY

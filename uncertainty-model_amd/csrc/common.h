@@ -16,11 +16,14 @@
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __hip_bfloat16 bf16_t;
-typedef _Float16 f16_t;  // the pre-BN conv output y when stored as f16 (UM_Y_F16)
 
 // ------------------------------------------------------------ error state --
 namespace umamd {
 void set_error(const char* fmt, ...);
+// Tuning values for sweeps: the ONE environment variable UMAMD_TUNING holds
+// "key=value,key=value" (keys as um_set_tuning's); a key not listed there
+// gives ``dflt``.  Read once per key by each caller (static initialisers).
+long tuning_env(const char* key, long dflt);
 }  // namespace umamd
 
 #define UM_CHECK_ARG(cond, ...)                    \
@@ -48,8 +51,6 @@ template <> __device__ __forceinline__ float from_f32<float>(float x) { return x
 template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float x) {
   return __float2bfloat16(x);
 }
-__device__ __forceinline__ float to_f32(f16_t x) { return (float)x; }
-template <> __device__ __forceinline__ f16_t from_f32<f16_t>(float x) { return (f16_t)x; }
 
 // 8-element vector load/store (16 B for bf16, 32 B for f32) -> f32[8]
 __device__ __forceinline__ void load8(const float* p, float* v) {
@@ -66,19 +67,6 @@ __device__ __forceinline__ void load8(const bf16_t* p, float* v) {
     v[2 * i] = __uint_as_float(w[i] << 16);
     v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
   }
-}
-__device__ __forceinline__ void load8(const f16_t* p, float* v) {
-  typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-  const f16x8 u = *reinterpret_cast<const f16x8*>(p);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = (float)u[i];
-}
-__device__ __forceinline__ void store8(f16_t* p, const float* v) {
-  typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-  f16x8 u;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) u[i] = (_Float16)v[i];
-  *reinterpret_cast<f16x8*>(p) = u;
 }
 __device__ __forceinline__ void store8(float* p, const float* v) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);

@@ -568,55 +568,6 @@ __global__ void __launch_bounds__(256) wgrad_reduce4_kernel(const float* __restr
                      gridDim.x, red);
 }
 
-// Many weight gradients' slab reductions in ONE launch (the weight-gradient
-// side stream's batch, umamd/overlap.py): descriptor d owns workgroups
-// [first[d], first[d + 1]).  The descriptors travel as kernel arguments, so
-// a captured graph keeps them by value.
-struct WredDesc {
-  const float* slabs;
-  float* dw;
-  int splits, K, Kreal, R, C, Creal, accumulate, L;
-  Segs sg;
-};
-struct WredBatch {
-  int n;
-  int first[UM_WRED_MAX + 1];
-  WredDesc d[UM_WRED_MAX];
-};
-
-__global__ void __launch_bounds__(256) wgrad_reduce_batch_kernel(WredBatch b) {
-  __shared__ float4 red[256];
-  // the descriptor field by field, by unrolled uniform selects: a runtime
-  // index into the by-value kernel argument (or a struct copy of one entry)
-  // would go through scratch
-  int i = 0;
-#pragma unroll
-  for (int j = 1; j < UM_WRED_MAX; ++j)
-    if (j < b.n && (int)blockIdx.x >= b.first[j]) i = j;
-#define WSEL(expr)                                          \
-  ({                                                        \
-    auto v_ = b.d[0].expr;                                  \
-    _Pragma("unroll") for (int j = 1; j < UM_WRED_MAX; ++j) \
-      if (j == i) v_ = b.d[j].expr;                         \
-    v_;                                                     \
-  })
-  Segs sg;
-  sg.n = WSEL(sg.n);
-#pragma unroll
-  for (int q = 0; q < MAX_SEG; ++q) {
-    sg.src0[q] = WSEL(sg.src0[q]);
-    sg.dst0[q] = WSEL(sg.dst0[q]);
-    sg.len[q] = WSEL(sg.len[q]);
-  }
-  int f0 = 0, f1 = 0;
-#pragma unroll
-  for (int j = 0; j < UM_WRED_MAX; ++j)
-    if (j == i) { f0 = b.first[j]; f1 = b.first[j + 1]; }
-  wgrad_reduce4_body(WSEL(slabs), WSEL(splits), WSEL(K), WSEL(Kreal), WSEL(R), WSEL(C), WSEL(Creal),
-                     WSEL(dw), WSEL(accumulate), sg, WSEL(L), blockIdx.x - f0, f1 - f0, red);
-#undef WSEL
-}
-
 // split-bf16 value of a packed row: rows [0, K) the weight rounded to the
 // activation type, rows [K, 2K) (split packs only) its rounding residual, so
 // that a GEMM over both row sets summed in f32 sees the f32 weight to ~2^-17
@@ -1080,10 +1031,7 @@ int um_conv2d_fwd_up2(int dtype, int N, int H, int W, int C, int ldx, const void
                "um_conv2d_fwd_up2: epilogue");
   UM_CHECK_ARG(K % 8 == 0 && ldy % 8 == 0 && up2_ld % 8 == 0 && P == H && Q == W,
                "um_conv2d_fwd_up2: K / strides must be multiples of 8, 1x1 same-size conv");
-  static const int valu = [] {
-    const char* e = getenv("UMAMD_UP2_VALU");
-    return e ? atoi(e) : 1;
-  }();
+  static const int valu = (int)umamd::tuning_env("up2_valu", 1);
   const int G = K / 8;
   if (valu && C % 8 == 0 && C <= 16 && K <= 128 && 256 % G == 0 && ldx % 8 == 0 &&
       (epilogue == UM_EPI_NONE || epilogue == UM_EPI_STAT_SLOTS)) {
@@ -1123,8 +1071,7 @@ static int conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void
   UM_CHECK_ARG((epilogue != UM_EPI_STATS && epilogue != UM_EPI_STAT_SLOTS) || stats != nullptr,
                "um_conv2d_fwd: stats buffer missing");
   UM_CHECK_ARG(epilogue != UM_EPI_RESIDUAL || residual != nullptr, "um_conv2d_fwd: residual missing");
-  UM_CHECK_ARG(ydtype == dtype || ydtype == UM_F32 || (ydtype == UM_F16 && dtype == UM_BF16),
-               "um_conv2d_fwd: ydtype must be dtype, f32, or f16 with bf16 activations");
+  UM_CHECK_ARG(ydtype == dtype || ydtype == UM_F32, "um_conv2d_fwd: ydtype must be dtype or f32");
   umamd::IgArgs a{};
   a.a = x; a.ah = H; a.aw = W; a.ach = C; a.lda = ldx;
   a.on = N; a.oh = P; a.ow = Q;
@@ -1135,7 +1082,6 @@ static int conv2d_fwd(int dtype, int N, int H, int W, int C, int ldx, const void
   a.b = wf; a.ldb = (long)R * R * C;
   a.NC = K; a.M = N * P * Q;
   a.bias = bias; a.out = y; a.ld_out = ldy; a.out_f32 = (ydtype == UM_F32);
-  a.out_f16 = (ydtype == UM_F16);
   a.epilogue = epilogue == UM_EPI_STAT_SLOTS ? UM_EPI_STATS : epilogue;
   a.stat_slots = epilogue == UM_EPI_STAT_SLOTS;
   a.accumulate = accumulate; a.epi_scale = epi_scale;
@@ -1268,11 +1214,8 @@ static int generic_wgrad_splits(int M, int K, int RRC, bool tr) {
   // tiles of the bf16 kernels (the f32 kernel uses 64x64 tiles; same split count)
   const int bm = tr ? umamd::wgrad_tr_bm(K) : wgrad_bm(K);
   const long tiles = (long)ceil_div(K, bm) * ceil_div(RRC, 128);
-  // target workgroups over the chip (UMAMD_WSPLIT_BLOCKS overrides for sweeps)
-  static const long target = [] {
-    const char* e = getenv("UMAMD_WSPLIT_BLOCKS");
-    return e ? atol(e) : 768l;
-  }();
+  // target workgroups over the chip (UMAMD_TUNING wsplit_blocks for sweeps)
+  static const long target = umamd::tuning_env("wsplit_blocks", 768);
   long splits = (target + tiles - 1) / tiles;
   const long max_by_m = (M + 255) / 256;  // >= 256 pixels per split
   if (splits > max_by_m) splits = max_by_m;
@@ -1354,10 +1297,7 @@ int um_conv_wgrad_reduce_seg(const float* slabs, int splits, int K, int Kreal, i
   UM_CHECK_ARG(make_segs(g, nseg, src0, dst0, len, Creal, C), "um_conv_wgrad_reduce: segments");
   const long total = (long)Kreal * R * R * C;
   const long RRC = (long)R * R * C;
-  static const int wred_t = [] {
-    const char* e = getenv("UMAMD_WRED_T");
-    return e ? atoi(e) : 1;
-  }();
+  static const int wred_t = (int)umamd::tuning_env("wred_t", 1);
   if (wred_t && R > 1 && total >= (1l << 18)) {
     const size_t shm = (size_t)R * R * (WRT_CW + 1) * sizeof(float);
     hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3(ceil_div(C, WRT_CW), Kreal), dim3(256), shm, st,
@@ -1392,41 +1332,6 @@ int um_conv_wgrad_reduce(const float* slabs, int splits, int K, int Kreal, int R
                          int Creal, float* dw, int accumulate, hipStream_t st) {
   return um_conv_wgrad_reduce_seg(slabs, splits, K, Kreal, R, C, Creal, dw, accumulate, 0,
                                   nullptr, nullptr, nullptr, st);
-}
-
-int um_conv_wgrad_reduce_batch(const um_wred_desc* descs, int n, hipStream_t st) {
-  UM_CHECK_ARG(descs != nullptr && n >= 0 && n <= UM_WRED_MAX, "um_conv_wgrad_reduce_batch: n");
-  if (n == 0) return UM_OK;
-  WredBatch b{};
-  b.n = n;
-  int blocks = 0;
-  for (int i = 0; i < n; ++i) {
-    const um_wred_desc& e = descs[i];
-    UM_CHECK_ARG(e.slabs != nullptr && e.dw != nullptr && e.splits >= 1 && e.Kreal <= e.K &&
-                     (e.nseg > 0 || e.Creal <= e.C),
-                 "um_conv_wgrad_reduce_batch: descriptor");
-    const long RRC = (long)e.R * e.R * e.C;
-    UM_CHECK_ARG(RRC % 4 == 0 && (long)e.splits * e.K * RRC < (1l << 33),
-                 "um_conv_wgrad_reduce_batch: slab layout (R*R*C % 4, 32-bit offsets)");
-    WredDesc& d = b.d[i];
-    d.slabs = e.slabs;
-    d.dw = e.dw;
-    d.splits = e.splits; d.K = e.K; d.Kreal = e.Kreal; d.R = e.R; d.C = e.C; d.Creal = e.Creal;
-    d.accumulate = e.accumulate;
-    UM_CHECK_ARG(make_segs(d.sg, e.nseg, e.src0, e.dst0, e.len, e.Creal, e.C),
-                 "um_conv_wgrad_reduce_batch: segments");
-    const long total4 = (long)e.Kreal * RRC / 4;
-    int L = 1;  // as um_conv_wgrad_reduce_seg
-    while (L < 32 && L * 4 <= e.splits && (total4 * L) / 256 < 2048) L <<= 1;
-    d.L = L;
-    const int EB = 256 / L;
-    b.first[i] = blocks;
-    blocks += (int)std::min<long>((total4 + EB - 1) / EB, 8192);
-  }
-  b.first[n] = blocks;
-  hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3(blocks), dim3(256), 0, st, b);
-  UM_LAUNCH_CHECK();
-  return UM_OK;
 }
 
 int um_pack_weight_seg(int dtype, const float* w, int K, int Creal, int R, int C, void* wf,

@@ -651,15 +651,12 @@ __global__ void __launch_bounds__(256) parts_accum_kernel(const float* __restric
 }
 
 
-// knob UMAMD_CAT_FUSED (default 0): all sources of a concat in one launch.
+// tuning key cat_fused (default 0): all sources of a concat in one launch.
 // Measured slower (decoder concats 514 -> 693 us per step, 716 -> 705
 // pairs/s): waves spanning several sources run every source's path, and the
 // per-source launches already write whole 16-byte lanes
 bool cat_fused() {
-  static const int v = [] {
-    const char* e = getenv("UMAMD_CAT_FUSED");
-    return e ? atoi(e) : 0;
-  }();
+  static const int v = (int)umamd::tuning_env("cat_fused", 0);
   return v != 0;
 }
 

@@ -357,10 +357,6 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
             float* o = reinterpret_cast<float*>(a.out) + off;
             if (a.accumulate) v += *o;
             *o = v;
-          } else if (a.out_f16) {
-            f16_t* o = reinterpret_cast<f16_t*>(a.out) + off;
-            if (a.accumulate) v += to_f32(*o);
-            *o = from_f32<f16_t>(v);
           } else {
             bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + off;
             if (a.accumulate) v += to_f32(*o);

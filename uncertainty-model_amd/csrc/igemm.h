@@ -36,7 +36,6 @@ struct IgArgs {
   const float* bias;
   void* out;
   int ld_out, out_f32, epilogue, accumulate;
-  int out_f16;      // y stored as f16 (UM_Y_F16; out_f32 == 0)
   float epi_scale;
   const void* residual;
   int ldr;
@@ -87,7 +86,7 @@ int igemm_run_cls4(int dtype, IgArgs (&as)[4], hipStream_t st);
 
 // reflect data gradients with more input channels than this run as one fold
 // pass, the others as a zero-pad pass + the border-list pass (knob
-// "fold_split_nc", UMAMD_FOLD_SPLIT_NC)
+// "fold_split_nc")
 int igemm_fold_split_nc();
 bool igemm_halo_dgrad(int dtype, int N, int H, int W, int C, int R);
 
@@ -95,7 +94,7 @@ bool igemm_halo_dgrad(int dtype, int N, int H, int W, int C, int R);
 // dx wider than fold_split_nc, 2 all
 int igemm_pad_dgrad();
 
-// halo conv weight rows two rows ahead (knob "halo_pf2", UMAMD_HALO_PF2)
+// halo conv weight rows two rows ahead (tuning key "halo_pf2")
 int igemm_halo_pf2();
 // halo conv grid: persistent workgroups per resident slot (knob
 // "halo_persist", 0 = one tile per workgroup) and a grid cap ("halo_grid")
@@ -105,9 +104,6 @@ int igemm_halo_grid();
 int igemm_halo_res_kb();
 // reflect fold of the split-form data gradient as a VALU pass ("border_valu")
 int igemm_border_valu();
-// loss backward consistency scatter: 1 row-owned waves, 0 LDS-atomic strips
-// (knob "loss_scatter", UMAMD_LOSS_SCATTER; loss.hip)
-int knob_loss_scatter();
 
 // fill the border-list fields of a (oh, ow, fold_pad set) and return the
 // number of listed pixels per image

@@ -236,7 +236,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
     }
     return;
   }
-  const bool stageable = sOut != nullptr && !a.out_f32 && !a.out_f16 && a.NC % 8 == 0 &&
+  const bool stageable = sOut != nullptr && !a.out_f32 && a.NC % 8 == 0 &&
                          a.ld_out % 8 == 0;
   // accumulate + statistics slots (the decoder skip conv's feature-map half
   // onto up2(z)): the statistics of the SUM are taken in the 16-byte row
@@ -269,10 +269,6 @@ __device__ __forceinline__ void igemm_epilogue(const IgArgs& a, float* __restric
           float* o = reinterpret_cast<float*>(a.out) + off;
           if (a.accumulate) v += *o;
           *o = v;
-        } else if (a.out_f16) {
-          f16_t* o = reinterpret_cast<f16_t*>(a.out) + off;
-          if (a.accumulate) v += to_f32(*o);
-          *o = from_f32<f16_t>(v);
         } else if (staged) {  // accumulate (if any) happens at the row store
           sOut[(m - bm) * BN + (n - bn)] = from_f32<T>(v);
         } else {
@@ -830,10 +826,6 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const fl
           float* o = reinterpret_cast<float*>(a.out) + off;
           if (a.accumulate) v[e] += *o;
           *o = v[e];
-        } else if (a.out_f16) {
-          f16_t* o = reinterpret_cast<f16_t*>(a.out) + off;
-          if (a.accumulate) v[e] += to_f32(*o);
-          *o = from_f32<f16_t>(v[e]);
         } else {
           T* o = reinterpret_cast<T*>(a.out) + off;
           if (a.accumulate) v[e] += to_f32(*o);
@@ -875,7 +867,8 @@ struct Plan {
   int bk, bm, bn, wm, wn, splits, steps, per;
 };
 
-// tuning knobs (read once; UMAMD_IG_* environment variables for sweeps)
+// tuning knobs (read once; defaults below, UMAMD_TUNING="key=value,..." for
+// sweeps, um_set_tuning at run time for tests)
 struct Knobs {
   int small, small_tiles, split_below, split_target, split_minsteps, halo, halo_min_tiles, odd_bn, bk64;
   int glds_split_below, glds_split_target;
@@ -890,80 +883,72 @@ struct Knobs {
   int halo_pf2;
   int halo_persist, halo_grid, halo_res_kb;
   int border_valu;
-  int loss_scatter;
   Knobs() {
-    auto env = [](const char* n, int d) {
-      const char* v = getenv(n);
-      return v ? atoi(v) : d;
-    };
-    small = env("UMAMD_IG_SMALL", 1);
+    auto env = [](const char* n, int d) { return (int)umamd::tuning_env(n, d); };
+    small = env("small", 1);
     // measured on MI355X (bench step, tools/sweep.sh): the deep layers' main
     // loops are load-latency bound (one double-buffered stage in flight per
     // block, ~1 us per k-step at 1 block per CU), so more, smaller and split
     // tiles help: 160/320/8/256 -> 600/1024/4/1024 took 578 -> 599 pairs/s
-    small_tiles = env("UMAMD_IG_SMALL_TILES", 1024);
-    split_below = env("UMAMD_IG_SPLIT_BELOW", 600);
-    split_target = env("UMAMD_IG_SPLIT_TARGET", 1024);
+    small_tiles = env("small_tiles", 1024);
+    split_below = env("split_below", 600);
+    split_target = env("split_target", 1024);
     // the 8-wave LDS-DMA loop (glds bit 2) hides more of a 64x64-tile
     // block's own latency: measured per conv (tools/ig_micro.sh), split only
     // below 256 tiles and to ~512 blocks -- 16x32x256->256 27 -> 24 us,
     // 32x64x128->128 27 -> 19 us, 8x16x512->512 28 -> 25 us.  The register
     // path (reflect-fold data gradients, f32) keeps the thresholds above.
-    glds_split_below = env("UMAMD_IG_GLDS_SPLIT_BELOW", 256);
-    glds_split_target = env("UMAMD_IG_GLDS_SPLIT_TARGET", 512);
-    split_minsteps = env("UMAMD_IG_SPLIT_MINSTEPS", 4);
-    halo = env("UMAMD_HALO", 1);
-    halo_min_tiles = env("UMAMD_HALO_MIN_TILES", 256);
+    glds_split_below = env("glds_split_below", 256);
+    glds_split_target = env("glds_split_target", 512);
+    split_minsteps = env("split_minsteps", 4);
+    halo = env("halo", 1);
+    halo_min_tiles = env("halo_min_tiles", 256);
     // widest output (columns) the halo kernel takes: 64 = one column block
     // (round 2); up to 192 adds 96/128-wide 3x3 blocks and column grids
-    halo_max_nc = env("UMAMD_HALO_MAX_NC", 192);
-    odd_bn = env("UMAMD_IG_ODD_BN", 1);
+    halo_max_nc = env("halo_max_nc", 192);
+    odd_bn = env("odd_bn", 1);
     // bit 0: 64-deep k-steps for the 64x64 tiles, bit 1: for the 128-row tiles
-    bk64 = env("UMAMD_IG_BK64", 3);
+    bk64 = env("bk64", 3);
     // bit 0: LDS-DMA main loop for the 64x64 tiles, bit 1: for the 128-row
     // tiles, bit 2: 8 waves per 64x64 tile.  Step sweep (tools/sweep.sh):
     // 0 -> 653.6, 7 -> 654.8, 5 -> 661.3 pairs/s (the 128-row tiles keep the
     // register path: 3 LDS stages of 128-row tiles leave 1 block per CU)
-    glds = env("UMAMD_IG_GLDS", 5);
+    glds = env("glds", 5);
     // 6-stage LDS-DMA loop for 8-wave 64x64 grids of at most this many
     // blocks (one 96 KB block per CU); 3 = off.  Step sweep: 3 -> 721,
     // 6 -> 715 pairs/s (unsplit deep grids 713-717): five k-steps in flight
     // do not shorten the deep layers' k-loop, so latency is not its limit
-    glds_deep = env("UMAMD_IG_GLDS_DEEP", 3);
-    glds_deep_blocks = env("UMAMD_IG_GLDS_DEEP_BLOCKS", 256);
+    glds_deep = env("glds_deep", 3);
+    glds_deep_blocks = env("glds_deep_blocks", 256);
     // column-major tile order for weight-heavy GEMMs (0 off, 1 auto, 2 on):
     // per conv and per step within noise (714 vs 713 pairs/s), off
-    xcd_col = env("UMAMD_IG_XCD_COL", 0);
+    xcd_col = env("xcd_col", 0);
     // 8-channel operands: bit 0 packs 4 taps per 32-deep k-step, bit 1 also
     // routes them past the halo kernel.  First conv (7x7 s2, C8) 93 -> 51 us;
     // step 711 -> 715-716 pairs/s with 1 or 3 (the heads' halo path is as fast)
-    tappack = env("UMAMD_IG_TAPPACK", 1);
+    tappack = env("tappack", 1);
     // the four parity classes of a stride-2 data gradient as one launch
-    cls4 = env("UMAMD_IG_CLS4", 1);
+    cls4 = env("cls4", 1);
     // reflect data gradient as a zero-pad transposed conv onto the padded
     // input + a fold pass (0 off, 1 the wide layers, 2 all)
-    pad_dgrad = env("UMAMD_IG_PAD_DGRAD", 1);
+    pad_dgrad = env("pad_dgrad", 1);
     // per conv (tools/conv_table.py): split form 256x512 C48 171 -> 117 us,
     // C32 K8 125 -> 85; one pass stays ahead from C = 128 up (16x32 C640:
     // 106 vs 140, 8x16 C512: 53 vs 79)
-    fold_split_nc = env("UMAMD_FOLD_SPLIT_NC", 64);
+    fold_split_nc = env("fold_split_nc", 64);
     // halo conv: weight tap rows loaded two rows ahead (halo_conv.hip PF2)
-    halo_pf2 = env("UMAMD_HALO_PF2", 0);
+    halo_pf2 = env("halo_pf2", 0);
     // halo conv as persistent workgroups (resident count x this; 0 = one
     // tile per workgroup) that prefetch the next tile's halo; halo_grid > 0
     // caps the grid (tests: several tiles per workgroup on small images)
-    halo_persist = env("UMAMD_HALO_PERSIST", 1);
-    halo_grid = env("UMAMD_HALO_GRID", 0);
+    halo_persist = env("halo_persist", 1);
+    halo_grid = env("halo_grid", 0);
     // 3x3 halo convs keep all their tap weights in LDS (per workgroup, for
     // all its tiles) when they need at most this many KB; 0 = stream rows
-    halo_res_kb = env("UMAMD_HALO_RES_KB", 48);
+    halo_res_kb = env("halo_res_kb", 48);
     // reflect fold of the split-form data gradient: a VALU pass over the
     // border list (conv.hip reflect_border_kernel) instead of the GEMM
-    border_valu = env("UMAMD_BORDER_VALU", 1);
-    // consistency-gradient scatter of the loss backward: 1/2/4 row-owned waves
-    // without LDS atomics (steps per iteration), 0 the atomic strip kernel
-    // (loss.hip; the row form is within noise at the step level)
-    loss_scatter = env("UMAMD_LOSS_SCATTER", 0);
+    border_valu = env("border_valu", 1);
   }
 };
 Knobs& knobs() {
@@ -1140,7 +1125,6 @@ int igemm_halo_persist() { return knobs().halo_persist; }
 int igemm_halo_grid() { return knobs().halo_grid; }
 int igemm_halo_res_kb() { return knobs().halo_res_kb; }
 int igemm_border_valu() { return knobs().border_valu; }
-int knob_loss_scatter() { return knobs().loss_scatter; }
 
 int igemm_border_list(IgArgs& a) {
   const int H = a.oh, W = a.ow, p = a.fold_pad;
@@ -1268,7 +1252,6 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "halo_grid")) f = &k.halo_grid;
   else if (!strcmp(key, "halo_res_kb")) f = &k.halo_res_kb;
   else if (!strcmp(key, "border_valu")) f = &k.border_valu;
-  else if (!strcmp(key, "loss_scatter")) f = &k.loss_scatter;
   if (!f) return -1;
   const int old = *f;
   *f = value;

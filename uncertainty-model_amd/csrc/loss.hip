@@ -836,127 +836,6 @@ __global__ void __launch_bounds__(SCT) loss_scatter_kernel(LArgs a) {
   }
 }
 
-// (1') the same scatter without LDS atomics (knob loss_scatter /
-// UMAMD_LOSS_SCATTER = 1, 2, 4 steps per iteration; default 0 = the kernel
-// above: the two are within noise at the step level, profiles/r04/
-// loss_scatter_ab.txt).  The atomic adds above run at ~2.5 LDS cycles per
-// lane (SQ_LDS_IDX_ACTIVE / lane-adds, profiles/r04/w_counters.json) and kept
-// the LDS busy for the whole launch.  Here one wave owns each source row, so
-// no other wave touches that row's accumulator, and it walks the row 64
-// consecutive sources per step.  When a step's left taps x0 are strictly
-// increasing across the lanes (the shift moves by less than a pixel between
-// neighbours: smooth disparities) lane L adds its e-part plus lane L-1's w-part
-// when that lands on the same column, and its own w-part only when lane L+1
-// does not take it: every column is touched by one lane, so a plain
-// read-modify-write is exact and the summation order fixed.  A step whose
-// taps are not increasing takes LDS atomics for that term.
-constexpr int STW = 6;               // target rows per workgroup
-constexpr int SWT = (STW + 2) * 64;  // one wave per source row
-
-__device__ __forceinline__ void row_scatter(float* X, int W, bool in, int x0, float ve,
-                                            float vw) {
-  constexpr int NONE = -(1 << 30);
-  const int lane = threadIdx.x & 63;
-  const int xo = in ? x0 : NONE;  // lanes past the row end are a tail
-  const int up = __shfl_up(xo, 1, 64), dn = __shfl_down(xo, 1, 64);
-  const float wp = __shfl_up(vw, 1, 64);
-  const int xp = lane > 0 ? up : NONE, xn = lane < 63 ? dn : NONE;
-  if (__any(in && xp != NONE && xo <= xp)) {
-    if (in && x0 >= 0 && x0 < W) atomicAdd(&X[x0], ve);
-    if (in && x0 + 1 >= 0 && x0 + 1 < W) atomicAdd(&X[x0 + 1], vw);
-    return;
-  }
-  const bool take = xp != NONE && xp + 1 == xo;  // lane L-1's w-part lands on my x0
-  const bool give = xn != NONE && xn == xo + 1;  // lane L+1 takes my w-part
-  if (in && x0 >= 0 && x0 < W) X[x0] += ve + (take ? wp : 0.f);
-  if (in && !give && x0 + 1 >= 0 && x0 + 1 < W) X[x0 + 1] += vw;
-}
-
-template <int U>
-__global__ void __launch_bounds__(SWT) loss_scatter_rows_kernel(LArgs a) {
-  extern __shared__ float acc[];  // [STW + 2 source rows][2 target ch][W]
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int s = scale_of(a, blockIdx.x);
-  const LScale S = scale_desc(a, s);
-  const int H = S.h, W = S.w;
-  const int HW = H * W;
-  const int lb = blockIdx.x - S.block0;
-  const int n = lb / S.tiles_y, y0 = (lb - n * S.tiles_y) * STW;
-  const float* pp = S.pred + (long)n * HW * 4;
-  const double np = (double)a.N * HW;
-  const float kcd = (float)(a.gout[0] * a.w_cons / np);
-  const float kce = (float)(a.gout[1] * a.w_err * a.ecw / np);
-  const float Wh = (float)W * 0.5f;
-  const float stepx = W > 1 ? 1.f / (float)(W - 1) : 0.f;
-  const int halfw = W / 2;
-  const int r0 = max(0, y0 - 1), r1 = min(H, y0 + STW + 1);
-  const int nr = r1 - r0;
-  for (int i = tid; i < nr * 2 * W; i += SWT) acc[i] = 0.f;
-  __syncthreads();
-  if (wid < nr) {
-    const int y = r0 + wid;
-    const RowW rw = row_w(y, H);
-    float* X = acc + wid * 2 * W;
-    const float* prow = pp + (long)y * W * 4;
-    // U steps of 64 sources per iteration: every step's taps are gathered
-    // before the first step's LDS updates
-    for (int xb = 0; xb < W; xb += 64 * U) {
-      bool in[U];
-      Samp t[U][4];
-      float val[U][4], wv[U][4];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int x = xb + 64 * u + lane;
-        in[u] = x < W;
-        const float4 p = *reinterpret_cast<const float4*>(prow + min(x, W - 1) * 4);
-        const float linx = lin01s(min(x, W - 1), W, halfw, stepx);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {  // (view, term): (0,d) (1,d) (0,sigma) (1,sigma)
-          const int v = j & 1;
-          val[u][j] = comp(p, j < 2 ? v : 2 + v);
-          t[u][j] = warp_tab(linx, rw, (v == 0 ? -1.f : 1.f) * val[u][j], Wh);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        cons_samples<1>(pp + 1, H, W, t[u], wv[u], nullptr);
-        cons_samples<1>(pp + 0, H, W, t[u] + 1, wv[u] + 1, nullptr);
-        if (a.ecw != 0.f) {
-          cons_samples<1>(pp + 1, H, W, t[u] + 2, wv[u] + 2, nullptr);
-          cons_samples<1>(pp + 0, H, W, t[u] + 3, wv[u] + 3, nullptr);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (xb + 64 * u >= W) break;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (j >= 2 && a.ecw == 0.f) break;
-          const int v = j & 1;
-          const float gg = in[u] ? -sgnf(val[u][j] - wv[u][j]) * (j < 2 ? kcd : kce) : 0.f;
-          row_scatter(X + (1 - v) * W, W, in[u], t[u][j].x0, gg * t[u][j].e, gg * t[u][j].w);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  float* sa = S.dpred + ((long)n * HW + (long)y0 * W) * 4;
-  const int rows = min(STW, H - y0);
-  for (int i = tid; i < rows * W; i += SWT) {
-    const int T = y0 + i / W, x = i % W;
-    float g0 = 0.f, g1 = 0.f;
-    for (int r = max(r0, T - 2); r <= min(r1 - 1, T + 2); ++r) {
-      const RowW rw = row_w(r, H);
-      const float wgt = rw.y0 == T ? 1.f - rw.n : (rw.y0 + 1 == T ? rw.n : 0.f);
-      if (wgt == 0.f) continue;
-      const float* X = acc + (r - r0) * 2 * W;
-      g0 += wgt * X[x];
-      g1 += wgt * X[W + x];
-    }
-    *reinterpret_cast<float2*>(sa + i * 4) = make_float2(g0, g1);
-  }
-}
-
 // (2) every other gradient, per TY x TX tile (both views), plus the scatter sums
 constexpr int BTY = 16, BTX = 32, BNT = 512;
 using BT = Tile<BTY, BTX>;
@@ -1328,8 +1207,7 @@ int um_loss_bwd(int nscales, int N, int H, int W, const float* const* img,
   UM_CHECK_ARG(nscales >= 1 && nscales <= MAXS, "um_loss_bwd: %d scales (1..%d)", nscales, MAXS);
   UM_CHECK_ARG((H >> (nscales - 1)) >= 3 && (W >> (nscales - 1)) >= 3,
                "um_loss_bwd: image %dx%d too small for %d scales", H, W, nscales);
-  const bool rows = umamd::knob_loss_scatter() != 0;
-  const size_t lds = (size_t)((rows ? STW : STR) + 2) * W * 2 * sizeof(float);
+  const size_t lds = (size_t)(STR + 2) * W * 2 * sizeof(float);
   UM_CHECK_ARG(lds <= 128 * 1024, "um_loss_bwd: width %d too large", W);
   LArgs a{};
   a.alpha = alpha; a.loss_type = loss_type; a.esw = esw; a.ecw = ecw;
@@ -1339,25 +1217,11 @@ int um_loss_bwd(int nscales, int N, int H, int W, const float* const* img,
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&loss_scatter_kernel),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&loss_scatter_rows_kernel<1>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&loss_scatter_rows_kernel<2>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&loss_scatter_rows_kernel<4>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
     attr = true;
   }
   // (1) consistency scatter sums into channels 0/1 of dpred, (2) the rest
-  int blocks = loss_setup(a, nscales, N, H, W, img, pred, dpred, rows ? STW : STR, 0);
-  const int su = umamd::knob_loss_scatter();
-  if (su >= 4)
-    hipLaunchKernelGGL(loss_scatter_rows_kernel<4>, dim3(blocks), dim3(SWT), lds, st, a);
-  else if (su == 2)
-    hipLaunchKernelGGL(loss_scatter_rows_kernel<2>, dim3(blocks), dim3(SWT), lds, st, a);
-  else if (su == 1)
-    hipLaunchKernelGGL(loss_scatter_rows_kernel<1>, dim3(blocks), dim3(SWT), lds, st, a);
-  else
-    hipLaunchKernelGGL(loss_scatter_kernel, dim3(blocks), dim3(SCT), lds, st, a);
+  int blocks = loss_setup(a, nscales, N, H, W, img, pred, dpred, STR, 0);
+  hipLaunchKernelGGL(loss_scatter_kernel, dim3(blocks), dim3(SCT), lds, st, a);
   blocks = loss_setup(a, nscales, N, H, W, img, pred, dpred, BTY, BTX);
   hipLaunchKernelGGL(loss_grad_kernel, dim3(blocks), dim3(BNT), 0, st, a);
   UM_LAUNCH_CHECK();

@@ -413,7 +413,6 @@ int um_merge_bwd_bn(int dtype, int nsrc, const void* const* srcs, void* const* d
                      n8, (const T_*)dm, parts, fsrc, (const TY_*)y, C, mean, invstd, scale, shift,   \
                      apply_elu, slots, M)
   if (dtype == (UM_BF16 | UM_Y_ACT)) UM_MBB(bf16_t, bf16_t);
-  else if (dtype == (UM_BF16 | UM_Y_F16)) UM_MBB(bf16_t, f16_t);
   else if (dtype == UM_BF16) UM_MBB(bf16_t, float);
   else UM_MBB(float, float);
 #undef UM_MBB

@@ -18,6 +18,8 @@
 // stream-ordered (one stream per process, as everywhere in umamd).
 #include <cstdlib>
 
+#include <cstring>
+
 #include "common.h"
 #include "reduce.h"
 
@@ -215,15 +217,23 @@ namespace umamd {
 // agent-scope release/acquire pair costs about as much as a kernel boundary,
 // MI355X_MICROARCH.md price list).  Larger: 256-thread workgroups of >= 16K
 // values each and the last-arriver finish.
-// (UMAMD_COLRED_SINGLE / UMAMD_COLRED_PER override the two sizes for sweeps)
-static long env_long(const char* n, long d) {
-  const char* v = getenv(n);
-  return v ? atol(v) : d;
+// (UMAMD_TUNING colred_single / colred_per override the two sizes for sweeps)
+long tuning_env(const char* key, long dflt) {
+  const char* v = getenv("UMAMD_TUNING");
+  if (v == nullptr) return dflt;
+  const size_t n = strlen(key);
+  for (const char* p = v; *p;) {
+    if (!strncmp(p, key, n) && p[n] == '=') return atol(p + n + 1);
+    p = strchr(p, ',');
+    if (p == nullptr) break;
+    ++p;
+  }
+  return dflt;
 }
 
 int colred_blocks(int nparts, int C, int NV) {
-  static const long single = env_long("UMAMD_COLRED_SINGLE", 128 * 1024);
-  static const long per = env_long("UMAMD_COLRED_PER", 16384);
+  static const long single = tuning_env("colred_single", 128 * 1024);
+  static const long per = tuning_env("colred_per", 16384);
   const long work = (long)nparts * C * NV;
   if (work <= single) return 1;
   long b = (work + per - 1) / per;  // >= `per` values per workgroup

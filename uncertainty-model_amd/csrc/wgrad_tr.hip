@@ -254,11 +254,10 @@ namespace umamd {
 
 int wgrad_tr_bm(int K) { return K <= 64 ? 64 : 128; }
 
-// pixels per k-step (UMAMD_WTR_TBK overrides: 32, 64 or 128)
+// pixels per k-step (tuning key wtr_tbk: 32, 64 or 128)
 int wgrad_tr_tbk() {
   static const int v = [] {
-    const char* e = getenv("UMAMD_WTR_TBK");
-    const int t = e ? atoi(e) : 32;
+    const int t = (int)umamd::tuning_env("wtr_tbk", 32);
     return (t == 64 || t == 128) ? t : 32;
   }();
   return v;

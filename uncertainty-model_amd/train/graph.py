@@ -37,7 +37,6 @@ stream (``stream=``).
 """
 from __future__ import annotations
 
-import contextlib
 import os
 
 import torch
@@ -85,13 +84,12 @@ class CapturedTrainStep:
             self._buckets = GradBuckets(model.parameters(), self.group, self.world,
                                         cap_mb=mb if mb > 0 else 1e9)
         # RCCL collectives of the step (SyncBN, gradient buckets) through the
-        # step's own communicator on the launch stream (umamd.rccl: no process
-        # group watchdog polling events of a capturing stream, no stream hop);
-        # UMAMD_OWN_RCCL=0 keeps the process group
+        # step's own communicator, in one total order across the issuing
+        # streams (umamd.rccl: no process group watchdog polling events of a
+        # capturing stream, no stream hop, no cross-communicator deadlock)
         self._comm = None
-        if self.group is not None and dist.get_backend(self.group) == 'nccl' and \
-                os.environ.get('UMAMD_OWN_RCCL', '1') != '0':
-            self._comm = rccl.comms_for(self.group)
+        if self.group is not None and dist.get_backend(self.group) == 'nccl':
+            self._comm = rccl.acquire(self.group)
         snap = self._snapshot(model, optimiser) if restore_state else None
         self.model, self.loss_function, self.optimiser = model, loss_function, optimiser
         self.scale, self.scales = float(scale), scales
@@ -102,16 +100,6 @@ class CapturedTrainStep:
             self.overlap = overlap.WgradStream(p for p in model.parameters() if p.requires_grad)
         self.left = left.detach().clone().contiguous()
         self.right = right.detach().clone().contiguous()
-        # UMAMD_LOSS_OVERLAP=1: the fused loss forward (the loss values) on a
-        # side stream beside the backward (umamd.lossfn.forward_on_side_stream).
-        # Off: bench step A/B on MI355X 763 with vs 766 pairs/s without
-        # (profiles/r04/loss_overlap_arms.txt) -- the loss tiles contend with
-        # the backward's first kernels instead of filling idle CUs
-        self._loss_stream = None
-        if os.environ.get('UMAMD_LOSS_OVERLAP', '0') != '0':
-            self._loss_stream = torch.cuda.Stream(device=self.left.device)
-        self._one = torch.ones((), dtype=torch.float32, device=self.left.device)
-        self._loss_events = []
         cur = torch.cuda.current_stream()
         side = stream if stream is not None else torch.cuda.Stream()
         if side != cur:
@@ -196,19 +184,10 @@ class CapturedTrainStep:
                 recon = u.reconstruct_pyramid(disparities, pyramid)
         else:
             recon = u.reconstruct_pyramid(disparities, pyramid)
-        side = self._loss_stream if isinstance(self.loss_function, TukraUncertaintyLoss) else None
-        events = []
-        with (LF.forward_on_side_stream(side, events) if side is not None
-              else contextlib.nullcontext()):
-            disp_loss, error_loss = self.loss_function(pyramid, disparities, recon, 0, None)
+        disp_loss, error_loss = self.loss_function(pyramid, disparities, recon, 0, None)
 
         def backward():
-            if side is not None:
-                # d(disp + error)/d(each) = 1 without reading the values (a sum
-                # would wait for the loss forward on the side stream)
-                torch.autograd.backward([disp_loss, error_loss], [self._one, self._one])
-            else:
-                (disp_loss + error_loss).backward()
+            (disp_loss + error_loss).backward()
         if self.overlap is None:
             if self._buckets is not None:
                 self._buckets.arm()
@@ -220,9 +199,6 @@ class CapturedTrainStep:
                 backward()
         if self._buckets is not None:
             self._reduce_grads()
-        if side is not None:  # the loss values join the step
-            overlap.stream_wait(torch.cuda.current_stream(), side, events)
-            self._loss_events = events  # alive until the next capture or step
         return disp_loss, error_loss
 
     @property
@@ -249,6 +225,10 @@ class CapturedTrainStep:
             self._buckets = None
         self.g_fb = self.g_opt = None
         self._opt_tables = []
+        if self._comm is not None:  # after the graphs that recorded its collectives
+            torch.cuda.synchronize()
+            rccl.release(self._comm)
+            self._comm = None
 
     def __call__(self, left=None, right=None):
         if left is not None:

@@ -48,13 +48,22 @@ def _headers():
     return sorted(glob.glob(os.path.join(CSRC, '*.h')) + glob.glob(os.path.join(INCLUDE, '*.h')))
 
 
+def _flags_key() -> str:
+    """the compile flags as they enter the stamps: the include directories
+    relative to the repository, so a copy of the tree at another path (the
+    GPU box's snapshot) sees the same stamps and loads the shipped library
+    instead of rebuilding it"""
+    root = os.path.dirname(PKG)
+    return ' '.join(os.path.relpath(f, root) if os.path.isabs(f) else f for f in FLAGS)
+
+
 def _hash_files(files, extra=b'') -> str:
     h = hashlib.sha256()
     for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, 'rb') as fh:
             h.update(fh.read())
-    h.update(' '.join(FLAGS).encode())
+    h.update(_flags_key().encode())
     h.update(extra)
     return h.hexdigest()
 

@@ -14,11 +14,10 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libumamd.so')
 
-UM_F32, UM_BF16, UM_F16 = 0, 1, 2
+UM_F32, UM_BF16 = 0, 1
 # OR'ed into the dtype of the um_bn_elu_* entries / um_conv2d_fwd_up2: the
 # pre-BN y is stored in the activation dtype (include/umamd.h)
 Y_ACT = 0x100
-Y_F16 = 0x200
 PAD_ZERO, PAD_REFLECT = 0, 1
 EPI_NONE, EPI_STATS, EPI_SIGMOID_SCALE, EPI_RESIDUAL, EPI_STAT_SLOTS = 0, 1, 2, 3, 4
 STAT_SLOTS = 16  # UM_STAT_SLOTS (include/umamd.h)
@@ -34,16 +33,6 @@ _D = ctypes.c_double
 class CatSrc(ctypes.Structure):
     _fields_ = [('ptr', _P), ('scale', _P), ('C', _I), ('ld', _I), ('op', _I),
                 ('coff', _I), ('dtype', _I), ('h', _I), ('w', _I)]
-
-
-WRED_MAX = 24  # UM_WRED_MAX
-
-
-class WredDesc(ctypes.Structure):
-    """um_wred_desc: one slab reduction of um_conv_wgrad_reduce_batch"""
-    _fields_ = [('slabs', _P), ('dw', _P), ('splits', _I), ('K', _I), ('Kreal', _I), ('R', _I),
-                ('C', _I), ('Creal', _I), ('accumulate', _I), ('nseg', _I),
-                ('src0', _I * 4), ('dst0', _I * 4), ('len', _I * 4)]
 
 
 MWG_MAX, MWG_SRC = 24, 8  # UM_MWG_MAX, UM_MWG_SRC
@@ -87,7 +76,6 @@ _SIG = {
     'um_pack_tiles': (_I, [_I, _I, _I]),
     'um_pack_weight_seg': (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P, 's']),
     'um_conv_wgrad_reduce_seg': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, 's']),
-    'um_conv_wgrad_reduce_batch': (_I, [_P, _I, 's']),
     'um_colsum_parts': (_I, [_I]),
     'um_colsum_batch': (_I, [_I, _P, _I, 's']),
     'um_colsum': (_I, [_I, _I, _I, _I, _P, _P, 's']),
@@ -102,18 +90,15 @@ _SIG = {
     'um_bn_fwd_pool_parts_c': (_I, [_L, _L, _I]),
     'um_bn_elu_fwd': (_I, [_I, _L, _I, _P, _I, _P, _P, _P, _I, _I, _L, _P, 's']),
     'um_bn_elu_fwd_slots': (_I, [_I, _L, _I, _P, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P, _P, _P,
-                                 _P, _P, _P, _I, _I, _L, _P, _P, _P, 's']),
+                                 _P, _P, _P, _I, _I, _L, _P, 's']),
     'um_bn_elu_fwd_slots_merge': (_I, [_I, _L, _I, _P, _I, _P, _D, _P, _P, _F, _F, _P, _P, _P,
-                                       _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P,
-                                       _P, 's']),
+                                       _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P,
+                                       's']),
     'um_bn_elu_bwd_reduce_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
                                         _P, 's']),
     'um_bn_elu_bwd_apply_slots': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
                                        _P, _D, _P, _P, _P, _P, _P, _F, _P, _I, 's']),
     'um_bn_bwd_parts': (_I, [_L]),
-    'um_bn_bwd_fin_ws': (_L, [_L, _I]),
-    'um_bn_elu_bwd_reduce_coeffs': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I,
-                                        _P, _P, _P, _P, _P, _P, _P, _P, _P, 's']),
     'um_bn_elu_bwd_reduce': (_I, [_I, _L, _I, _L, _P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P,
                                   's']),
     'um_bn_bwd_coeffs': (_I, [_P, _D, _I, _P, _P, _P, _P, _P, _P, _F, _I, _P, _P, _P, 's']),
@@ -132,9 +117,6 @@ _SIG = {
     'um_sigmoid_scale_bwd': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
     'um_sigmoid_scale_bwd_split': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
     'um_head_split_fin': (_I, [_L, _I, _P, _I, _P, _F, _P, _I, 's']),
-    'um_head_fwd': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, 's']),
-    'um_head_dgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, 's']),
-    'um_head_wgrad': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, 's']),
     'um_pack_weight_split': (_I, [_P, _I, _I, _I, _I, _P, _P, _I, 's']),
     'um_attn_ws_kstats': (_L, [_I, _I, _I]),
     'um_attn_ws_ctx': (_L, [_I, _I, _I, _I]),
@@ -296,6 +278,4 @@ def dtype_code(dt: torch.dtype) -> int:
         return UM_F32
     if dt == torch.bfloat16:
         return UM_BF16
-    if dt == torch.float16:  # the pre-BN y storage of UM_Y_F16 only
-        return UM_F16
     raise UmamdError(f'unsupported activation dtype {dt}')

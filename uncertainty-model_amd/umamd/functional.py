@@ -139,58 +139,27 @@ def _conv_wgrad(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw=None, segs=
     dw_ptr = ptr(dw)
     N, _, _, _ = x.shape
     _, P, Q, _ = dy.shape
-    if _WRED_BATCH:  # kernel now, slab reduce batched with the flush's others
-        launch = lambda: _conv_wgrad_slabs(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode,  # noqa: E731
-                                           dw_ptr, segs)
-    else:
-        launch = lambda: _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad,  # noqa: E731
-                                        pad_mode, dw_ptr, segs)
+    launch = lambda: _conv_wgrad_on(x, dy, K, Kreal, Creal, R, stride, pad,  # noqa: E731
+                                    pad_mode, dw_ptr, segs)
     ov.defer((x, dy), launch, out_ptr=dw_ptr, flop=_conv_flops(N, P, Q, Kreal, R, Creal),
              out_bytes=dw.numel() * 4)
     return dw
 
 
-# the side stream's slab reductions as ONE um_conv_wgrad_reduce_batch launch
-# per flush instead of one um_conv_wgrad_reduce_seg per conv.  Measured on
-# MI355X (bench step, tools/gpu_arms.sh r03j): 734 with vs 771 pairs/s
-# without -- the batch lands as one chip-wide burst at the end of each flush
-# instead of small reductions filling the gaps beside the data-gradient
-# chain -- so it is off; the merge-weight gradients (15 single-workgroup
-# launches -> 1 per flush) stay batched (UMAMD_MWG_BATCH)
-_WRED_BATCH = os.environ.get('UMAMD_WRED_BATCH', '0') == '1'
+# the merge-weight gradients of a side-stream flush as one um_merge_wgrad_batch
+# launch (15 single-workgroup launches -> 1 per flush)
 _MWG_BATCH = os.environ.get('UMAMD_MWG_BATCH', '1') == '1'
 
 
-def _conv_wgrad_slabs(x, dy, K, Kreal, Creal, R, stride, pad, pad_mode, dw_ptr, segs):
-    """The weight-gradient kernel into f32 slabs -> (slabs, um_wred_desc) for
-    a batched reduction (overlap.WgradStream._flush)."""
-    N, H, W, C = x.shape
-    _, P, Q, ldy = dy.shape
-    splits = query('um_conv_wgrad_splits', _dt(x), N, H, W, C, C, K, R, stride, pad, pad_mode,
-                   P, Q, ldy)
-    slabs = torch.empty((splits, K, R * R * C), dtype=torch.float32, device=x.device)
-    call('um_conv2d_wgrad', _dt(x), N, H, W, C, C, ptr(x), K, R, stride, pad, pad_mode, P, Q,
-         ptr(dy), ldy, ptr(slabs), splits, work=_conv_flops(N, P, Q, Kreal, R, Creal))
-    d = L.WredDesc()
-    d.slabs, d.dw = slabs.data_ptr(), dw_ptr
-    d.splits, d.K, d.Kreal, d.R, d.C, d.Creal, d.accumulate = splits, K, Kreal, R, C, Creal, 0
-    d.nseg = len(segs) if segs else 0
-    for i, (a0, b0, l0) in enumerate(segs or ()):
-        d.src0[i], d.dst0[i], d.len[i] = a0, b0, l0
-    return slabs, d
-
-
 def batched_launch(descs):
-    """The batched launches of a side-stream flush: every um_wred_desc in
-    um_conv_wgrad_reduce_batch calls, every um_mwg_desc in
-    um_merge_wgrad_batch calls (in chunks of the entries' maxima)."""
-    for kind, name, cap in ((L.WredDesc, 'um_conv_wgrad_reduce_batch', L.WRED_MAX),
-                            (L.MwgDesc, 'um_merge_wgrad_batch', L.MWG_MAX)):
-        ds = [d for d in descs if isinstance(d, kind)]
-        for i in range(0, len(ds), cap):
-            chunk = ds[i:i + cap]
-            arr = (kind * len(chunk))(*chunk)
-            call(name, _ct.cast(arr, ctypes_p), len(chunk))
+    """The batched launches of a side-stream flush: every um_mwg_desc in
+    um_merge_wgrad_batch calls, every um_csum_desc in um_colsum_batch calls
+    (in chunks of the entries' maxima)."""
+    ds = [d for d in descs if isinstance(d, L.MwgDesc)]
+    for i in range(0, len(ds), L.MWG_MAX):
+        chunk = ds[i:i + L.MWG_MAX]
+        arr = (L.MwgDesc * len(chunk))(*chunk)
+        call('um_merge_wgrad_batch', _ct.cast(arr, ctypes_p), len(chunk))
     cs = [d for d in descs if isinstance(d, _Csum)]
     for dt in sorted({d.dtype for d in cs}):
         ds = [d.desc for d in cs if d.dtype == dt]
@@ -293,11 +262,10 @@ _CONSTS = {}
 # A/B switches for two fused paths (bench step, tools/sweep.sh):
 #  - the SE squeeze summed inside the BN forward (per-block channel sums,
 #    finished by the SE MLP kernel): on, 676 -> 678 pairs/s (-10 launches)
-#  - the BN backward coefficients finished inside the reduce kernel by a
-#    two-level last-arriver tree: off, 676 -> 652 -- every block's
-#    agent-scope release + ticket costs more than the separate reduction
-#    launch it replaces
-_FUSED_BN_BWD = os.environ.get('UMAMD_FUSED_BN_BWD', '0') == '1'
+#  - (removed round 5) the BN backward coefficients finished inside the
+#    reduce kernel by a two-level last-arriver tree: 676 -> 652 -- every
+#    block's agent-scope release + ticket cost more than the separate
+#    reduction launch it replaced
 _FUSED_SE = os.environ.get('UMAMD_FUSED_SE', '1') == '1'
 #  - single-process BN statistics as f64 atomics into zeroed slots, finished
 #    by the consumer kernels (no reduction launch per BN layer and direction)
@@ -308,47 +276,23 @@ _BN_SLOTS = os.environ.get('UMAMD_BN_SLOTS', '1') == '1'
 #    the conv's store move 2 bytes per element less.  OFF by default since
 #    round 4: +2.3 % throughput (790 -> 808 pairs/s, round 3), but the
 #    step-0 error loss at BASELINE config 2 moves 4.7e-3 from the reference
-#    with bf16 y against 1.9e-3 with f32 y (3.6e-3 with the centring below;
-#    tools/bf16_arms.py, profiles/r04/bf16_arms.txt): in the smooth layers the
-#    batch std is ~1/17 of the mean, so the rounding of y is ~17x larger
-#    relative to the normalised x-hat than the rounding of the activations
+#    with bf16 y against 1.9e-3 with f32 y (tools/bf16_arms.py,
+#    profiles/r04/bf16_arms.txt): in the smooth layers the batch std is ~1/17
+#    of the mean, so the rounding of y is ~17x larger relative to the
+#    normalised x-hat than the rounding of the activations.  (Round 5 removed
+#    the f16 y and the centred bf16 y: both measured, neither reached the
+#    f32 y's error.)
 _Y_ACT = os.environ.get('UMAMD_Y_ACT', '0') == '1'
-#  - ... or in f16 (UM_Y_F16): 2 bytes like bf16 y with 3 more mantissa bits;
-#    with the centring below the values are O(batch std), far inside f16's range
-_Y_F16 = os.environ.get('UMAMD_Y_F16', '0') == '1'
 
 
 def _ydtype(dt):
     """storage dtype of the pre-BN conv output for activations of ``dt``"""
-    if dt == torch.bfloat16 and _Y_F16:
-        return torch.float16
     return dt if (_Y_ACT and dt == torch.bfloat16) else torch.float32
-
-
-_Y_CENTER = os.environ.get('UMAMD_Y_CENTER', '1') == '1'
-
-
-def _ycen(bn, K, dev):
-    """The BN layer's centring buffer for its bf16 pre-BN output ([K] f32,
-    persistent on the module, not in its state_dict; see um_bn_elu_fwd_slots):
-    the conv runs with it as its bias, and the BN pass sets it to minus the
-    conv-only batch mean for the next step.  Any value gives the same BN
-    output; a centred y keeps its bf16 rounding error relative to the batch
-    std instead of the mean.  None with UMAMD_Y_CENTER=0."""
-    if not _Y_CENTER:
-        return None
-    t = getattr(bn, '_umamd_ycen', None)
-    if t is None or t.numel() != K or t.device != dev:
-        t = torch.zeros(K, dtype=torch.float32, device=dev)
-        bn._umamd_ycen = t
-    return t
 
 
 def _ydt(a, y):
     """dtype code of a BN entry: activations ``a`` (a / da), plus UM_Y_ACT
-    when the pre-BN ``y`` is stored in their dtype, UM_Y_F16 when in f16"""
-    if y.dtype == torch.float16:
-        return _dt(a) | L.Y_F16
+    when the pre-BN ``y`` is stored in their dtype"""
     return _dt(a) | (L.Y_ACT if y.dtype != torch.float32 else 0)
 
 
@@ -430,13 +374,24 @@ class GradSlots:
     (or into that buffer in place, by its own choice), so a later registered
     consumer's accumulate could land in a tensor autograd no longer passes
     on: its term would be lost.  In the model every pooled tensor is
-    consumed only inside the forward (the disparities, which the loss reads,
-    have a single registered use and are never pooled).
+    consumed only inside the forward (the submodules run through their
+    ``_fwd`` paths, so no forward hook sees an intermediate; the
+    disparities, which the loss reads, have a single registered use and are
+    never pooled).
+    Guard: every pooled tensor gets a gradient hook that checks that the
+    gradient autograd finally hands on IS the pooled buffer; if another
+    consumer made autograd sum into a new one, it raises (the step's
+    gradient is incomplete) and turns pooling off for every later forward
+    (``GradSlots.broken``), so the next step runs on autograd's sums.
     UMAMD_GRAD_SLOTS=0 turns it off."""
+
+    broken = False
 
     def __init__(self):
         self.uses = {}
         self.bufs = {}
+        self.final = {}   # key -> data_ptr of the pooled buffer (set by done)
+        self.hooked = set()
 
     @staticmethod
     def key(t):
@@ -447,7 +402,22 @@ class GradSlots:
         if t is not None and t.requires_grad:
             k = self.key(t)
             self.uses[k] = self.uses.get(k, 0) + 1
+            if self.uses[k] == 2 and k not in self.hooked:
+                self.hooked.add(k)
+                t.register_hook(lambda g, k=k: self._check(k, g))
             return k
+        return None
+
+    def _check(self, k, g):
+        """gradient hook of a pooled tensor: autograd's final gradient must
+        be the pooled buffer (no unregistered consumer summed into another)"""
+        want = self.final.get(k)
+        if want is not None and g is not None and g.data_ptr() != want:
+            GradSlots.broken = True
+            raise RuntimeError(
+                'umamd GradSlots: an activation that umamd ops accumulate gradients into in '
+                'place also has a consumer outside them, so its gradient is incomplete for this '
+                'step; pooling is now off for later forwards (UMAMD_GRAD_SLOTS=0 avoids it)')
         return None
 
     def target(self, k):
@@ -464,6 +434,7 @@ class GradSlots:
         e = self.bufs.get(k)
         if e is None:  # first consumer: keep the buffer for the others
             self.bufs[k] = [g, self.uses[k] - 1]
+            self.final[k] = g.data_ptr()
             return g
         e[1] -= 1
         if e[1] <= 0:
@@ -480,7 +451,7 @@ def grad_slots():
     """one GradSlots registry for the consumers called inside (a model forward)"""
     global _GSLOTS
     prev = _GSLOTS
-    _GSLOTS = GradSlots() if _GRAD_SLOTS else None
+    _GSLOTS = GradSlots() if _GRAD_SLOTS and not GradSlots.broken else None
     try:
         yield
     finally:
@@ -539,7 +510,7 @@ class BNSync:
 
     def all_reduce(self, t: torch.Tensor):
         if self.collective:
-            c = _rccl.active(self.group, 'bn')  # the captured step's own communicator
+            c = _rccl.active(self.group)  # the captured step's own communicator
             if c is not None:
                 c.all_reduce(t)
             else:
@@ -640,13 +611,9 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
         nslot = L.STAT_SLOTS * K * 2
         slots_f = _ARENA.take(nslot + 1)
         slots_b = _ARENA.take(nslot + 1)
-        # a bf16 y is stored centred: the conv's bias is the layer's ycen
-        # buffer (minus the last step's conv-only mean), see um_bn_elu_fwd_slots
-        ycen = _ycen(bn, K, dev) if _ydtype(x.dtype) != torch.float32 else None
-        cbias = ycen if ycen is not None else bias_f
-        y = _conv_fwd(x, wf, cbias, K, R, spec.stride, spec.pad, spec.pad_mode,
+        y = _conv_fwd(x, wf, bias_f, K, R, spec.stride, spec.pad, spec.pad_mode,
                       out_dtype=_ydtype(x.dtype), epi=L.EPI_STAT_SLOTS, stats=slots_f,
-                      creal=Creal) if yconv is None else yconv(L.EPI_STAT_SLOTS, slots_f, cbias)
+                      creal=Creal) if yconv is None else yconv(L.EPI_STAT_SLOTS, slots_f, bias_f)
         if sync.collective:  # the conv stored this rank's count after the slots
             sync.all_reduce(slots_f)
             count = -1.0  # read the all-reduced count after the slots
@@ -690,13 +657,12 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
                  ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K, int(spec.elu), n,
                  (ctypes_p * n)(*[t.data_ptr() if t is not None else None for t in msrcs]),
-                 (ctypes_i * n)(*mwidx), ptr(mw), msrcs.index(None), ptr(merged), ptr(ycen),
-                 ptr(bias_f))
+                 (ctypes_i * n)(*mwidx), ptr(mw), msrcs.index(None), ptr(merged))
         else:
             call('um_bn_elu_fwd_slots', _ydt(a, y), M, K, ptr(y), K, ptr(slots_f), count,
                  ptr(gamma), ptr(beta), float(bn.eps), float(bn.momentum or 0.0), *rs,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(a), K,
-                 int(spec.elu), P * Q, ptr(pool), ptr(ycen), ptr(bias_f))
+                 int(spec.elu), P * Q, ptr(pool))
     else:
         call('um_bn_elu_fwd', _ydt(a, y), M, K, ptr(y), K, ptr(scale), ptr(shift), ptr(a), K,
              int(spec.elu), P * Q, ptr(pool))
@@ -730,9 +696,6 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
     ctx.se = se
     ctx.saved = (x, wT, y, mean, invstd, scale, shift, gamma, w1, w2)
     return tuple(outs), ctx
-
-
-_SYNCBN_LOCAL = os.environ.get('UMAMD_SYNCBN_LOCAL', '0') == '1'
 
 
 def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=False,
@@ -779,12 +742,16 @@ def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=
         local, bcount, bscale = None, float(M), 1.0
         if ctx.sync is not None and ctx.sync.collective:
             # k1..k3 from the global sums.  dgamma/dbeta and the conv-bias
-            # gradient: the global sums / world, whose DDP average equals the
-            # average of torch SyncBatchNorm's per-rank sums -- no copy of
-            # this rank's slots before the in-place all-reduce (one launch
-            # per layer less); UMAMD_SYNCBN_LOCAL=1 keeps the per-rank sums
-            if _SYNCBN_LOCAL:
-                local = slots_b.clone()  # the reduce kernel stored the count after the slots
+            # gradient: the global sums / world -- no copy of this rank's
+            # slots before the in-place all-reduce (one launch per layer
+            # less).  PRECONDITION: the parameter gradients are AVERAGED over
+            # the ranks afterwards (DDP, train.parallel.data_parallel; the
+            # captured step's GradBuckets, RCCL AVG).  Then every rank ends
+            # with mean_r(G / world) = G / world = mean_r(local_r), exactly
+            # torch SyncBatchNorm's per-rank sums averaged by DDP (the
+            # reference, parallel_main.py:156-158).  A caller that SUMS the
+            # ranks' gradients gets G from both forms: also equal; one that
+            # keeps per-rank gradients without any reduction is not supported
             ctx.sync.all_reduce(slots_b)
             bcount, bscale = -1.0, 1.0 / ctx.sync.world
     elif ctx.has_bn:
@@ -802,15 +769,7 @@ def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=
             dgamma = torch.empty(K, dtype=torch.float32, device=dev)
             dbeta = torch.empty(K, dtype=torch.float32, device=dev)
         single = ctx.sync is None or not ctx.sync.collective
-        if single and _FUSED_BN_BWD:
-            # one launch: the reduce kernel's last blocks finish the coefficients
-            fin = torch.empty((query('um_bn_bwd_fin_ws', M, K) // 8,), dtype=torch.float64,
-                              device=dev)
-            call('um_bn_elu_bwd_reduce_coeffs', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K,
-                 ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
-                 ptr(parts), ptr(fin), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dbias),
-                 ptr(k1), ptr(k2), ptr(k3))
-        elif single:
+        if single:
             call('um_bn_elu_bwd_reduce', _ydt(da, y), M, K, P * Q, ptr(da), K, ptr(y), K,
                  ptr(mean), ptr(invstd), ptr(scale), ptr(shift), ptr(add_nc), int(spec.elu),
                  ptr(parts))
@@ -932,8 +891,6 @@ class SkipConvFn(torch.autograd.Function):
         wf_s, wT_s = _pack(weight, Cg, dt, segs=[(fin, 0, skin)])
         wf_f, wT_f = _pack(weight, Cf, dt, segs=[(0, 0, fin)])
         ydt = _ydtype(dt)
-        if ydt == torch.float16:  # the upsample pass into y has no f16 path
-            ydt = torch.float32
         z = _conv_fwd(gs, wf_s, None, K, 1, 1, 0, L.PAD_ZERO, out_dtype=ydt, creal=skin)
 
         def yconv(epi, stats, cbias):
@@ -1506,11 +1463,6 @@ def concat(sources: Sequence[CatSource], N, H, W, dtype):
 _SPLIT_HEAD = os.environ.get('UMAMD_SPLIT_HEAD', '1') == '1'
 
 
-# the 4-output heads as VALU kernels (csrc/head.hip: f32 weights, no
-# packing, no MFMA padding columns); UMAMD_VALU_HEAD=0 keeps the GEMM path
-_VALU_HEAD = os.environ.get('UMAMD_VALU_HEAD', '0') == '1'
-
-
 class DispHeadFn(torch.autograd.Function):
     """disp = scale * sigmoid(Conv3x3reflect(x)) (reference
     model/layers/decoder.py:244-247), all 4 channels."""
@@ -1521,19 +1473,6 @@ class DispHeadFn(torch.autograd.Function):
         K, Creal, R, _ = weight.shape
         Kp = ceil8(K)
         bias_f = bias.detach().float().contiguous()
-        valu = _VALU_HEAD and K == 4 and R == 3 and Cp % 32 == 0 and H >= 2 and W >= 2 \
-            and x.stride(-1) == 1
-        ctx.valu = valu
-        if valu:
-            w32 = weight.detach().float().contiguous()
-            d = torch.empty((N, H, W, K), dtype=torch.float32, device=x.device)
-            call('um_head_fwd', _dt(x), N, H, W, Creal, Cp, x.stride(2), ptr(x), ptr(w32),
-                 ptr(bias_f), float(scale), ptr(d), work=_conv_flops(N, H, W, K, R, Creal))
-            ctx.scale, ctx.split = float(scale), False
-            _use(ctx, x)
-            ctx.save_for_backward(x, w32, d)
-            ctx.geom = (K, Kp, Creal, R)
-            return d
         split = _SPLIT_HEAD and x.dtype == torch.bfloat16 and 2 * K <= Kp
         if split:
             wf, wT = _pack(weight, Cp, x.dtype, ldT=Kp, split=True)
@@ -1567,49 +1506,15 @@ class DispHeadFn(torch.autograd.Function):
         # over the split rows of wT sums dl (w_hi + w_lo)
         call('um_sigmoid_scale_bwd_split' if ctx.split else 'um_sigmoid_scale_bwd', _dt(dl), M,
              K, ptr(d), K, ptr(dd), dd.shape[-1], ctx.scale, ptr(dl), Kp)
-        if ctx.valu:
-            dW, db = _head_wgrad(x, dl, Kp, Creal)
-        else:
-            dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)  # rows K.. unused
-            db = _colsum_grad(dl, Kp)[:K]  # channels K..Kp of dl are zero or a copy
+        dW = _conv_wgrad(x, dl, Kp, K, Creal, R, 1, 1, L.PAD_REFLECT)  # rows K.. unused
+        db = _colsum_grad(dl, Kp)[:K]  # channels K..Kp of dl are zero or a copy
         dx = None
-        if ctx.needs_input_grad[0] and ctx.valu:
-            tgt = _slot(ctx, 0)
-            dxt = tgt if tgt is not None else torch.empty_like(x)
-            call('um_head_dgrad', _dt(x), N, H, W, Creal, Cp, ptr(dl), Kp, ptr(wT), ptr(dxt),
-                 dxt.stride(2), int(tgt is not None),
-                 work=_conv_flops(N, H, W, K, R, Creal))
-            dx = _give(ctx, 0, dxt)
-        elif ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0]:
             tgt = _slot(ctx, 0)
             dx = _give(ctx, 0, _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT,
                                            dx=tgt, accumulate=tgt is not None, creal=Creal,
                                            kreal=K))
         return dx, dW, db, None
-
-
-def _head_wgrad(x, dl, ldl, Creal):
-    """The head's weight and bias gradients in one VALU launch
-    (um_head_wgrad) into one zeroed f32 buffer [4*Creal*9 + 4] (dW, db views):
-    under overlap.WgradStream it is queued on the weight-gradient side stream
-    like the conv weight gradients (by address: see _conv_wgrad)."""
-    N, H, W, _ = x.shape
-    n = 4 * Creal * 9
-    buf = torch.zeros((n + 4,), dtype=torch.float32, device=x.device)
-    dW, db = buf[:n].view(4, Creal, 3, 3), buf[n:]
-    bp = buf.data_ptr()
-    args = (_dt(x), N, H, W, Creal, x.stride(2), x.data_ptr(), dl.data_ptr(), ldl, bp, bp + 4 * n)
-
-    def launch():
-        call('um_head_wgrad', *args, work=_conv_flops(N, H, W, 4, 3, Creal))
-    ov = _overlap.active()
-    if ov is None:
-        launch()
-    else:
-        buf.record_stream(ov.stream)
-        ov.defer((x, dl), launch, out_ptr=bp, flop=_conv_flops(N, H, W, 4, 3, Creal),
-                 out_bytes=4 * (n + 4))
-    return dW, db
 
 
 def disp_head(x, conv, scale):

@@ -165,7 +165,7 @@ class GradBuckets:
         torch.cat([g.reshape(-1) for g in grads], out=dst)
 
     def _reduce(self, dst):
-        c = _rccl.active(self.group, 'grad')  # the captured step's own communicator
+        c = _rccl.active(self.group)  # the captured step's own communicator
         if c is not None:
             c.all_reduce(dst, average=True)
         elif dist.get_backend(self.group) == 'nccl':

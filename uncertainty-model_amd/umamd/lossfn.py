@@ -36,28 +36,6 @@ LOSS_TYPES = {'l1': 0, 'bayesian': 1, 'log_bayesian': 2}
 MAX_LEVELS = 6
 
 _defer = [False]
-# (stream, events) while forward_on_side_stream is active
-_side = [None, None]
-
-
-@contextlib.contextmanager
-def forward_on_side_stream(stream, events: list):
-    """Inside this context TukraLossFn's forward kernel -- the loss VALUES,
-    which no gradient needs -- runs on ``stream`` (after it waits for the
-    current stream), so it overlaps the backward pass that follows on the
-    current stream: um_loss_bwd re-derives everything it needs.  The caller
-    joins ``stream`` back before anything reads the losses (train.graph's
-    captured step, which also backpropagates with explicit unit gradients
-    instead of reading the values in a sum).  ``events``: the fork/join
-    events, kept alive by the caller (overlap.stream_wait)."""
-    prev = list(_side)
-    _side[0], _side[1] = stream, events
-    try:
-        yield stream
-    finally:
-        _side[0], _side[1] = prev
-
-
 @contextlib.contextmanager
 def deferred_recon():
     """Inside this context ``reconstruct_pyramid`` only allocates its outputs
@@ -267,16 +245,7 @@ class TukraLossFn(torch.autograd.Function):
                  cfg['w_smooth'], cfg['w_err'], ptr(ws), ptr(emap), rarr, ptr(out))
             dl.copy_(out[0])
             el.copy_(out[1])
-        side, events = _side
-        if side is None:
-            launch()
-        else:
-            from .overlap import stream_wait
-            stream_wait(side, torch.cuda.current_stream(), events)
-            for t in (ws, emap, out, dl, el, *preds, *pyr, *(recon_out or ())):
-                t.record_stream(side)
-            with torch.cuda.stream(side):
-                launch()
+        launch()
         ctx.cfg = cfg
         ctx.n = n
         ctx.geom = (N, H, W)

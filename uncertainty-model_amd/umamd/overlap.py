@@ -106,11 +106,11 @@ class WgradStream:
             keep, descs = [], []
             for _, launch in self._pending:
                 # a batched piece returns (what it must keep alive, descriptor):
-                # conv weight gradients (slabs, um_wred_desc), merge weights
-                # (partial sums, um_mwg_desc), biases (partial rows, um_csum_desc)
+                # merge weights (partial sums, um_mwg_desc), biases (partial
+                # rows, um_csum_desc)
                 r = launch()
                 if isinstance(r, tuple) and len(r) == 2 and \
-                        isinstance(r[1], (L.WredDesc, L.MwgDesc, F._Csum)):
+                        isinstance(r[1], (L.MwgDesc, F._Csum)):
                     keep.append(r[0])
                     descs.append(r[1])
             if descs:

@@ -1,5 +1,5 @@
 """The captured step's own RCCL communicator (SyncBN statistics and the
-bucketed gradient all-reduce), called on the launch stream itself.
+bucketed gradient all-reduce), called on the issuing stream itself.
 
 The reference's data-parallel step goes through torch's process group
 (parallel_main.py:156-158: SyncBatchNorm + DDP on 'nccl').  Inside a HIP graph
@@ -16,19 +16,39 @@ that has two costs on MI355X:
     (two event edges per collective in the graph: 80 SyncBN all-reduces and
     the gradient buckets per step).
 
-So the captured step opens its own RCCL communicators over the process
-group's ranks (one per issuing stream, see ``TAGS``; the unique ids travel
-over the group once, eagerly) and calls ``ncclAllReduce``
-through ctypes on the caller's current stream: no watchdog, no stream hop, and
-the eager warm-up steps use the same communicator (its lazy connection setup
-happens there, never inside a capture).  The library is the RCCL torch itself
-loaded (torch/lib/librccl.so), so there is one RCCL in the process.
+So the captured step opens ONE RCCL communicator over the process group's
+ranks (the unique id travels over the group once, eagerly) and calls
+``ncclAllReduce`` through ctypes on the caller's current stream: no watchdog,
+no stream hop, and the eager warm-up steps use the same communicator (its lazy
+connection setup happens there, never inside a capture).  The library is the
+RCCL torch itself loaded (torch/lib/librccl.so), so there is one RCCL in the
+process.
+
+Ordering (safe by construction).  Collectives are issued from two streams:
+SyncBN's on the launch stream, the gradient buckets' on their communication
+stream (umamd.gradsync).  Every collective of the communicator is chained
+after the previous one, whatever stream issued it: when the issuing stream
+changes, the new stream first waits for an event recorded on the previous
+one (``Comm._order``).  So the collectives run one at a time, in the host's
+issue order, which is the same on every rank (the same program: SyncBN in
+forward / autograd order, buckets from the deterministic post-accumulate-grad
+hooks and side-stream flushes) -- the order torch's process group gets from
+its single internal stream, without its watchdog.  Two communicators driven
+concurrently from two streams (round 4) had no such order: nothing stopped
+rank 0 from starting a bucket's all-reduce while rank 1 started a SyncBN one,
+the classic multi-communicator deadlock.  ``tests/test_ddp_cpu.py`` checks
+the chain and the identical sequence on two gloo ranks with a recording
+stand-in.
+
+Lifetime: ``acquire`` counts the captured steps that use a group's
+communicator, ``release`` (CapturedTrainStep.close) destroys it
+(``ncclCommDestroy``) when the last one lets go.
 """
 from __future__ import annotations
 
 import ctypes
 import os
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import torch
 from torch import distributed as dist
@@ -58,6 +78,7 @@ def _rccl() -> ctypes.CDLL:
         lib.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                       ctypes.c_void_p]
+        lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
         lib.ncclGetErrorString.restype = ctypes.c_char_p
         lib.ncclGetErrorString.argtypes = [ctypes.c_int]
         _lib = lib
@@ -70,6 +91,48 @@ def _check(rc: int, what: str):
         raise RuntimeError(f'umamd.rccl: {what} failed ({rc}): {msg}')
 
 
+class _Order:
+    """The total order of one communicator's collectives across issuing
+    streams (see the module docstring).  ``before(stream)`` is called before
+    each collective: if the previous collective came from another stream,
+    ``stream`` waits for an event recorded on that one now (which follows
+    the previous collective in its stream order).  Events stay referenced
+    until ``reset`` (the start of the next step): under graph capture an event
+    destroyed and re-created at the same address mid-capture attaches a later
+    wait to the wrong record (umamd.overlap.stream_wait)."""
+
+    def __init__(self, record=None, wait=None):
+        self.last = None          # the stream of the previous collective
+        self.events: List = []
+        self.log: List = []       # ('wait', dst, src) / ('coll', stream) for tests
+        self._record = record or _cuda_record
+        self._wait = wait or _cuda_wait
+
+    def reset(self):
+        self.last = None
+        self.events = []
+        self.log = []
+
+    def before(self, stream):
+        if self.last is not None and self.last != stream:
+            ev = self._record(self.last)
+            self._wait(stream, ev)
+            self.events.append(ev)
+            self.log.append(('wait', stream, self.last))
+        self.log.append(('coll', stream))
+        self.last = stream
+
+
+def _cuda_record(stream):
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    return ev
+
+
+def _cuda_wait(stream, ev):
+    stream.wait_event(ev)
+
+
 class Comm:
     """An RCCL communicator over the ranks of a 'nccl' process group."""
 
@@ -78,6 +141,7 @@ class Comm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.ranks = dist.get_process_group_ranks(group)
+        self.order = _Order()
         lib = _rccl()
         uid = _UniqueId()
         if self.rank == 0:
@@ -92,74 +156,100 @@ class Comm:
 
     def all_reduce(self, t: torch.Tensor, average: bool = False):
         """In-place sum (or average) of ``t`` over the ranks, on the current
-        stream (recorded as a graph node when that stream is capturing)."""
+        stream (recorded as a graph node when that stream is capturing),
+        ordered after this communicator's previous collective."""
+        if self.comm is None:
+            raise RuntimeError('umamd.rccl.all_reduce: communicator destroyed')
         if not t.is_contiguous():
             raise ValueError('umamd.rccl.all_reduce: contiguous tensor expected')
         dt = _DTYPES.get(t.dtype)
         if dt is None:
             raise TypeError(f'umamd.rccl.all_reduce: dtype {t.dtype}')
-        stream = torch.cuda.current_stream(t.device).cuda_stream
+        cur = torch.cuda.current_stream(t.device)
+        self.order.before(cur)
         _check(_rccl().ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), dt,
-                                     _AVG if average else _SUM, self.comm, stream),
+                                     _AVG if average else _SUM, self.comm, cur.cuda_stream),
                'ncclAllReduce')
 
-
-_comms: Dict[tuple, Comm] = {}
-
-# the communicators of one captured step, one per stream that issues
-# collectives: SyncBN's statistics on the launch stream, the gradient buckets
-# on their communication stream.  One communicator must not be driven from
-# two streams at once: its collectives then run concurrently on its one set of
-# channels and corrupt each other (measured on MI355X with one communicator:
-# gradients of buckets all-reduced during the backward, beside the SyncBN
-# all-reduces, came out wrong)
-TAGS = ('bn', 'grad')
+    def close(self):
+        """ncclCommDestroy (after the device has finished every collective
+        of this communicator; graphs that recorded them must be gone)."""
+        if self.comm is not None:
+            torch.cuda.synchronize()
+            _check(_rccl().ncclCommDestroy(self.comm), 'ncclCommDestroy')
+            self.comm = None
+        self.order.reset()
 
 
-def comm_for(group, tag: str) -> Comm:
-    """The process's communicator ``tag`` for ``group`` (created on first
-    use; every rank of the group must call this at the same point)."""
-    key = (id(group), tag)
-    c = _comms.get(key)
-    if c is None or c.group is not group:
-        c = _comms[key] = Comm(group)
-    return c
+# group key -> [Comm, users]
+_comms: Dict[int, list] = {}
 
 
-def comms_for(group) -> Dict[str, Comm]:
-    return {t: comm_for(group, t) for t in TAGS}
+def _key(group):
+    return id(group)
 
 
-_active: Optional[Dict[str, Comm]] = None
+def acquire(group) -> Comm:
+    """The process's communicator for ``group`` (created on first use; every
+    rank of the group must call this at the same point), one user more."""
+    e = _comms.get(_key(group))
+    if e is None or e[0].group is not group or e[0].comm is None:
+        e = _comms[_key(group)] = [Comm(group), 0]
+    e[1] += 1
+    return e[0]
+
+
+def release(comm: Optional[Comm]):
+    """One user less; the last one destroys the communicator (every rank
+    releases at the same point, as it acquired)."""
+    if comm is None:
+        return
+    for k, e in list(_comms.items()):
+        if e[0] is comm:
+            e[1] -= 1
+            if e[1] <= 0:
+                del _comms[k]
+                comm.close()
+            return
+    comm.close()
+
+
+_active: Optional[Comm] = None
 
 
 class use:
     """Within this context, umamd's collectives on a 'nccl' group go through
-    these communicators instead of the process group (BNSync: ``'bn'``,
-    GradBuckets: ``'grad'``)."""
+    this communicator instead of the process group (BNSync, GradBuckets).
+    Entering starts a new collective chain (the previous step's collectives
+    were joined into the launch stream at its end)."""
 
-    def __init__(self, comms: Optional[Dict[str, Comm]]):
-        self.comms = comms
+    def __init__(self, comm: Optional[Comm]):
+        self.comm = comm
         self.prev = None
 
     def __enter__(self):
         global _active
-        self.prev, _active = _active, self.comms
-        return self.comms
+        self.prev, _active = _active, self.comm
+        if self.comm is not None:
+            self.comm.order.reset()
+        return self.comm
 
     def __exit__(self, *exc):
         global _active
         _active = self.prev
 
 
-def active(group, tag: str) -> Optional[Comm]:
-    """The communicator to use for a collective ``tag`` over ``group`` (None:
-    use the process group): the active one when it spans the same ranks."""
-    if _active is None or group is None:
-        return None
-    c = _active.get(tag)
-    if c is None:
+def active(group) -> Optional[Comm]:
+    """The communicator for a collective over ``group`` (None: no step
+    communicator is active, use the process group).  Raises when one is
+    active but spans other ranks: a collective of the captured step must
+    not fall back to the process group inside a capture (its watchdog
+    aborts the process, see the module docstring)."""
+    c = _active
+    if c is None or group is None:
         return None
     if group is c.group or dist.get_process_group_ranks(group) == c.ranks:
         return c
-    return None
+    raise RuntimeError('umamd.rccl: a collective over a group other than the captured '
+                       "step's (SyncBatchNorm process_group differs from DDP's) is not "
+                       'supported in the captured step')
