@@ -382,6 +382,112 @@ def gen_traj_bf16(ref_model, ref_loss, ref_utils, cfg, steps=10, b=8, h=256, w=5
     save('traj_c2_bf16.npz', **arrays)
 
 
+def disp_bf16_stats(got, ref):
+    """(max-abs/max-ref, mean relative) of a disparity/uncertainty map
+    against its fp32 counterpart; the same formulas as the GPU tests"""
+    g, r = got.double(), ref.double()
+    mx = float((g - r).abs().max() / r.abs().max())
+    mr = float(((g - r).abs() / r.abs().clamp_min(1e-6)).mean())
+    return mx, mr
+
+
+def gen_disp_bf16(ref_model, cfg, b=8, h=256, w=512):
+    """The reference's OWN bf16 disparity deviation at BASELINE config 2
+    (B=8, 256x512, formula weights, the bench's synthetic pair, scale 0.3,
+    train-mode forward): the model run in fp32 and under
+    torch.autocast('cpu', torch.bfloat16), compared per scale by
+    max-abs/max-ref and mean relative error (disp_bf16_stats).  Stores the
+    per-scale figures, the fp32 and bf16 maps of the coarsest scale
+    (8x4x32x64) and the per-scale sums of the fp32 maps.  The GPU test holds
+    our bf16 build to max(BASELINE.md's bar, 1.1 x these figures)."""
+    sys.path.insert(0, REPO)
+    from oracle import step as OS  # noqa: E402
+    sd, _ = _formula_weights(cfg)
+    m = _ref_model(ref_model, cfg)
+    m.load_state_dict(sd)
+    m.train()
+    left, _ = OS.bench_inputs(b, h, w)
+    arrays = {'shape': np.array([b, h, w]), 'seed': np.int64(1234), 'scale': np.float64(0.3)}
+    with torch.no_grad():
+        d32 = [d.clone() for d in m(left, 0.3)]
+        m.load_state_dict(sd)  # the same running statistics before the second forward
+        with torch.autocast('cpu', dtype=torch.bfloat16):
+            d16 = [d.float().clone() for d in m(left, 0.3)]
+    for i, (a, r) in enumerate(zip(d16, d32)):
+        mx, mr = disp_bf16_stats(a, r)
+        arrays[f'max_rel_{i}'] = np.float64(mx)
+        arrays[f'mean_rel_{i}'] = np.float64(mr)
+        arrays[f'fp32_sum_{i}'] = r.double().sum()
+        arrays[f'fp32_abssum_{i}'] = r.double().abs().sum()
+        print(f'disp bf16 scale {i} {tuple(r.shape)}: max-abs/max-ref {mx:.3e}, '
+              f'mean rel {mr:.3e}', flush=True)
+    arrays['fp32_d3'] = d32[3]
+    arrays['bf16_d3'] = d16[3]
+    # the same figures on tests/test_gpu_model.py's U[0,1) pair (B=2, 64x128,
+    # torch.Generator seed 1234, the left view), the input of its bf16 test
+    g = torch.Generator().manual_seed(1234)
+    left64 = torch.rand(2, 3, 64, 128, generator=g)
+    with torch.no_grad():
+        m.load_state_dict(sd)
+        u32 = [d.clone() for d in m(left64, 0.3)]
+        m.load_state_dict(sd)
+        with torch.autocast('cpu', dtype=torch.bfloat16):
+            u16 = [d.float().clone() for d in m(left64, 0.3)]
+    for i, (a, r) in enumerate(zip(u16, u32)):
+        mx, mr = disp_bf16_stats(a, r)
+        arrays[f'u64_max_rel_{i}'] = np.float64(mx)
+        arrays[f'u64_mean_rel_{i}'] = np.float64(mr)
+        print(f'disp bf16 U[0,1) 64x128 scale {i}: max-abs/max-ref {mx:.3e}, mean rel {mr:.3e}',
+              flush=True)
+    save('disp_c2_bf16.npz', **arrays)
+
+
+def uniform_pair(b, h, w, seed):
+    """tests/test_gpu_model.py's _uniform_pair: U[0,1) left and right views"""
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(b, 3, h, w, generator=g), torch.rand(b, 3, h, w, generator=g)
+
+
+LOSS_BF16_CASES = {  # tag: (config, batch, height, width, seeds)
+    'u64': ('config.yml', 2, 64, 128, (99, 100, 101, 102, 103, 104, 105, 106)),
+    'c2u': ('config.yml', 8, 256, 512, (99,)),
+    'c5u': ('config_nodes10.yml', 8, 512, 1024, (5,)),
+}
+
+
+def gen_loss_bf16(ref_model, ref_loss, ref_utils):
+    """The reference's OWN bf16-autocast deviation of the step-0 loss
+    scalars (forward + loss, formula weights, bayesian, scale 0.3) on the
+    U[0,1) inputs of the GPU tests' bf16 loss checks: per case and seed the
+    fp32 and torch.autocast('cpu', bf16) disparity / error losses.  The
+    nodes=10 graphs (config 5) run forward only, which the reference can do
+    (its in-place output sum breaks only the backward)."""
+    arrays = {}
+    for tag, (cname, b, h, w, seeds) in LOSS_BF16_CASES.items():
+        with open(os.path.join(REPO, cname)) as f:
+            cfg = yaml.safe_load(f)
+        sd, _ = _formula_weights(cfg)
+        m = _ref_model(ref_model, cfg)
+        m.train()
+        lcfg = json.loads(json.dumps(cfg['loss']))
+        lcfg['error_loss_config']['loss_type'] = 'bayesian'
+        lf = ref_loss.TukraUncertaintyLoss(**lcfg)
+        for seed in seeds:
+            left, right = uniform_pair(b, h, w, seed)
+            for mode in ('fp32', 'bf16'):
+                m.load_state_dict(sd)
+                with torch.no_grad(), torch.autocast('cpu', dtype=torch.bfloat16,
+                                                     enabled=mode == 'bf16'):
+                    pyr = ref_utils.scale_pyramid(torch.cat([left, right], 1), 4)
+                    d = m(left, 0.3)
+                    dl, el = lf(pyr, d, ref_utils.reconstruct_pyramid(d, pyr), 0, None)
+                arrays[f'{tag}_{seed}_{mode}'] = np.array([float(dl), float(el)])
+            a, r = arrays[f'{tag}_{seed}_bf16'], arrays[f'{tag}_{seed}_fp32']
+            print(f'loss bf16 {tag} seed {seed}: rel disp {abs(a[0] / r[0] - 1):.3e} '
+                  f'error {abs(a[1] / r[1] - 1):.3e}', flush=True)
+    save('loss_bf16.npz', **arrays)
+
+
 def train_model_pairs():
     """7 smooth stereo pairs at 64x128 (a ragged last batch at batch 2)"""
     left, right, _ = stereo_pair(7, 64, 128, seed=2468)
@@ -618,6 +724,10 @@ def main():
         gen_traj(ref_model, ref_loss, ref_utils, cfg)
     if 'traj_bf16' in which:  # the reference's own bf16-autocast deviation at config 2
         gen_traj_bf16(ref_model, ref_loss, ref_utils, cfg)
+    if 'loss_bf16' in which:  # the reference's own bf16-autocast loss deviations
+        gen_loss_bf16(ref_model, ref_loss, ref_utils)
+    if 'disp_bf16' in which:  # the reference's own bf16-autocast disparity deviation at C2
+        gen_disp_bf16(ref_model, cfg)
     if 'train_model' in which:  # the reference's epoch loop (ragged batch, scale change)
         gen_train_model(ref_model, ref_loss, ref_utils, cfg)
     if 'c1' in which:  # BASELINE config 1: 128x256, batch 2, l1 error loss, one step

@@ -2,7 +2,9 @@
 fixtures generated from the reference (tests/golden/make_goldens.py).
 Tolerances: fp32 build vs reference 1e-3 rel on disparity/uncertainty and
 loss scalars (measured noise ~1e-5); bf16 build: loss scalars
-<= 1e-2 rel, disparity max-abs/max-ref <= 5e-2."""
+within max(2e-3, 1.1 x the reference's own bf16-autocast deviation on the
+same input; loss_bf16.npz), disparities within max(BASELINE.md's bar, 1.1 x the reference's
+own bf16-autocast deviation on the same input; disp_c2_bf16.npz)."""
 import json
 import os
 
@@ -80,12 +82,28 @@ def _uniform_pair(b=2, h=64, w=128, seed=1234):
     return torch.rand(b, 3, h, w, generator=g), torch.rand(b, 3, h, w, generator=g)
 
 
+def disp_bf16_bar(z, prefix=''):
+    """per-scale bars for bf16 disparities: max(BASELINE.md's bar -- ~1e-2
+    mean relative, 3e-2 max-abs/max-ref --, 1.1 x the reference's OWN
+    bf16-autocast deviation on the same input, tests/golden/disp_c2_bf16.npz)"""
+    return [(max(3e-2, 1.1 * float(z[f'{prefix}max_rel_{i}'])),
+             max(1e-2, 1.1 * float(z[f'{prefix}mean_rel_{i}']))) for i in range(4)]
+
+
+def disp_stats(got, ref):
+    """(max-abs/max-ref, mean relative) as make_goldens.disp_bf16_stats"""
+    g, r = got.double(), ref.double()
+    return (float((g - r).abs().max() / r.abs().max()),
+            float(((g - r).abs() / r.abs().clamp_min(1e-6)).mean()))
+
+
 def test_model_forward_bf16():
-    """bf16 build vs fp32 build on U[0,1) pairs (the benchmark's data; SURVEY
-    F8 measured the reference under bf16 autocast at ~1e-2 mean / 2.6e-2 max
-    relative).  On very smooth inputs BN amplifies bf16 operand rounding by
-    mean/std of the first conv (~17 on the golden textures): measured 4e-2 at
-    the first node on the CPU oracle with bf16-rounded operands too."""
+    """bf16 build vs fp32 build on a U[0,1) pair (B=2, 64x128): every scale
+    within max(BASELINE.md's bar, 1.1 x the reference's own bf16-autocast
+    deviation on this same input) -- disp_c2_bf16.npz u64_*: 3.8-5.2e-2
+    max-abs/max-ref, 1.5-2.1e-2 mean relative."""
+    z = _z('disp_c2_bf16.npz')
+    bar = disp_bf16_bar(z, 'u64_')
     left, _ = _uniform_pair()
     left = left.to(DEV)
     m32 = _model(_cfg()).train()
@@ -96,13 +114,11 @@ def test_model_forward_bf16():
     errs = []
     for i in range(4):
         assert d16[i].dtype == torch.float32
-        ref = d32[i].double()
-        got = d16[i].double()
-        mean_rel = float(((got - ref).abs() / ref.abs().clamp_min(1e-6)).mean())
-        errs.append((i, float((got - ref).abs().max() / ref.abs().max()), mean_rel))
-    print('bf16 vs fp32 disparity errors (scale, max-abs/max-ref, mean rel):', errs)
-    for i, mx, mr in errs:
-        assert mx < 0.1 and mr < 2e-2, errs
+        errs.append(disp_stats(d16[i], d32[i]))
+    print('bf16 vs fp32 disparity (max-abs/max-ref, mean rel) per scale:', errs)
+    print('bars:', bar)
+    for i in range(4):
+        assert errs[i][0] <= bar[i][0] and errs[i][1] <= bar[i][1], (i, errs[i], bar[i])
 
 
 def test_nodes10_forward():
@@ -241,28 +257,65 @@ def test_train_step_fp32(lt):
                     assert abs(got - float(z[k])) <= 1e-4 * float(z['param_abs/' + name]) + flips, name
 
 
+def loss_bf16_bar(tag, seed, z=None):
+    """(disp, error) bars for a bf16 step-0 loss delta on a loss_bf16.npz
+    case: max(2e-3 -- BASELINE.md's 1e-3 with the margin of the measured
+    config-2 error loss, DESIGN.md 2 --, 1.1 x the reference's OWN
+    bf16-autocast deviation on the same input)"""
+    z = z if z is not None else _z('loss_bf16.npz')
+    a, r = z[f'{tag}_{seed}_bf16'], z[f'{tag}_{seed}_fp32']
+    return tuple(max(2e-3, 1.1 * abs(float(a[j]) / float(r[j]) - 1)) for j in range(2))
+
+
 def test_train_step_bf16_loss_delta():
+    """bf16 vs fp32 step-0 losses on eight U[0,1) pairs (B=2, 64x128,
+    seeds 99..106).  The disparity loss is held per seed to
+    max(2e-3, 1.1 x the reference's own bf16-autocast deviation on that
+    seed) (loss_bf16.npz).  The error loss (Laplacian NLL) at this size
+    has a bf16 noise floor of ~1e-2: the reference's own autocast moves it
+    by 2.9e-3..2.7e-2 across these seeds, and running any ONE of our five
+    encoder stages in f32 moves ours by 5e-3..1.8e-2 (tools/bf16_localize.py,
+    DESIGN.md 2), so it is held to the same bar on the RMS over the seeds
+    and per seed to the reference's worst.  The first seed also runs the
+    backward (finite gradients)."""
+    import math
     import train.utils as u
     from train.loss import TukraUncertaintyLoss
+    z = _z('loss_bf16.npz')
+    seeds = sorted(int(k.split('_')[1]) for k in z.files
+                   if k.startswith('u64_') and k.endswith('_fp32'))
     cfg = _cfg()
     cfg['loss']['error_loss_config']['loss_type'] = 'bayesian'
-    left, right = [t.to(DEV) for t in _uniform_pair(seed=99)]
-    pyr = u.scale_pyramid(torch.cat([left, right], 1), 4)
-    res = {}
-    for dt in ('fp32', 'bf16'):
-        m = _model(cfg, dt).train()
-        lf = TukraUncertaintyLoss(**cfg['loss'])
-        d = m(left, 0.3)
-        dl, el = lf(pyr, d, u.reconstruct_pyramid(d, pyr), 0, None)
-        (dl + el).backward()
-        for k, p in m.named_parameters():
-            assert torch.isfinite(p.grad).all(), k
-        res[dt] = (float(dl), float(el))
-    print('bf16 loss delta:', res)
-    # disparity loss: 1e-2.  Bayesian NLL mean(e/sigma + log sigma) inherits the
-    # ~1.3e-2 mean relative sigma deviation of bf16 operands (measured 1.6e-2)
-    assert abs(res['bf16'][0] / res['fp32'][0] - 1) < 1e-2
-    assert abs(res['bf16'][1] / res['fp32'][1] - 1) < 3e-2
+    ours, refs = [], []
+    for i, seed in enumerate(seeds):
+        left, right = [t.to(DEV) for t in _uniform_pair(seed=seed)]
+        pyr = u.scale_pyramid(torch.cat([left, right], 1), 4)
+        res = {}
+        for dt in ('fp32', 'bf16'):
+            m = _model(cfg, dt).train()
+            lf = TukraUncertaintyLoss(**cfg['loss'])
+            d = m(left, 0.3)
+            dl, el = lf(pyr, d, u.reconstruct_pyramid(d, pyr), 0, None)
+            if i == 0:
+                m.zero_grad()
+                (dl + el).backward()
+                for k, p in m.named_parameters():
+                    assert torch.isfinite(p.grad).all(), k
+            res[dt] = (float(dl), float(el))
+        dev = [abs(res['bf16'][j] / res['fp32'][j] - 1) for j in range(2)]
+        a, r = z[f'u64_{seed}_bf16'], z[f'u64_{seed}_fp32']
+        rdev = [abs(float(a[j]) / float(r[j]) - 1) for j in range(2)]
+        ours.append(dev)
+        refs.append(rdev)
+        print(f'seed {seed}: ours disp {dev[0]:.2e} err {dev[1]:.2e} | '
+              f'reference autocast disp {rdev[0]:.2e} err {rdev[1]:.2e}')
+        assert dev[0] <= loss_bf16_bar('u64', seed, z)[0], (seed, dev, rdev)
+    rms = lambda v: math.sqrt(sum(x * x for x in v) / len(v))  # noqa: E731
+    ours_e, refs_e = [o[1] for o in ours], [r[1] for r in refs]
+    print(f'error-loss deviation RMS: ours {rms(ours_e):.3e}, reference autocast '
+          f'{rms(refs_e):.3e}')
+    assert rms(ours_e) <= max(2e-3, 1.1 * rms(refs_e)), (ours_e, refs_e)
+    assert max(ours_e) <= max(2e-3, 1.1 * max(refs_e)), (ours_e, refs_e)
 
 
 @pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
@@ -355,8 +408,9 @@ def test_train_step_config1_l1():
 def test_train_step_config2_bf16_properties():
     """BASELINE config 2 shape (B=8, 256x512, bayesian, bf16): the captured
     step's losses and gradients are finite, and the bf16 loss scalars agree
-    with an fp32 step from the same weights within the bf16 bar (SURVEY F8:
-    <= 1e-2 disp, 3e-2 error relative)."""
+    with an fp32 step from the same weights within max(2e-3, 1.1 x the
+    reference's own bf16-autocast deviation on this input: loss_bf16.npz
+    c2u, 1.3e-3 / 2.1e-3)."""
     import train.utils as u
     from train.loss import TukraUncertaintyLoss
     from train.train import train_step
@@ -380,7 +434,9 @@ def test_train_step_config2_bf16_properties():
             assert p.grad is not None and torch.isfinite(p.grad).all(), k
         losses.append((float(dl), float(el)))
     (d16, e16), (d32, e32) = losses
-    assert abs(d16 / d32 - 1) < 1e-2 and abs(e16 / e32 - 1) < 3e-2, losses
+    bd, be = loss_bf16_bar('c2u', 99)
+    print('config 2 bf16 step-0 loss deltas', abs(d16 / d32 - 1), abs(e16 / e32 - 1), (bd, be))
+    assert abs(d16 / d32 - 1) <= bd and abs(e16 / e32 - 1) <= be, (losses, bd, be)
 
 
 def test_nodes10_train_step_matches_oracle():
@@ -423,7 +479,9 @@ def test_config5_nodes10_512x1024_properties():
     """BASELINE config 5 per-GPU shape (B=8, 512x1024, nodes=10 graphs,
     bayesian, bf16): one training step through the out-of-place GraphBlock
     sum -- finite losses and gradients, and the bf16 loss scalars
-    within the bf16 bar of an fp32 step from the same weights."""
+    within max(2e-3, 1.1 x the reference's own bf16-autocast deviation of
+    the same forward: loss_bf16.npz c5u, 2.0e-3 / 2.1e-4) of an fp32 step
+    from the same weights."""
     from train.loss import TukraUncertaintyLoss
     from train.train import train_step
     from umamd.optim import Adam
@@ -443,4 +501,6 @@ def test_config5_nodes10_512x1024_properties():
             assert p.grad is not None and torch.isfinite(p.grad).all(), k
         losses.append((float(dl), float(el)))
     (d16, e16), (d32, e32) = losses
-    assert abs(d16 / d32 - 1) < 1e-2 and abs(e16 / e32 - 1) < 3e-2, losses
+    bd, be = loss_bf16_bar('c5u', 5)
+    print('config 5 bf16 step-0 loss deltas', abs(d16 / d32 - 1), abs(e16 / e32 - 1), (bd, be))
+    assert abs(d16 / d32 - 1) <= bd and abs(e16 / e32 - 1) <= be, (losses, bd, be)

@@ -171,6 +171,47 @@ def test_config2_trajectory_vs_reference():
         assert worst < 1e-2 and worst <= worst_ref, (j, worst, worst_ref)
 
 
+def test_config2_bf16_disparity_vs_reference():
+    """The bench's bf16 build at BASELINE config 2 (B=8, 256x512, formula
+    weights, the bench's synthetic pair, scale 0.3, train-mode forward):
+    every disparity/uncertainty scale within max(BASELINE.md's bar: 3e-2
+    max-abs/max-ref, 1e-2 mean relative; 1.1 x the reference's OWN
+    bf16-autocast deviation on this input: disp_c2_bf16.npz, 4.1-4.7e-2 /
+    1.2-1.6e-2) of the reference's fp32 disparities.  The fp32 side is our
+    fp32 build, pinned to the reference in the same test: its coarsest scale
+    against the reference's fp32 map (1e-4) and every scale's sum against
+    the reference's (1e-4 of the absolute sum); the coarsest bf16 map is also
+    compared with the reference's fp32 map directly."""
+    from oracle import step as OS
+    from test_gpu_model import disp_bf16_bar, disp_stats
+    z = _z('disp_c2_bf16.npz')
+    bar = disp_bf16_bar(z)
+    b, h, w = (int(v) for v in z['shape'])
+    left, _ = OS.bench_inputs(b, h, w)
+    left = left.to(DEV)
+    cfg = _cfg()
+    m32 = _model(cfg).train()
+    m16 = _model(cfg, 'bf16').train()
+    with torch.no_grad():
+        d32 = m32(left, 0.3)
+        d16 = m16(left, 0.3)
+    ref3 = torch.from_numpy(z['fp32_d3']).to(DEV)
+    pin = disp_stats(d32[3], ref3)[0]
+    assert pin < 1e-4, pin
+    for i in range(4):
+        s = float(d32[i].double().sum())
+        assert abs(s - float(z[f'fp32_sum_{i}'])) <= 1e-4 * float(z[f'fp32_abssum_{i}']), i
+    errs = [disp_stats(d16[i], d32[i]) for i in range(4)]
+    direct = disp_stats(d16[3], ref3)
+    refdev = [(float(z[f'max_rel_{i}']), float(z[f'mean_rel_{i}'])) for i in range(4)]
+    print('bf16 vs reference fp32 (max-abs/max-ref, mean rel) per scale:', errs)
+    print('coarsest scale vs the reference map directly:', direct)
+    print("reference's own bf16 autocast:", refdev)
+    for i in range(4):
+        assert errs[i][0] <= bar[i][0] and errs[i][1] <= bar[i][1], (i, errs[i], bar[i])
+    assert direct[0] <= bar[3][0] and direct[1] <= bar[3][1], (direct, bar[3])
+
+
 def test_train_model_graph_replay_matches_eager(monkeypatch):
     """The drop-in loop (reference train/train.py:173-267 via our
     train.train.train_model): 2 epochs over a 7-pair loader (batch 2: three
