@@ -210,7 +210,11 @@ def test_merge(dtype):
 
 
 @pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 8), (512, 2, 4), (256, 4, 8),
-                                   (32, 20, 30), (128, 12, 16), (64, 40, 72)])
+                                   (32, 20, 30), (128, 12, 16), (64, 40, 72),
+                                   # the MFMA heads (d = 16/32/64) at the encoder's
+                                   # stage 3-5 sizes and at ragged pixel counts
+                                   (128, 32, 64), (256, 16, 32), (512, 8, 16), (256, 9, 13),
+                                   (512, 5, 7), (128, 3, 50)])
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 def test_attention_block(C, H, W, dtype):
     from oracle.model import efficient_attention

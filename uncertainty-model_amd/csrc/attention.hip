@@ -655,6 +655,468 @@ int attn_bwd_small(int dtype, int N, int S, int C, int heads, const void* qkv, i
                                              dqkv, ldq, dks_ws, ws, dctx, r, st);
 }
 
+// ------------------------------------------------ MFMA heads (d = 16..64) --
+// Stages 3-5 of the encoder (C = 128 / 256 / 512, 8 heads: d = 16 / 32 / 64).
+// The d x d products run on v_mfma_f32_16x16x4_f32 from f32 LDS images (f32
+// operands: the fp32 build keeps fp32 arithmetic, and at these sizes the
+// launches are latency-bound, not MFMA-bound), and the passes are fused:
+//   forward : ctx_part_mfma (per pixel chunk: the chunk's own key-softmax
+//             max m_b and sum l_b, and ctx_b = exp(K - m_b)^T V) ->
+//             apply_mfma (every tile workgroup combines the chunk partials,
+//             ctx = sum_b e^(m_b - M) ctx_b / sum_b e^(m_b - M) l_b, in its
+//             prologue; tile 0 publishes kmax = M, ksum, ctx for the
+//             backward; then att = softmax_c(Q) ctx)
+//   backward: apply_bwd_mfma (dQ, dctx partial per tile) -> kv_bwd_mfma
+//             (dctx combined in the prologue; dV, dKs, r partial) ->
+//             k_bwd_mfma (r combined in the prologue; dK)
+// 2 + 3 launches per attention instead of 5 + 5 (kstats, combine, ctx,
+// part sums, apply / apply_bwd, part sums, kv_bwd, part sums, k_bwd).
+constexpr int MCH = 64;        // pixels per chunk / tile
+constexpr int PST = MCH + 16;  // row stride of [channel][pixel] images (floats)
+
+// row stride of [pixel][channel] / [channel][channel] images: 16 banks
+// between consecutive rows, so the two 16-lane halves of a ds_read_b32
+// group read disjoint banks
+template <int D> struct MS { static constexpr int ST = (D % 32 == 0) ? D + 16 : D + 32; };
+
+// acc (one 16x16 block) += A(r, k) B(k, c) over k in [0, K), K % 4 == 0;
+// A(r, k) at a[r * ar + k * ak], B(k, c) at b[k * bk + c * bc].  Lane l
+// feeds A(l % 16, k + l / 16), B(k + l / 16, l % 16) and holds
+// D(4 * (l / 16) + j, l % 16) in acc[j].
+__device__ __forceinline__ void mma16(f32x4_t& acc, const float* a, int ar, int ak,
+                                      const float* b, int bk, int bc, int K) {
+  const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+  for (int k = 0; k < K; k += 4)
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i * ar + (k + kk) * ak],
+                                                b[(k + kk) * bk + i * bc], acc, 0, 0, 0);
+}
+
+// rows [row0, row0 + np) of src (pixel stride ld), channels [col0, col0 + D)
+// -> f32 LDS image, zero rows up to MCH.  T_ = true: transposed image
+// dst[c * PST + s], else dst[s * ST + c]
+template <typename T, int D, bool T_>
+__device__ __forceinline__ void load_img(float* dst, const T* __restrict__ src, long row0, int ld,
+                                         int col0, int np) {
+  constexpr int ST = MS<D>::ST, V = D / 8;
+  for (int i = threadIdx.x; i < MCH * V; i += 256) {
+    const int s = i / V, c = (i - s * V) * 8;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (s < np) load8(src + (row0 + s) * ld + col0 + c, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (T_) dst[(c + e) * PST + s] = v[e];
+      else dst[s * ST + c + e] = v[e];
+    }
+  }
+}
+
+// the wave's share of the (D/16)^2 output blocks of a D x D product, or for
+// D = 16 the whole block over a quarter of the MCH-deep reduction (wave_k)
+template <int D> struct Blocks {
+  static constexpr int NB = (D / 16) * (D / 16);
+  static constexpr int PER = NB >= 4 ? NB / 4 : 1;
+  static constexpr bool KSPLIT = NB < 4;
+};
+
+// D x D product over the MCH pixels (A(c, s), B(s, c')), result written by
+// `put(c, c', v)`; for D = 16 the four waves' k-quarters are summed in red
+// (4 * 256 floats)
+template <int D, typename F>
+__device__ __forceinline__ void dd_product(const float* a, int ar, int ak, const float* b, int bk,
+                                           int bc, float* red, F put) {
+  using B = Blocks<D>;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  f32x4_t acc[B::PER];
+#pragma unroll
+  for (int q = 0; q < B::PER; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  if constexpr (B::KSPLIT) {
+    const int k0 = w * (MCH / 4);
+    mma16(acc[0], a + k0 * ak, ar, ak, b + k0 * bk, bk, bc, MCH / 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[w * 256 + (4 * (lane >> 4) + j) * 16 + (lane & 15)] = acc[0][j];
+    __syncthreads();
+    const int o = threadIdx.x;  // 256 = 16 x 16 outputs
+    put(o >> 4, o & 15, red[o] + red[256 + o] + red[512 + o] + red[768 + o]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < B::PER; ++q) {
+      const int blk = w * B::PER + q, bi = blk / (D / 16), bj = blk % (D / 16);
+      mma16(acc[q], a + 16 * bi * ar, ar, ak, b + 16 * bj * bc, bk, bc, MCH);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) put(16 * bi + 4 * (lane >> 4) + j, 16 * bj + (lane & 15), acc[q][j]);
+    }
+  }
+}
+
+// forward (1): chunk partials [n][h][b] = {m[D], l[D], ctx[D][D]}
+template <typename T, int D>
+__global__ void __launch_bounds__(256) ctx_part_mfma(const T* __restrict__ qkv, int ld, int S,
+                                                     int C, int heads, int nb,
+                                                     float* __restrict__ part) {
+  constexpr int ST = MS<D>::ST, G = 256 / D;
+  __shared__ float sK[MCH * ST], sV[MCH * ST];
+  __shared__ float red[1024];
+  const int b = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int s0 = b * MCH, np = min(MCH, S - s0);
+  const long row0 = (long)n * S + s0;
+  load_img<T, D, false>(sK, qkv, row0, ld, h * D, np);
+  load_img<T, D, false>(sV, qkv, row0, ld, 2 * C + h * D, np);
+  __syncthreads();
+  const int c = threadIdx.x % D, g = threadIdx.x / D;
+  float mx = -INFINITY;
+  for (int s = g; s < np; s += G) mx = fmaxf(mx, sK[s * ST + c]);
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  mx = red[c];
+  for (int q = 1; q < G; ++q) mx = fmaxf(mx, red[q * D + c]);
+  float sum = 0.f;
+  for (int s = g; s < MCH; s += G) {
+    float e = 0.f;
+    if (s < np) {
+      e = __expf(sK[s * ST + c] - mx);
+      sum += e;
+    }
+    sK[s * ST + c] = e;
+  }
+  __syncthreads();  // every thread has read red (the maxima)
+  red[threadIdx.x] = sum;
+  __syncthreads();
+  float* o = part + (((long)n * heads + h) * nb + b) * (D * D + 2 * D);
+  if (g == 0) {
+    for (int q = 1; q < G; ++q) sum += red[q * D + c];
+    o[c] = mx;
+    o[D + c] = sum;
+  }
+  __syncthreads();  // red is reused by the product (D = 16)
+  // ctx_b(c, c') = sum_s sK[s][c] sV[s][c']
+  dd_product<D>(sK, 1, ST, sV, ST, 1, red,
+                [&](int r, int cc, float v) { o[2 * D + r * D + cc] = v; });
+}
+
+// combine the chunk partials of (n, h): M[c], L[c] into sM / sL, and the
+// final ctx (D x D) into dst[c * dst_r + c' * dst_c] (every workgroup of
+// the pair does the same, bit-identically)
+template <int D>
+__device__ __forceinline__ void ctx_combine(const float* __restrict__ p, int nb, float* sM,
+                                            float* sL, float* dst, int dst_r, int dst_c) {
+  const int t = threadIdx.x;
+  if (t < D) {
+    float M = -INFINITY;
+    for (int b = 0; b < nb; ++b) M = fmaxf(M, p[(long)b * (D * D + 2 * D) + t]);
+    float L = 0.f;
+    for (int b = 0; b < nb; ++b) {
+      const float* q = p + (long)b * (D * D + 2 * D);
+      L += __expf(q[t] - M) * q[D + t];
+    }
+    sM[t] = M;
+    sL[t] = L;
+  }
+  __syncthreads();
+  for (int o = t; o < D * D; o += 256) {
+    const int c = o / D, cc = o - c * D;
+    const float M = sM[c];
+    float acc = 0.f;
+    for (int b = 0; b < nb; ++b) {
+      const float* q = p + (long)b * (D * D + 2 * D);
+      acc += __expf(q[c] - M) * q[2 * D + o];
+    }
+    dst[c * dst_r + cc * dst_c] = acc / sL[c];
+  }
+}
+
+// softmax over the D channels of each of the MCH pixels of a transposed
+// image x[c * PST + s] (wave 0: one pixel per lane; the other waves idle)
+template <int D>
+__device__ __forceinline__ void softmax_cols(float* x) {
+  if (threadIdx.x < MCH) {
+    const int s = threadIdx.x;
+    float mx = -INFINITY;
+    for (int c = 0; c < D; ++c) mx = fmaxf(mx, x[c * PST + s]);
+    float sum = 0.f;
+    for (int c = 0; c < D; ++c) {
+      const float e = __expf(x[c * PST + s] - mx);
+      x[c * PST + s] = e;
+      sum += e;
+    }
+    const float inv = 1.f / sum;
+    for (int c = 0; c < D; ++c) x[c * PST + s] *= inv;
+  }
+}
+
+// forward (2): att = softmax_c(Q) ctx per MCH-pixel tile
+template <typename T, int D>
+__global__ void __launch_bounds__(256) apply_mfma(const T* __restrict__ qkv, int ld, int S, int C,
+                                                  int heads, int nb,
+                                                  const float* __restrict__ part,
+                                                  float* __restrict__ kmax,
+                                                  float* __restrict__ ksum,
+                                                  float* __restrict__ ctxg, T* __restrict__ att,
+                                                  int ldo) {
+  constexpr int ST = MS<D>::ST;
+  __shared__ float sC[D * ST], sQt[D * PST];
+  __shared__ float sM[D], sL[D];
+  const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int s0 = tile * MCH, np = min(MCH, S - s0);
+  const long row0 = (long)n * S + s0;
+  load_img<T, D, true>(sQt, qkv, row0, ld, C + h * D, np);
+  ctx_combine<D>(part + ((long)n * heads + h) * nb * (D * D + 2 * D), nb, sM, sL, sC, ST, 1);
+  __syncthreads();
+  if (tile == 0) {  // the backward's kmax / ksum / ctx
+    for (int o = threadIdx.x; o < D * D; o += 256)
+      ctxg[((long)n * heads + h) * D * D + o] = sC[(o / D) * ST + o % D];
+    if (threadIdx.x < D) {
+      kmax[(long)n * C + h * D + threadIdx.x] = sM[threadIdx.x];
+      ksum[(long)n * C + h * D + threadIdx.x] = sL[threadIdx.x];
+    }
+  }
+  softmax_cols<D>(sQt);
+  __syncthreads();
+  // att(s, c') = sum_c Qs(s, c) ctx(c, c'): wave w takes pixel rows 16w..16w+15
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int bj = 0; bj < D / 16; ++bj) {
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    mma16(acc, sQt + 16 * w, 1, PST, sC + 16 * bj, ST, 1, D);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = 16 * w + 4 * (lane >> 4) + j;
+      if (s < np)
+        att[(row0 + s) * ldo + h * D + 16 * bj + (lane & 15)] = from_f32<T>(acc[j]);
+    }
+  }
+}
+
+// backward (1): dQ and the tile's dctx partial ws[n][h][tile][D][D]
+//   dQs(s, c) = sum_c' datt(s, c') ctx(c, c'), dQ = Qs (dQs - <Qs, dQs>_c)
+//   dctx(c, c') = sum_s Qs(s, c) datt(s, c')
+template <typename T, int D>
+__global__ void __launch_bounds__(256) apply_bwd_mfma(const T* __restrict__ qkv, int ld, int S,
+                                                      int C, int heads,
+                                                      const float* __restrict__ ctxg,
+                                                      const T* __restrict__ datt, int ldd,
+                                                      T* __restrict__ dqkv, int ldq, int nt,
+                                                      float* __restrict__ ws) {
+  constexpr int ST = MS<D>::ST;
+  extern __shared__ float sh[];
+  float* sCt = sh;                // ctx^T [c'][c]
+  float* sGt = sCt + D * ST;      // datt^T [c'][s]
+  float* sG = sGt + D * PST;      // datt [s][c']
+  float* sQt = sG + MCH * ST;     // Qs^T [c][s]
+  float* sQ = sQt + D * PST;      // Qs [s][c]
+  float* red = sQ + MCH * ST;     // [1024]
+  const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int s0 = tile * MCH, np = min(MCH, S - s0);
+  const long row0 = (long)n * S + s0;
+  const float* cg = ctxg + ((long)n * heads + h) * D * D;
+  for (int o = threadIdx.x; o < D * D; o += 256) sCt[(o % D) * ST + o / D] = cg[o];
+  load_img<T, D, true>(sGt, datt, row0, ldd, h * D, np);
+  load_img<T, D, false>(sG, datt, row0, ldd, h * D, np);
+  load_img<T, D, true>(sQt, qkv, row0, ld, C + h * D, np);
+  __syncthreads();
+  softmax_cols<D>(sQt);
+  __syncthreads();
+  for (int i = threadIdx.x; i < MCH * D; i += 256) {
+    const int s = i / D, c = i - s * D;
+    sQ[s * ST + c] = s < np ? sQt[c * PST + s] : 0.f;  // pad pixels add nothing to dctx
+  }
+  __syncthreads();
+  // dctx partial
+  float* o = ws + (((long)n * heads + h) * nt + tile) * D * D;
+  dd_product<D>(sQ, 1, ST, sG, ST, 1, red,
+                [&](int r, int cc, float v) { o[r * D + cc] = v; });
+  // dQs for pixel rows 16w..: lane holds (s = 16w + 4(l/16) + j, c = 16 bj + l % 16)
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  f32x4_t acc[D / 16];
+#pragma unroll
+  for (int bj = 0; bj < D / 16; ++bj) {
+    acc[bj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    mma16(acc[bj], sGt + 16 * w, 1, PST, sCt + 16 * bj, ST, 1, D);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int s = 16 * w + 4 * (lane >> 4) + j;
+    float dot = 0.f;
+#pragma unroll
+    for (int bj = 0; bj < D / 16; ++bj) dot += sQ[s * ST + 16 * bj + (lane & 15)] * acc[bj][j];
+    // sum over the 16 lanes of this row group (same lane >> 4)
+    dot += __shfl_xor(dot, 1, 64);
+    dot += __shfl_xor(dot, 2, 64);
+    dot += __shfl_xor(dot, 4, 64);
+    dot += __shfl_xor(dot, 8, 64);
+    if (s < np) {
+#pragma unroll
+      for (int bj = 0; bj < D / 16; ++bj) {
+        const int c = 16 * bj + (lane & 15);
+        dqkv[(row0 + s) * ldq + C + h * D + c] = from_f32<T>(sQ[s * ST + c] * (acc[bj][j] - dot));
+      }
+    }
+  }
+}
+
+// backward (2): dctx combined from the tile partials; dV into dqkv, dKs into
+// dks [M][C] f32, r partial ws_r[n][tile][C] = sum_s Ks dKs
+//   dKs(s, c) = sum_c' V(s, c') dctx(c, c'), dV(s, c') = sum_c Ks(s, c) dctx(c, c')
+template <typename T, int D>
+__global__ void __launch_bounds__(256) kv_bwd_mfma(const T* __restrict__ qkv, int ld, int S, int C,
+                                                   int heads, const float* __restrict__ kmax,
+                                                   const float* __restrict__ ksum, int nt,
+                                                   const float* __restrict__ ws_dctx,
+                                                   T* __restrict__ dqkv, int ldq,
+                                                   float* __restrict__ dks,
+                                                   float* __restrict__ ws_r) {
+  constexpr int ST = MS<D>::ST;
+  extern __shared__ float sh[];
+  float* sD = sh;               // dctx [c][c']
+  float* sDt = sD + D * ST;     // dctx^T [c'][c]
+  float* sVt = sDt + D * ST;    // V^T [c'][s]
+  float* sKt = sVt + D * PST;   // Ks^T [c][s]
+  float* sR = sKt + D * PST;    // [4][D] per-wave r partials
+  const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int s0 = tile * MCH, np = min(MCH, S - s0);
+  const long row0 = (long)n * S + s0;
+  const float* p = ws_dctx + ((long)n * heads + h) * nt * D * D;
+  for (int o = threadIdx.x; o < D * D; o += 256) {
+    float acc = 0.f;
+    for (int t = 0; t < nt; ++t) acc += p[(long)t * D * D + o];
+    const int c = o / D, cc = o - c * D;
+    sD[c * ST + cc] = acc;
+    sDt[cc * ST + c] = acc;
+  }
+  load_img<T, D, true>(sVt, qkv, row0, ld, 2 * C + h * D, np);
+  load_img<T, D, true>(sKt, qkv, row0, ld, h * D, np);
+  __syncthreads();
+  for (int i = threadIdx.x; i < D * MCH; i += 256) {
+    const int c = i / MCH, s = i - c * MCH;
+    const int ch = h * D + c;
+    sKt[c * PST + s] = s < np ? __expf(sKt[c * PST + s] - kmax[(long)n * C + ch]) /
+                                    ksum[(long)n * C + ch]
+                              : 0.f;
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int bj = 0; bj < D / 16; ++bj) {
+    f32x4_t kv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+    mma16(kv, sVt + 16 * w, 1, PST, sDt + 16 * bj, ST, 1, D);  // dKs, cols c
+    mma16(dv, sKt + 16 * w, 1, PST, sD + 16 * bj, ST, 1, D);   // dV, cols c'
+    const int c = 16 * bj + (lane & 15);
+    float r = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = 16 * w + 4 * (lane >> 4) + j;
+      if (s < np) {
+        dks[(row0 + s) * C + h * D + c] = kv[j];
+        dqkv[(row0 + s) * ldq + 2 * C + h * D + c] = from_f32<T>(dv[j]);
+        r += sKt[c * PST + s] * kv[j];
+      }
+    }
+    r += __shfl_xor(r, 16, 64);
+    r += __shfl_xor(r, 32, 64);
+    if (lane < 16) sR[w * D + c] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x < D) {
+    const int c = threadIdx.x;
+    ws_r[((long)n * nt + tile) * C + h * D + c] = sR[c] + sR[D + c] + sR[2 * D + c] + sR[3 * D + c];
+  }
+}
+
+// backward (3): r combined from the tile partials; dK = Ks (dKs - r)
+template <typename T, int D>
+__global__ void __launch_bounds__(256) k_bwd_mfma(const T* __restrict__ qkv, int ld, int S, int C,
+                                                  const float* __restrict__ kmax,
+                                                  const float* __restrict__ ksum, int nt,
+                                                  const float* __restrict__ ws_r,
+                                                  const float* __restrict__ dks,
+                                                  T* __restrict__ dqkv, int ldq) {
+  __shared__ float sR[D];
+  const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
+  const int s0 = tile * MCH, np = min(MCH, S - s0);
+  const long row0 = (long)n * S + s0;
+  if (threadIdx.x < D) {
+    float r = 0.f;
+    for (int t = 0; t < nt; ++t) r += ws_r[((long)n * nt + t) * C + h * D + threadIdx.x];
+    sR[threadIdx.x] = r;
+  }
+  __syncthreads();
+  constexpr int V = D / 8;
+  for (int i = threadIdx.x; i < np * V; i += 256) {
+    const int s = i / V, c = (i - s * V) * 8;
+    const long m = row0 + s;
+    float k[8], g[8], out[8];
+    load8(qkv + m * ld + h * D + c, k);
+    load8(dks + m * C + h * D + c, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int ch = h * D + c + e;
+      const float ks = __expf(k[e] - kmax[(long)n * C + ch]) / ksum[(long)n * C + ch];
+      out[e] = ks * (g[e] - sR[c + e]);
+    }
+    store8(dqkv + m * ldq + h * D + c, out);
+  }
+}
+
+inline bool mfma_heads(int C, int heads) {
+  const int d = C / heads;
+  return C % heads == 0 && (d == 16 || d == 32 || d == 64);
+}
+
+
+template <typename T, int D>
+int attn_fwd_mfma_t(int N, int S, int C, int heads, const void* qkv, int ld, float* kmax,
+                    float* ksum, float* ctx, float* ws, void* att, int ldo, hipStream_t st) {
+  const int nb = ceil_div(S, MCH);
+  hipLaunchKernelGGL((ctx_part_mfma<T, D>), dim3(nb, heads, N), dim3(256), 0, st,
+                     (const T*)qkv, ld, S, C, heads, nb, ws);
+  hipLaunchKernelGGL((apply_mfma<T, D>), dim3(nb, heads, N), dim3(256), 0, st, (const T*)qkv, ld,
+                     S, C, heads, nb, ws, kmax, ksum, ctx, (T*)att, ldo);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+template <typename T, int D>
+size_t apply_bwd_mfma_lds() {
+  constexpr int ST = MS<D>::ST;
+  return (size_t)(D * ST + 2 * D * PST + 2 * MCH * ST + 1024) * sizeof(float);
+}
+template <int D>
+size_t kv_bwd_mfma_lds() {
+  constexpr int ST = MS<D>::ST;
+  return (size_t)(2 * D * ST + 2 * D * PST + 4 * D) * sizeof(float);
+}
+
+template <typename T, int D>
+int attn_bwd_mfma_t(int N, int S, int C, int heads, const void* qkv, int ld, const float* kmax,
+                    const float* ksum, const float* ctx, const void* datt, int ldd, void* dqkv,
+                    int ldq, float* dks_ws, float* ws, hipStream_t st) {
+  const int nt = ceil_div(S, MCH);
+  float* ws_dctx = ws;
+  float* ws_r = ws + (long)N * heads * nt * D * D;
+  static bool attr = false;  // d = 64 needs more than the default 64 KB of dynamic LDS
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&apply_bwd_mfma<T, D>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&kv_bwd_mfma<T, D>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const dim3 g(nt, heads, N);
+  const size_t lds_a = apply_bwd_mfma_lds<T, D>(), lds_k = kv_bwd_mfma_lds<D>();
+  hipLaunchKernelGGL((apply_bwd_mfma<T, D>), g, dim3(256), lds_a, st,
+                     (const T*)qkv, ld, S, C, heads, ctx, (const T*)datt, ldd, (T*)dqkv, ldq, nt,
+                     ws_dctx);
+  hipLaunchKernelGGL((kv_bwd_mfma<T, D>), g, dim3(256), lds_k, st, (const T*)qkv,
+                     ld, S, C, heads, kmax, ksum, nt, ws_dctx, (T*)dqkv, ldq, dks_ws, ws_r);
+  hipLaunchKernelGGL((k_bwd_mfma<T, D>), g, dim3(256), 0, st, (const T*)qkv, ld, S, C, kmax, ksum,
+                     nt, ws_r, dks_ws, (T*)dqkv, ldq);
+  UM_LAUNCH_CHECK();
+  return UM_OK;
+}
+
+#define UM_ATTN_D(FN, T_, d, ...)                              \
+  (d == 16 ? FN<T_, 16>(__VA_ARGS__)                           \
+           : (d == 32 ? FN<T_, 32>(__VA_ARGS__) : FN<T_, 64>(__VA_ARGS__)))
+
 }  // namespace
 
 extern "C" {
@@ -665,10 +1127,14 @@ long um_attn_ws_kstats(int N, int S, int C) {
 }
 long um_attn_ws_ctx(int N, int S, int C, int heads) {
   const int d = C / heads;
+  if (mfma_heads(C, heads))  // chunk partials {m, l, ctx}
+    return (long)N * heads * ceil_div(S, MCH) * (d * d + 2 * d);
   return (long)N * ceil_div(S, ctx_chunk(d)) * heads * d * d;
 }
 long um_attn_ws_tiles(int N, int S, int C, int heads) {
   const int d = C / heads;
+  if (mfma_heads(C, heads))  // dctx partials, then r partials
+    return (long)N * ceil_div(S, MCH) * (heads * d * d + C);
   const long a = (long)N * ceil_div(S, PT) * heads * d * d;
   const long b = (long)N * ceil_div(S, PT) * C;
   return a > b ? a : b;
@@ -680,6 +1146,13 @@ int um_attn_fwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
   UM_CHECK_ARG(C % heads == 0, "um_attn_fwd: C %% heads");
   const int d = C / heads;
   UM_CHECK_ARG(d <= 64, "um_attn_fwd: head dim %d > 64", d);
+  if (mfma_heads(C, heads) && ld % 8 == 0 && ldo % 8 == 0) {
+    if (dtype == UM_BF16)
+      return UM_ATTN_D(attn_fwd_mfma_t, bf16_t, d, N, S, C, heads, qkv, ld, kmax, ksum, ctx, ws,
+                       att, ldo, st);
+    return UM_ATTN_D(attn_fwd_mfma_t, float, d, N, S, C, heads, qkv, ld, kmax, ksum, ctx, ws, att,
+                     ldo, st);
+  }
   const int kch = ks_chunk(S);
   const int nks = ceil_div(S, kch);
   const int cch = ctx_chunk(d);
@@ -742,6 +1215,13 @@ int um_attn_bwd(int dtype, int N, int S, int C, int heads, const void* qkv, int 
                 hipStream_t st) {
   const int d = C / heads;
   UM_CHECK_ARG(d <= 64 && C % heads == 0, "um_attn_bwd: head dim");
+  if (mfma_heads(C, heads) && ld % 8 == 0 && ldd % 8 == 0 && ldq % 8 == 0 && C % 8 == 0) {
+    if (dtype == UM_BF16)
+      return UM_ATTN_D(attn_bwd_mfma_t, bf16_t, d, N, S, C, heads, qkv, ld, kmax, ksum, ctx, datt,
+                       ldd, dqkv, ldq, dks_ws, ws, st);
+    return UM_ATTN_D(attn_bwd_mfma_t, float, d, N, S, C, heads, qkv, ld, kmax, ksum, ctx, datt, ldd,
+                     dqkv, ldq, dks_ws, ws, st);
+  }
   if (small_heads(C, heads) && ld % 8 == 0 && ldd % 8 == 0 && ldq % 8 == 0)
     return attn_bwd_small(dtype, N, S, C, heads, qkv, ld, kmax, ksum, ctx, datt, ldd, dqkv, ldq,
                           dks_ws, ws, dctx, r, st);
