@@ -698,14 +698,23 @@ template <typename T, int D, bool T_>
 __device__ __forceinline__ void load_img(float* dst, const T* __restrict__ src, long row0, int ld,
                                          int col0, int np) {
   constexpr int ST = MS<D>::ST, V = D / 8;
-  for (int i = threadIdx.x; i < MCH * V; i += 256) {
-    const int s = i / V, c = (i - s * V) * 8;
-    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (s < np) load8(src + (row0 + s) * ld + col0 + c, v);
+  constexpr int IT = (MCH * V + 255) / 256;  // 1 (D <= 32) or 2
+  float v[IT][8];
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {  // every load issued before the first LDS store
+    const int i = threadIdx.x + u * 256, s = i / V, c = (i - s * V) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
+    if (i < MCH * V && s < np) load8(src + (row0 + s) * ld + col0 + c, v[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    const int i = threadIdx.x + u * 256, s = i / V, c = (i - s * V) * 8;
+    if (i >= MCH * V) continue;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      if (T_) dst[(c + e) * PST + s] = v[e];
-      else dst[s * ST + c + e] = v[e];
+      if (T_) dst[(c + e) * PST + s] = v[u][e];
+      else dst[s * ST + c + e] = v[u][e];
     }
   }
 }
@@ -798,55 +807,83 @@ __global__ void __launch_bounds__(256) ctx_part_mfma(const T* __restrict__ qkv, 
 // the pair does the same, bit-identically)
 template <int D>
 __device__ __forceinline__ void ctx_combine(const float* __restrict__ p, int nb, float* sM,
-                                            float* sL, float* dst, int dst_r, int dst_c) {
-  const int t = threadIdx.x;
-  if (t < D) {
-    float M = -INFINITY;
-    for (int b = 0; b < nb; ++b) M = fmaxf(M, p[(long)b * (D * D + 2 * D) + t]);
-    float L = 0.f;
-    for (int b = 0; b < nb; ++b) {
-      const float* q = p + (long)b * (D * D + 2 * D);
-      L += __expf(q[t] - M) * q[D + t];
-    }
-    sM[t] = M;
-    sL[t] = L;
+                                            float* sL, float* red, float* dst, int dst_r,
+                                            int dst_c) {
+  constexpr int G = 256 / D, PS = D * D + 2 * D;
+  const int t = threadIdx.x, c = t % D, g = t / D;
+  float M = -INFINITY;
+  for (int b = g; b < nb; b += G) M = fmaxf(M, p[(long)b * PS + c]);
+  red[t] = M;
+  __syncthreads();
+  M = red[c];
+  for (int q = 1; q < G; ++q) M = fmaxf(M, red[q * D + c]);
+  float L = 0.f;
+  for (int b = g; b < nb; b += G) {
+    const float* q = p + (long)b * PS;
+    L += __expf(q[c] - M) * q[D + c];
+  }
+  __syncthreads();  // every thread has read the maxima
+  red[t] = L;
+  __syncthreads();
+  if (g == 0) {
+    for (int q = 1; q < G; ++q) L += red[q * D + c];
+    sM[c] = M;
+    sL[c] = L;
   }
   __syncthreads();
-  for (int o = t; o < D * D; o += 256) {
-    const int c = o / D, cc = o - c * D;
-    const float M = sM[c];
-    float acc = 0.f;
-    for (int b = 0; b < nb; ++b) {
-      const float* q = p + (long)b * (D * D + 2 * D);
-      acc += __expf(q[c] - M) * q[2 * D + o];
+  // b outer, this thread's outputs inner: their loads are issued together
+  constexpr int PER = (D * D + 255) / 256;
+  float acc[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) acc[u] = 0.f;
+#pragma unroll 2
+  for (int b = 0; b < nb; ++b) {
+    const float* q = p + (long)b * PS;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int o = t + u * 256;
+      if (o < D * D) acc[u] += __expf(q[o / D] - sM[o / D]) * q[2 * D + o];
     }
-    dst[c * dst_r + cc * dst_c] = acc / sL[c];
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int o = t + u * 256;
+    if (o < D * D) dst[(o / D) * dst_r + (o % D) * dst_c] = acc[u] / sL[o / D];
   }
 }
 
 // softmax over the D channels of each of the MCH pixels of a transposed
-// image x[c * PST + s] (wave 0: one pixel per lane; the other waves idle)
+// image x[c * PST + s]: wave w takes channels [w D/4, (w+1) D/4) of every
+// pixel (lane = pixel), the maxima and sums meet in red (2 x 256 floats)
 template <int D>
-__device__ __forceinline__ void softmax_cols(float* x) {
-  if (threadIdx.x < MCH) {
-    const int s = threadIdx.x;
-    float mx = -INFINITY;
-    for (int c = 0; c < D; ++c) mx = fmaxf(mx, x[c * PST + s]);
-    float sum = 0.f;
-    for (int c = 0; c < D; ++c) {
-      const float e = __expf(x[c * PST + s] - mx);
-      x[c * PST + s] = e;
-      sum += e;
-    }
-    const float inv = 1.f / sum;
-    for (int c = 0; c < D; ++c) x[c * PST + s] *= inv;
+__device__ __forceinline__ void softmax_cols(float* x, float* red) {
+  const int s = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int Q = D / 4;
+  float mx = -INFINITY;
+#pragma unroll 4
+  for (int c = w * Q; c < (w + 1) * Q; ++c) mx = fmaxf(mx, x[c * PST + s]);
+  red[w * 64 + s] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[s], red[64 + s]), fmaxf(red[128 + s], red[192 + s]));
+  float sum = 0.f;
+#pragma unroll 4
+  for (int c = w * Q; c < (w + 1) * Q; ++c) {
+    const float e = __expf(x[c * PST + s] - mx);
+    x[c * PST + s] = e;
+    sum += e;
   }
+  red[256 + w * 64 + s] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[256 + s] + red[320 + s] + red[384 + s] + red[448 + s]);
+#pragma unroll 4
+  for (int c = w * Q; c < (w + 1) * Q; ++c) x[c * PST + s] *= inv;
 }
 
-// forward (2): att = softmax_c(Q) ctx per MCH-pixel tile
+// forward (2): att = softmax_c(Q) ctx over tiles [blockIdx.x * tpw, ...) of
+// MCH pixels (the combine is done once per workgroup)
 template <typename T, int D>
 __global__ void __launch_bounds__(256) apply_mfma(const T* __restrict__ qkv, int ld, int S, int C,
-                                                  int heads, int nb,
+                                                  int heads, int nb, int tpw,
                                                   const float* __restrict__ part,
                                                   float* __restrict__ kmax,
                                                   float* __restrict__ ksum,
@@ -854,14 +891,11 @@ __global__ void __launch_bounds__(256) apply_mfma(const T* __restrict__ qkv, int
                                                   int ldo) {
   constexpr int ST = MS<D>::ST;
   __shared__ float sC[D * ST], sQt[D * PST];
-  __shared__ float sM[D], sL[D];
-  const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
-  const int s0 = tile * MCH, np = min(MCH, S - s0);
-  const long row0 = (long)n * S + s0;
-  load_img<T, D, true>(sQt, qkv, row0, ld, C + h * D, np);
-  ctx_combine<D>(part + ((long)n * heads + h) * nb * (D * D + 2 * D), nb, sM, sL, sC, ST, 1);
+  __shared__ float sM[D], sL[D], red[512];
+  const int h = blockIdx.y, n = blockIdx.z;
+  ctx_combine<D>(part + ((long)n * heads + h) * nb * (D * D + 2 * D), nb, sM, sL, red, sC, ST, 1);
   __syncthreads();
-  if (tile == 0) {  // the backward's kmax / ksum / ctx
+  if (blockIdx.x == 0) {  // the backward's kmax / ksum / ctx
     for (int o = threadIdx.x; o < D * D; o += 256)
       ctxg[((long)n * heads + h) * D * D + o] = sC[(o / D) * ST + o % D];
     if (threadIdx.x < D) {
@@ -869,19 +903,27 @@ __global__ void __launch_bounds__(256) apply_mfma(const T* __restrict__ qkv, int
       ksum[(long)n * C + h * D + threadIdx.x] = sL[threadIdx.x];
     }
   }
-  softmax_cols<D>(sQt);
-  __syncthreads();
-  // att(s, c') = sum_c Qs(s, c) ctx(c, c'): wave w takes pixel rows 16w..16w+15
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nt = (S + MCH - 1) / MCH;
+  for (int tile = blockIdx.x * tpw; tile < min(nt, (blockIdx.x + 1) * tpw); ++tile) {
+    const int s0 = tile * MCH, np = min(MCH, S - s0);
+    const long row0 = (long)n * S + s0;
+    __syncthreads();  // the previous tile's products have read sQt
+    load_img<T, D, true>(sQt, qkv, row0, ld, C + h * D, np);
+    __syncthreads();
+    softmax_cols<D>(sQt, red);
+    __syncthreads();
+    // att(s, c') = sum_c Qs(s, c) ctx(c, c'): wave w takes pixel rows 16w..16w+15
 #pragma unroll
-  for (int bj = 0; bj < D / 16; ++bj) {
-    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-    mma16(acc, sQt + 16 * w, 1, PST, sC + 16 * bj, ST, 1, D);
+    for (int bj = 0; bj < D / 16; ++bj) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      mma16(acc, sQt + 16 * w, 1, PST, sC + 16 * bj, ST, 1, D);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int s = 16 * w + 4 * (lane >> 4) + j;
-      if (s < np)
-        att[(row0 + s) * ldo + h * D + 16 * bj + (lane & 15)] = from_f32<T>(acc[j]);
+      for (int j = 0; j < 4; ++j) {
+        const int s = 16 * w + 4 * (lane >> 4) + j;
+        if (s < np)
+          att[(row0 + s) * ldo + h * D + 16 * bj + (lane & 15)] = from_f32<T>(acc[j]);
+      }
     }
   }
 }
@@ -908,12 +950,25 @@ __global__ void __launch_bounds__(256) apply_bwd_mfma(const T* __restrict__ qkv,
   const int s0 = tile * MCH, np = min(MCH, S - s0);
   const long row0 = (long)n * S + s0;
   const float* cg = ctxg + ((long)n * heads + h) * D * D;
-  for (int o = threadIdx.x; o < D * D; o += 256) sCt[(o % D) * ST + o / D] = cg[o];
+  {
+    constexpr int PER = (D * D + 255) / 256;
+    float v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int o = threadIdx.x + u * 256;
+      v[u] = o < D * D ? cg[o] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int o = threadIdx.x + u * 256;
+      if (o < D * D) sCt[(o % D) * ST + o / D] = v[u];
+    }
+  }
   load_img<T, D, true>(sGt, datt, row0, ldd, h * D, np);
   load_img<T, D, false>(sG, datt, row0, ldd, h * D, np);
   load_img<T, D, true>(sQt, qkv, row0, ld, C + h * D, np);
   __syncthreads();
-  softmax_cols<D>(sQt);
+  softmax_cols<D>(sQt, red);
   __syncthreads();
   for (int i = threadIdx.x; i < MCH * D; i += 256) {
     const int s = i / D, c = i - s * D;
@@ -953,14 +1008,15 @@ __global__ void __launch_bounds__(256) apply_bwd_mfma(const T* __restrict__ qkv,
   }
 }
 
-// backward (2): dctx combined from the tile partials; dV into dqkv, dKs into
-// dks [M][C] f32, r partial ws_r[n][tile][C] = sum_s Ks dKs
+// backward (2): dctx combined from the tile partials; over tiles
+// [blockIdx.x * tpw, ...): dV into dqkv, dKs into dks [M][C] f32, and the
+// workgroup's r partial ws_r[n][blockIdx.x][C] = sum_s Ks dKs
 //   dKs(s, c) = sum_c' V(s, c') dctx(c, c'), dV(s, c') = sum_c Ks(s, c) dctx(c, c')
 template <typename T, int D>
 __global__ void __launch_bounds__(256) kv_bwd_mfma(const T* __restrict__ qkv, int ld, int S, int C,
                                                    int heads, const float* __restrict__ kmax,
                                                    const float* __restrict__ ksum, int nt,
-                                                   const float* __restrict__ ws_dctx,
+                                                   int tpw, const float* __restrict__ ws_dctx,
                                                    T* __restrict__ dqkv, int ldq,
                                                    float* __restrict__ dks,
                                                    float* __restrict__ ws_r) {
@@ -971,72 +1027,101 @@ __global__ void __launch_bounds__(256) kv_bwd_mfma(const T* __restrict__ qkv, in
   float* sVt = sDt + D * ST;    // V^T [c'][s]
   float* sKt = sVt + D * PST;   // Ks^T [c][s]
   float* sR = sKt + D * PST;    // [4][D] per-wave r partials
-  const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
-  const int s0 = tile * MCH, np = min(MCH, S - s0);
-  const long row0 = (long)n * S + s0;
+  const int h = blockIdx.y, n = blockIdx.z;
+  __shared__ float sKm[D], sKi[D];
   const float* p = ws_dctx + ((long)n * heads + h) * nt * D * D;
-  for (int o = threadIdx.x; o < D * D; o += 256) {
-    float acc = 0.f;
-    for (int t = 0; t < nt; ++t) acc += p[(long)t * D * D + o];
-    const int c = o / D, cc = o - c * D;
-    sD[c * ST + cc] = acc;
-    sDt[cc * ST + c] = acc;
-  }
-  load_img<T, D, true>(sVt, qkv, row0, ld, 2 * C + h * D, np);
-  load_img<T, D, true>(sKt, qkv, row0, ld, h * D, np);
-  __syncthreads();
-  for (int i = threadIdx.x; i < D * MCH; i += 256) {
-    const int c = i / MCH, s = i - c * MCH;
-    const int ch = h * D + c;
-    sKt[c * PST + s] = s < np ? __expf(sKt[c * PST + s] - kmax[(long)n * C + ch]) /
-                                    ksum[(long)n * C + ch]
-                              : 0.f;
-  }
-  __syncthreads();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  {
+    constexpr int PER = (D * D + 255) / 256;
+    float acc[PER];
 #pragma unroll
-  for (int bj = 0; bj < D / 16; ++bj) {
-    f32x4_t kv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
-    mma16(kv, sVt + 16 * w, 1, PST, sDt + 16 * bj, ST, 1, D);  // dKs, cols c
-    mma16(dv, sKt + 16 * w, 1, PST, sD + 16 * bj, ST, 1, D);   // dV, cols c'
-    const int c = 16 * bj + (lane & 15);
-    float r = 0.f;
+    for (int u = 0; u < PER; ++u) acc[u] = 0.f;
+#pragma unroll 2
+    for (int t = 0; t < nt; ++t)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int s = 16 * w + 4 * (lane >> 4) + j;
-      if (s < np) {
-        dks[(row0 + s) * C + h * D + c] = kv[j];
-        dqkv[(row0 + s) * ldq + 2 * C + h * D + c] = from_f32<T>(dv[j]);
-        r += sKt[c * PST + s] * kv[j];
+      for (int u = 0; u < PER; ++u) {
+        const int o = threadIdx.x + u * 256;
+        if (o < D * D) acc[u] += p[(long)t * D * D + o];
+      }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int o = threadIdx.x + u * 256;
+      if (o < D * D) {
+        const int c = o / D, cc = o - c * D;
+        sD[c * ST + cc] = acc[u];
+        sDt[cc * ST + c] = acc[u];
       }
     }
+  }
+  if (threadIdx.x < D) {
+    sKm[threadIdx.x] = kmax[(long)n * C + h * D + threadIdx.x];
+    sKi[threadIdx.x] = 1.f / ksum[(long)n * C + h * D + threadIdx.x];
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float racc[D / 16];
+#pragma unroll
+  for (int bj = 0; bj < D / 16; ++bj) racc[bj] = 0.f;
+  for (int tile = blockIdx.x * tpw; tile < min(nt, (blockIdx.x + 1) * tpw); ++tile) {
+    const int s0 = tile * MCH, np = min(MCH, S - s0);
+    const long row0 = (long)n * S + s0;
+    __syncthreads();  // the previous tile's products have read sVt / sKt
+    load_img<T, D, true>(sVt, qkv, row0, ld, 2 * C + h * D, np);
+    load_img<T, D, true>(sKt, qkv, row0, ld, h * D, np);
+    __syncthreads();
+    for (int i = threadIdx.x; i < D * MCH; i += 256) {
+      const int c = i / MCH, s = i - c * MCH;
+      sKt[c * PST + s] = s < np ? __expf(sKt[c * PST + s] - sKm[c]) * sKi[c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int bj = 0; bj < D / 16; ++bj) {
+      f32x4_t kv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+      mma16(kv, sVt + 16 * w, 1, PST, sDt + 16 * bj, ST, 1, D);  // dKs, cols c
+      mma16(dv, sKt + 16 * w, 1, PST, sD + 16 * bj, ST, 1, D);   // dV, cols c'
+      const int c = 16 * bj + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int s = 16 * w + 4 * (lane >> 4) + j;
+        if (s < np) {
+          dks[(row0 + s) * C + h * D + c] = kv[j];
+          dqkv[(row0 + s) * ldq + 2 * C + h * D + c] = from_f32<T>(dv[j]);
+          racc[bj] += sKt[c * PST + s] * kv[j];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int bj = 0; bj < D / 16; ++bj) {
+    float r = racc[bj];
     r += __shfl_xor(r, 16, 64);
     r += __shfl_xor(r, 32, 64);
-    if (lane < 16) sR[w * D + c] = r;
+    if (lane < 16) sR[w * D + 16 * bj + lane] = r;
   }
   __syncthreads();
   if (threadIdx.x < D) {
     const int c = threadIdx.x;
-    ws_r[((long)n * nt + tile) * C + h * D + c] = sR[c] + sR[D + c] + sR[2 * D + c] + sR[3 * D + c];
+    ws_r[((long)n * gridDim.x + blockIdx.x) * C + h * D + c] =
+        sR[c] + sR[D + c] + sR[2 * D + c] + sR[3 * D + c];
   }
 }
 
-// backward (3): r combined from the tile partials; dK = Ks (dKs - r)
+// backward (3): r combined from the kv workgroups' partials; dK = Ks (dKs - r)
 template <typename T, int D>
 __global__ void __launch_bounds__(256) k_bwd_mfma(const T* __restrict__ qkv, int ld, int S, int C,
                                                   const float* __restrict__ kmax,
-                                                  const float* __restrict__ ksum, int nt,
+                                                  const float* __restrict__ ksum, int nparts,
                                                   const float* __restrict__ ws_r,
                                                   const float* __restrict__ dks,
                                                   T* __restrict__ dqkv, int ldq) {
-  __shared__ float sR[D];
+  __shared__ float sR[D], sKm[D], sKi[D];
   const int tile = blockIdx.x, h = blockIdx.y, n = blockIdx.z;
   const int s0 = tile * MCH, np = min(MCH, S - s0);
   const long row0 = (long)n * S + s0;
   if (threadIdx.x < D) {
     float r = 0.f;
-    for (int t = 0; t < nt; ++t) r += ws_r[((long)n * nt + t) * C + h * D + threadIdx.x];
+    for (int t = 0; t < nparts; ++t) r += ws_r[((long)n * nparts + t) * C + h * D + threadIdx.x];
     sR[threadIdx.x] = r;
+    sKm[threadIdx.x] = kmax[(long)n * C + h * D + threadIdx.x];
+    sKi[threadIdx.x] = 1.f / ksum[(long)n * C + h * D + threadIdx.x];
   }
   __syncthreads();
   constexpr int V = D / 8;
@@ -1048,8 +1133,7 @@ __global__ void __launch_bounds__(256) k_bwd_mfma(const T* __restrict__ qkv, int
     load8(dks + m * C + h * D + c, g);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int ch = h * D + c + e;
-      const float ks = __expf(k[e] - kmax[(long)n * C + ch]) / ksum[(long)n * C + ch];
+      const float ks = __expf(k[e] - sKm[c + e]) * sKi[c + e];
       out[e] = ks * (g[e] - sR[c + e]);
     }
     store8(dqkv + m * ldq + h * D + c, out);
@@ -1062,14 +1146,23 @@ inline bool mfma_heads(int C, int heads) {
 }
 
 
+// tiles per workgroup of the kernels that combine partials in their
+// prologue: about 512 workgroups (the combine is read once per workgroup)
+inline int tiles_per_wg(int nt, int heads, int N) {
+  const long g = (long)nt * heads * N;
+  const int t = (int)std::max(1l, g / 512);
+  return std::min(t, nt);
+}
+
 template <typename T, int D>
 int attn_fwd_mfma_t(int N, int S, int C, int heads, const void* qkv, int ld, float* kmax,
                     float* ksum, float* ctx, float* ws, void* att, int ldo, hipStream_t st) {
   const int nb = ceil_div(S, MCH);
+  const int tpw = tiles_per_wg(nb, heads, N), nwg = ceil_div(nb, tpw);
   hipLaunchKernelGGL((ctx_part_mfma<T, D>), dim3(nb, heads, N), dim3(256), 0, st,
                      (const T*)qkv, ld, S, C, heads, nb, ws);
-  hipLaunchKernelGGL((apply_mfma<T, D>), dim3(nb, heads, N), dim3(256), 0, st, (const T*)qkv, ld,
-                     S, C, heads, nb, ws, kmax, ksum, ctx, (T*)att, ldo);
+  hipLaunchKernelGGL((apply_mfma<T, D>), dim3(nwg, heads, N), dim3(256), 0, st, (const T*)qkv, ld,
+                     S, C, heads, nb, tpw, ws, kmax, ksum, ctx, (T*)att, ldo);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
@@ -1095,9 +1188,9 @@ int attn_bwd_mfma_t(int N, int S, int C, int heads, const void* qkv, int ld, con
   static bool attr = false;  // d = 64 needs more than the default 64 KB of dynamic LDS
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&apply_bwd_mfma<T, D>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&kv_bwd_mfma<T, D>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
     attr = true;
   }
   const dim3 g(nt, heads, N);
@@ -1105,10 +1198,11 @@ int attn_bwd_mfma_t(int N, int S, int C, int heads, const void* qkv, int ld, con
   hipLaunchKernelGGL((apply_bwd_mfma<T, D>), g, dim3(256), lds_a, st,
                      (const T*)qkv, ld, S, C, heads, ctx, (const T*)datt, ldd, (T*)dqkv, ldq, nt,
                      ws_dctx);
-  hipLaunchKernelGGL((kv_bwd_mfma<T, D>), g, dim3(256), lds_k, st, (const T*)qkv,
-                     ld, S, C, heads, kmax, ksum, nt, ws_dctx, (T*)dqkv, ldq, dks_ws, ws_r);
+  const int tpw = tiles_per_wg(nt, heads, N), nwg = ceil_div(nt, tpw);
+  hipLaunchKernelGGL((kv_bwd_mfma<T, D>), dim3(nwg, heads, N), dim3(256), lds_k, st, (const T*)qkv,
+                     ld, S, C, heads, kmax, ksum, nt, tpw, ws_dctx, (T*)dqkv, ldq, dks_ws, ws_r);
   hipLaunchKernelGGL((k_bwd_mfma<T, D>), g, dim3(256), 0, st, (const T*)qkv, ld, S, C, kmax, ksum,
-                     nt, ws_r, dks_ws, (T*)dqkv, ldq);
+                     nwg, ws_r, dks_ws, (T*)dqkv, ldq);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
