@@ -851,3 +851,91 @@ def test_conv_bn_elu_ybf16(case, monkeypatch):
         assert _rel(bd.weight.grad, br.weight.grad) < 2.5e-1, step
     assert _rel(bd.running_mean, br.running_mean) < 1e-3
     assert _rel(bd.running_var, br.running_var) < 2e-2
+
+
+# the streaming 1x1 kernel (stream1x1.hip, tuning key s1x1) against the
+# 256-row GEMM tiles it replaces (s1x1 = 0) and f64 torch on the same bf16
+# operands: bias / residual (the attention's 1x1 convs), f32 output (the skip
+# conv's z map), accumulate onto up2(z) with the BN statistics slots of the
+# sum (the skip conv's feature-map half) and the data gradient with
+# accumulate; ragged pixel counts and reduction widths padded to 32/64/128
+@pytest.mark.parametrize('case', [(2, 64, 128, 32, 96, 'bias'), (2, 64, 128, 32, 32, 'residual'),
+                                  (1, 129, 131, 64, 32, 'f32'), (2, 64, 128, 32, 64, 'up2stats'),
+                                  (1, 129, 131, 96, 32, 'dgrad'), (2, 64, 128, 64, 192, 'bias'),
+                                  (1, 128, 130, 192, 64, 'dgrad'), (2, 64, 128, 128, 128, 'up2stats')])
+def test_stream1x1(case):
+    from umamd import functional as U
+    from umamd import _lib as L
+    from umamd._lib import PAD_ZERO, call, lib, ptr
+    N, H, W, C, K, mode = case
+    g = torch.Generator().manual_seed(11)
+    x = (torch.rand(N, H, W, C, generator=g) - 0.3).to(torch.bfloat16).to(DEV)
+    wt = (torch.randn(K, C, 1, 1, generator=g) / C ** 0.5).to(DEV)
+    bias = torch.randn(K, generator=g).to(DEV)
+    res = torch.randn(N, H, W, K, generator=g).to(torch.bfloat16).to(DEV)
+    prev = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16).to(DEV)
+    h, w = H // 2, W // 2
+    z = torch.randn(N, h, w, K, generator=g).to(DEV)
+    wq = wt.to(torch.bfloat16).double()[:, :, 0, 0]
+
+    def run():
+        wf, _ = U._pack(wt, C, torch.bfloat16)
+        if mode == 'up2stats':
+            y = torch.empty(N, H, W, K, dtype=torch.float32, device=DEV)
+            slots = torch.zeros(L.STAT_SLOTS * K * 2 + 1, dtype=torch.float64, device=DEV)
+            call('um_conv2d_fwd_up2', L.UM_BF16, N, H, W, C, C, ptr(x), ptr(wf), ptr(bias), K, H,
+                 W, ptr(y), K, L.EPI_STAT_SLOTS, ptr(slots), ptr(z), h, w, K)
+            return y, slots
+        if mode == 'residual':
+            return U._conv_fwd(x, wf, bias, K, 1, 1, 0, PAD_ZERO, epi=L.EPI_RESIDUAL,
+                               residual=res), None
+        if mode == 'f32':
+            return U._conv_fwd(x, wf, None, K, 1, 1, 0, PAD_ZERO, out_dtype=torch.float32), None
+        return U._conv_fwd(x, wf, bias, K, 1, 1, 0, PAD_ZERO), None
+
+    if mode == 'dgrad':
+        # dx (C' = K channels) += dy (C channels) . W^T with W [C][K]: a K -> C conv's
+        # input gradient; dgrad of (dy: C ch) through wT packed from a [C, K] weight
+        wfw = (torch.randn(C, K, 1, 1, generator=g) / K ** 0.5).to(DEV)
+        _, wTd = U._pack(wfw, K, torch.bfloat16)
+        outs = []
+        for flag in (1, 0):
+            old = lib().um_set_tuning(b's1x1', flag)
+            try:
+                dx = prev[..., :K].contiguous().clone()
+                U._conv_dgrad(x, wTd, (N, H, W, K), C, 1, 1, 0, PAD_ZERO, dx=dx, accumulate=True)
+                torch.cuda.synchronize()
+            finally:
+                lib().um_set_tuning(b's1x1', old)
+            outs.append(dx.double())
+        ref = prev[..., :K].double() + torch.einsum('nhwc,ck->nhwk', x.double(),
+                                                    wfw.to(torch.bfloat16).double()[:, :, 0, 0])
+        assert _rel(outs[0], ref) < 1e-2 and _rel(outs[0], outs[1]) < 1e-2
+        return
+    outs = []
+    for flag in (1, 0):
+        old = lib().um_set_tuning(b's1x1', flag)
+        try:
+            outs.append(run())
+            torch.cuda.synchronize()
+        finally:
+            lib().um_set_tuning(b's1x1', old)
+    ref = torch.einsum('nhwc,kc->nhwk', x.double(), wq)
+    if mode != 'f32':
+        ref = ref + bias.double()
+    if mode == 'residual':
+        ref = ref + res.double()
+    if mode == 'up2stats':
+        ref = ref + F.interpolate(z.double().permute(0, 3, 1, 2), scale_factor=2,
+                                  mode='bilinear', align_corners=True).permute(0, 2, 3, 1)
+    (y1, s1), (y0, s0) = outs
+    tol = 1e-2 if y1.dtype == torch.bfloat16 else 1e-5
+    assert _rel(y1.double(), ref) < tol and _rel(y1.double(), y0.double()) < tol
+    if mode == 'up2stats':
+        st1 = s1[:L.STAT_SLOTS * K * 2].view(L.STAT_SLOTS, K, 2).sum(0)
+        st0 = s0[:L.STAT_SLOTS * K * 2].view(L.STAT_SLOTS, K, 2).sum(0)
+        e1, e2 = ref.sum(dim=(0, 1, 2)), (ref * ref).sum(dim=(0, 1, 2))
+        assert float(((st1[:, 0] - e1).abs() / ref.abs().sum(dim=(0, 1, 2))).max()) < 1e-4
+        assert float(((st1[:, 1] - e2).abs() / e2).max()) < 1e-4
+        assert torch.allclose(st1, st0, rtol=1e-5, atol=1e-3)
+        assert float(s1[-1]) == N * H * W

@@ -32,6 +32,7 @@
 #include "common.h"
 #include "igemm.h"
 #include "halo_conv.h"
+#include "stream1x1.h"
 
 namespace {
 
@@ -883,6 +884,7 @@ struct Knobs {
   int halo_pf2;
   int halo_persist, halo_grid, halo_res_kb;
   int border_valu;
+  int s1x1;
   Knobs() {
     auto env = [](const char* n, int d) { return (int)umamd::tuning_env(n, d); };
     small = env("small", 1);
@@ -949,6 +951,9 @@ struct Knobs {
     // reflect fold of the split-form data gradient: a VALU pass over the
     // border list (conv.hip reflect_border_kernel) instead of the GEMM
     border_valu = env("border_valu", 1);
+    // high-resolution 1x1 convs (M >= 16k, C <= 256, N <= 192) on the
+    // streaming kernel (stream1x1.hip) instead of 256-row GEMM tiles
+    s1x1 = env("s1x1", 1);
   }
 };
 Knobs& knobs() {
@@ -1165,6 +1170,7 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
     if (dtype == UM_BF16) return launch_cls<bf16_t, 32, 64, 64, 2, 2, 2>(a, p, ws, st);
     return launch_cls<float, 32, 64, 64, 2, 2, 2>(a, p, ws, st);
   }
+  if (knobs().s1x1 && stream1x1_applicable(dtype, a)) return stream1x1_run(a, st);
   // 8-channel operands take the tap-packed GEMM instead of the halo kernel
   // (which stages 32-channel chunks) unless tappack bit 1 is clear
   const bool pack_first = (knobs().tappack & 3) == 3 && a.ach == 8;
@@ -1252,6 +1258,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "halo_grid")) f = &k.halo_grid;
   else if (!strcmp(key, "halo_res_kb")) f = &k.halo_res_kb;
   else if (!strcmp(key, "border_valu")) f = &k.border_valu;
+  else if (!strcmp(key, "s1x1")) f = &k.s1x1;
   if (!f) return -1;
   const int old = *f;
   *f = value;
