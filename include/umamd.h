@@ -431,20 +431,32 @@ int um_recon_pyramid(int nlevels, int N, int H, int W, const float* const* img,
  * img[s] = pyramid level s [N][6][H>>s][W>>s], pred[s] NHWC [N][H>>s][W>>s][4].
  * The recon is re-derived in the kernel (warp of the opposite view).
  * ws: um_loss_ws() bytes of f64 scratch; out[6] = disp_loss, error_loss,
- * wssim, consistency, smoothness, error term; emap_last (optional) = the last
+ * wssim, consistency, smoothness, error term (disp_loss / error_loss,
+ * optional: out[0] / out[1] again, as the two 0-d loss tensors the reference
+ * returns); emap_last (optional) = the last
  * scale's error map [N][2][h][w] (WeightedSSIMLoss.previous_image_error);
  * recon_out (optional, per scale) receives the reconstruction [N][6][h][w]
- * the kernel derives (reconstruct_pyramid's result, as a side output). */
+ * the kernel derives (reconstruct_pyramid's result, as a side output).
+ * gpart (optional, per scale NHWC [N][h][w][4] f32): the forward of a step
+ * that will differentiate the loss.  The launch then also computes the
+ * gradient per unit gout (channels 0/1: d disp_loss / d d_v without the
+ * consistency scatter, 2/3: d error_loss / d sigma_v), one tile pass for
+ * both, and um_loss_bwd completes it from gpart. */
 long um_loss_ws(int nscales, int N, int H, int W);
 int um_loss_fwd(int nscales, int N, int H, int W, const float* const* img,
                 const float* const* pred, float alpha, int loss_type, float esw, float ecw,
                 float w_wssim, float w_cons, float w_smooth, float w_err, double* ws,
-                float* emap_last, float* const* recon_out, float* out, hipStream_t stream);
-/* its backward in ONE launch: dpred[s] NHWC [N][h][w][4] = d(gout[0]*disp_loss +
- * gout[1]*error_loss)/d pred[s] (gout on the device) */
+                float* emap_last, float* const* recon_out, float* out, float* disp_loss,
+                float* error_loss, float* const* gpart, hipStream_t stream);
+/* its backward (the reference's autograd through loss.py:512-568):
+ * dpred[s] NHWC [N][h][w][4] = d(gout_disp*disp_loss + gout_err*error_loss)/d pred[s]
+ * (gout_disp / gout_err: device scalars, NULL = 0).  gpart NULL: two launches (the consistency scatter,
+ * then every other term); gpart = um_loss_fwd's partials of the same inputs:
+ * ONE launch (the scatter, which scales and completes them). */
 int um_loss_bwd(int nscales, int N, int H, int W, const float* const* img,
                 const float* const* pred, float alpha, int loss_type, float esw, float ecw,
-                float w_wssim, float w_cons, float w_smooth, float w_err, const float* gout,
+                float w_wssim, float w_cons, float w_smooth, float w_err,
+                const float* gout_disp, const float* gout_err, const float* const* gpart,
                 float* const* dpred, hipStream_t stream);
 /* WeightedSSIMLoss.image_error (loss.py:96-131) of an explicit recon: out [N][2][H][W] */
 int um_image_error(const float* img, const float* rec, int N, int H, int W, float alpha,

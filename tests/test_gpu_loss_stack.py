@@ -175,20 +175,15 @@ def _loss_grads(imgs, preds, cfg):
 @pytest.mark.parametrize('shape', [(2, 64, 128), (1, 40, 72), (2, 32, 200)])
 @pytest.mark.parametrize('noisy_right', [False, True])
 def test_row_scatter_vs_oracle(shape, noisy_right):
-    """loss backward with the row-owned consistency scatter (increasing taps:
-    plain read-modify-writes; otherwise the atomic fallback) against the f64
-    oracle, ragged widths (72, 200: a partial 64-source step per row)"""
-    from umamd._lib import lib
+    """loss backward (the strip-owned consistency scatter completing the
+    fused forward's gradient partials) against the f64 oracle, smooth and
+    per-pixel-noise disparities, ragged widths (72, 200: partial tiles)"""
     N, H, W = shape
     g = torch.Generator().manual_seed(11)
     imgs = torch.rand(N, 6, H, W, generator=g)
     preds = _smooth_preds(N, H, W, 12, noisy_right)
     cfg = _cfg()
-    old = lib().um_set_tuning(b'loss_scatter', 1)
-    try:
-        dl, el, gr = _loss_grads(imgs, preds, cfg)
-    finally:
-        lib().um_set_tuning(b'loss_scatter', old)
+    dl, el, gr = _loss_grads(imgs, preds, cfg)
     pyr_c = OL.scale_pyramid(imgs.double(), 4)
     pc = [p.double().requires_grad_(True) for p in preds]
     rc = OL.reconstruct_pyramid(pc, pyr_c)
@@ -203,21 +198,37 @@ def test_row_scatter_vs_oracle(shape, noisy_right):
 
 
 @pytest.mark.parametrize('noisy_right', [False, True])
-def test_row_scatter_matches_atomic_scatter_full_size(noisy_right):
-    """BASELINE config-2 shape: the row-owned scatter and the LDS-atomic
-    strip kernel give the same gradients up to the summation order"""
-    from umamd._lib import lib
+@pytest.mark.parametrize('loss_type', ['l1', 'bayesian', 'log_bayesian'])
+def test_fused_loss_matches_two_pass_full_size(noisy_right, loss_type):
+    """BASELINE config-2 shape: the fused forward (loss terms + gradient
+    partials in one tile pass, um_loss_fwd gpart) and its one-launch backward
+    against the plain forward kernel and the two-launch backward (a second
+    backward through the same graph has no partials left): the same values
+    up to the summation order"""
+    import train.utils as u
+    from train.loss import TukraUncertaintyLoss
+    from umamd import lossfn as LF
     g = torch.Generator().manual_seed(21)
     imgs = torch.rand(8, 6, 256, 512, generator=g)
     preds = _smooth_preds(8, 256, 512, 22, noisy_right)
-    cfg = _cfg()
-    res = {}
-    for mode in (0, 1):
-        old = lib().um_set_tuning(b'loss_scatter', mode)
-        try:
-            res[mode] = _loss_grads(imgs, preds, cfg)
-        finally:
-            lib().um_set_tuning(b'loss_scatter', old)
-    assert float(res[0][0]) == float(res[1][0]) and float(res[0][1]) == float(res[1][1])
-    for a, b in zip(res[0][2], res[1][2]):
-        assert _rel(b, a) < 1e-5
+    lf = TukraUncertaintyLoss(**_cfg(loss_type))
+    pyr = u.scale_pyramid(imgs.to(DEV), 4)
+    pd = [p.to(DEV).requires_grad_(True) for p in preds]
+    with LF.deferred_recon():
+        rec = u.reconstruct_pyramid(pd, pyr)
+    dl, el = lf(pyr, pd, rec, 0, None)
+    terms = lf.last_terms.clone()
+    eager = u.reconstruct_pyramid(pd, pyr)
+    for a, b in zip(rec, eager):
+        assert _rel(a, b) < 1e-6
+    g_fused = torch.autograd.grad(dl + 0.5 * el, pd, retain_graph=True)
+    g_plain = torch.autograd.grad(dl + 0.5 * el, pd)
+    with torch.no_grad():
+        pdd = [p.detach() for p in pd]
+        dl0, el0 = lf(pyr, pdd, u.reconstruct_pyramid(pdd, pyr), 0, None)
+    assert abs(float(dl) / float(dl0) - 1) < 1e-6
+    assert abs(float(el) / float(el0) - 1) < 1e-6
+    assert _rel(terms, lf.last_terms) < 1e-6
+    for a, b in zip(g_fused, g_plain):
+        assert torch.isfinite(a).all()
+        assert _rel(a, b) < 1e-5

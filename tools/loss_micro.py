@@ -53,7 +53,11 @@ def main():
     if a.only in ('all', 'recon'):
         res['recon'] = timed(lambda: LF.reconstruct_pyramid(preds, pyr))
     if a.only in ('all', 'fwd'):
-        res['loss_fwd'] = timed(lambda: LF.tukra_loss(cfg, preds, pyr))
+        def fwd_plain():
+            with torch.no_grad():
+                LF.tukra_loss(cfg, preds, pyr)
+        res['loss_fwd'] = timed(fwd_plain)
+        res['loss_fwd_fused'] = timed(lambda: LF.tukra_loss(cfg, preds, pyr))
     if a.only in ('all', 'bwd'):
         def fb():
             dl, el, _, _ = LF.tukra_loss(cfg, preds, pyr)

@@ -15,10 +15,15 @@
 // Launch structure (one step, all scales):
 //   um_pyramid         ONE launch, every level (level 0 = exact copy)
 //   um_recon_pyramid   ONE launch, every level and both views
-//   um_loss_fwd        ONE launch: every scale, both views, the six loss
-//                      terms; the last workgroup to finish (agent-scope
-//                      ticket) reduces the per-block f64 partials.
-//   um_loss_bwd        ONE launch: d(loss)/d(prediction), every scale.
+//   um_loss_fwd        every scale, both views, the six loss terms as f64
+//                      per-tile sums, then a one-workgroup launch that
+//                      reduces them in a fixed order.  With gpart (a step that
+//                      will differentiate the loss) the tile launch is
+//                      loss_grad_kernel<true>: the terms AND the gradient per
+//                      unit gout from one pass over the tiles.
+//   um_loss_bwd        with gpart: ONE launch (the consistency scatter, which
+//                      scales and completes the partials); without: the
+//                      scatter, then loss_grad_kernel<false>.
 // The loss kernels do not read the reconstruction: each tile re-warps the
 // opposite view itself (the recon of a pixel is 12 L2-resident taps), so
 // the WSSIM term's gradient through the warp is computed in place.  The
@@ -319,6 +324,7 @@ struct LScale {
   const float* img;   // [N][6][h][w]
   const float* pred;  // NHWC [N][h][w][4]
   float* dpred;       // bwd output NHWC [N][h][w][4]
+  float* gpart;       // gradient partials per unit gout (see loss_grad_kernel<true>)
   int h, w, tiles_x, tiles_y, block0;
 };
 
@@ -328,6 +334,7 @@ struct LArgs {
   const float* img[MAXS];
   const float* pred[MAXS];
   float* dpred[MAXS];
+  float* gpart[MAXS];  // fused forward: per-unit-gout gradient partials NHWC [N][h][w][4]
   int h[MAXS], w[MAXS], tiles_x[MAXS], tiles_y[MAXS], block0[MAXS];
   int nscales, N, nblocks;
   float alpha;
@@ -338,8 +345,13 @@ struct LArgs {
   float* emap;        // fwd: error map of the last scale [N][2][h][w] (or null)
   float* rec[MAXS];   // fwd (optional): the reconstruction [N][6][h][w] as a side output
   float* out;         // fwd: [6] disp_loss, error_loss, wssim, consistency, smoothness, error
-  const float* gout;  // bwd: [2] d total / d disp_loss, d total / d error_loss
+  float* disp_loss;    // fwd (optional): out[0] again
+  float* error_loss;   // fwd (optional): out[1] again
+  const float* gout_d;  // bwd: d total / d disp_loss (a device scalar; null = 0)
+  const float* gout_e;  // bwd: d total / d error_loss (null = 0)
 };
+
+__device__ __forceinline__ float gval(const float* p) { return p != nullptr ? *p : 0.f; }
 
 __device__ __forceinline__ int scale_of(const LArgs& a, int b) {
   int s = 0;
@@ -353,6 +365,7 @@ __device__ __forceinline__ LScale scale_desc(const LArgs& a, int s) {
   S.img = pick(a.img, s);
   S.pred = pick(a.pred, s);
   S.dpred = pick(a.dpred, s);
+  S.gpart = pick(a.gpart, s);
   S.h = pick(a.h, s);
   S.w = pick(a.w, s);
   S.tiles_x = pick(a.tiles_x, s);
@@ -361,7 +374,6 @@ __device__ __forceinline__ LScale scale_desc(const LArgs& a, int s) {
   return S;
 }
 
-__device__ unsigned int g_loss_ticket;
 
 // ---------------------------------------------------------- tile staging --
 // A tile of TY x TX pixels of one image, scale and view.  Staged region =
@@ -558,6 +570,102 @@ __device__ __forceinline__ float dssim_up(const float (*sD)[GX], const UpTap& uy
          uy.l1 * ((1.f - ux.l1) * sD[uy.i1][ux.i0] + ux.l1 * sD[uy.i1][ux.i1]);
 }
 
+// Block sums of the six loss terms (f64) into parts[blockIdx.x][0..5]; a
+// separate one-workgroup launch (loss_reduce_kernel) scales them per pyramid
+// level and sums them in a fixed order (deterministic).  An in-kernel
+// "last workgroup" ticket measured slower: every workgroup then waits for its
+// partials to land and (on gfx950) writes back its XCD's dirty L2 lines.
+template <int NT>
+__device__ __forceinline__ void loss_partials(const LArgs& a, const float (&acc)[6],
+                                              double (*red)[NT / 64]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const float tsum = wave_sum(acc[k]);
+    if ((tid & 63) == 0) red[k][tid >> 6] = (double)tsum;
+  }
+  __syncthreads();
+  if (tid < 6) {
+    double r = 0.0;
+    for (int w = 0; w < NT / 64; ++w) r += red[tid][w];
+    a.parts[(long)blockIdx.x * 8 + tid] = r;
+  }
+}
+
+constexpr int RNT = 1024;
+
+// out[6] from the block sums: per level s the pixel means (the smoothness
+// term also / 2^s, the NLL / 2 and for log_bayesian / 2 again), summed over
+// every block in a fixed order, then the weighted totals
+__global__ void __launch_bounds__(RNT) loss_reduce_kernel(LArgs a) {
+  __shared__ double red[6][RNT / 64];
+  __shared__ double fac[MAXS][6];
+  const int tid = threadIdx.x;
+  if (tid < a.nscales * 6) {
+    const int s = tid / 6, k = tid - s * 6;
+    const double np = (double)a.N * pick(a.h, s) * pick(a.w, s);
+    double f = 1.0 / np;
+    if (k == 2) f /= (double)(1 << s);
+    if (k == 3) f *= a.loss_type == 2 ? 0.25 : 0.5;
+    fac[s][k] = f;
+  }
+  __syncthreads();
+  double q[6] = {0, 0, 0, 0, 0, 0};
+  constexpr int U = 4;  // rows in flight per thread (the partials come from other XCDs' L2s)
+  for (int b0 = tid; b0 < a.nblocks; b0 += U * RNT) {
+    double2 v[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = min(b0 + u * RNT, a.nblocks - 1);
+      const double2* p = reinterpret_cast<const double2*>(a.parts + (long)b * 8);
+      v[u][0] = p[0];
+      v[u][1] = p[1];
+      v[u][2] = p[2];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = b0 + u * RNT;
+      if (b >= a.nblocks) break;
+      const int s = scale_of(a, b);
+      q[0] += v[u][0].x * fac[s][0];
+      q[1] += v[u][0].y * fac[s][1];
+      q[2] += v[u][1].x * fac[s][2];
+      q[3] += v[u][1].y * fac[s][3];
+      q[4] += v[u][2].x * fac[s][4];
+      q[5] += v[u][2].y * fac[s][5];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q[k] += __shfl_xor(q[k], o, 64);
+  }
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) red[k][tid >> 6] = q[k];
+  __syncthreads();
+  double f[6];
+  if (tid == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      f[k] = 0.0;
+      for (int w = 0; w < RNT / 64; ++w) f[k] += red[k][w];
+    }
+  }
+  if (tid == 0) {
+    const double ws = f[0], cs = f[1], sm = f[2];
+    const double er = f[3] + (double)a.esw * f[5] + (double)a.ecw * f[4];
+    a.out[0] = (float)(ws * a.w_wssim + cs * a.w_cons + sm * a.w_smooth);
+    a.out[1] = (float)(er * a.w_err);
+    if (a.disp_loss != nullptr) *a.disp_loss = a.out[0];
+    if (a.error_loss != nullptr) *a.error_loss = a.out[1];
+    a.out[2] = (float)ws;
+    a.out[3] = (float)cs;
+    a.out[4] = (float)sm;
+    a.out[5] = (float)er;
+  }
+}
+
 // ------------------------------------------------------------ forward ------
 constexpr int FTY = 16, FTX = 64, FNT = 512;
 using FT = Tile<FTY, FTX>;
@@ -570,7 +678,6 @@ __global__ void __launch_bounds__(FNT, 2) loss_fwd_kernel(LArgs a) {
   __shared__ float sD[FT::GY][FT::GX];
   __shared__ Tabs<FTY, FTX> tb;
   __shared__ double red[6][FNT / 64];
-  __shared__ int last;
   const int tid = threadIdx.x;
   const int s = scale_of(a, blockIdx.x);
   const LScale S = scale_desc(a, s);
@@ -676,76 +783,7 @@ __global__ void __launch_bounds__(FNT, 2) loss_fwd_kernel(LArgs a) {
     }
     __syncthreads();
   }
-  // block partials, pre-scaled per scale (f64)
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const float tsum = wave_sum(acc[k]);
-    if ((tid & 63) == 0) red[k][tid >> 6] = (double)tsum;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    const double np = (double)a.N * HW;
-    double r[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      r[k] = 0.0;
-      for (int w = 0; w < FNT / 64; ++w) r[k] += red[k][w];
-    }
-    double* o = a.parts + (long)blockIdx.x * 8;
-    o[0] = r[0] / np;
-    o[1] = r[1] / np;
-    o[2] = r[2] / np / (double)(1 << s);
-    o[3] = r[3] / (2.0 * np) * (a.loss_type == 2 ? 0.5 : 1.0);
-    o[4] = r[4] / np;
-    o[5] = r[5] / np;
-  }
-  // the last workgroup to finish sums the partials (fixed order: deterministic)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned tk =
-        __hip_atomic_fetch_add(&g_loss_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (tk == gridDim.x - 1);
-    if (last) {
-      __hip_atomic_store(&g_loss_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  double q[6] = {0, 0, 0, 0, 0, 0};
-  for (int b = tid; b < a.nblocks; b += FNT)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) q[k] += a.parts[(long)b * 8 + k];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) q[k] += __shfl_xor(q[k], o, 64);
-  }
-  __syncthreads();
-  if ((tid & 63) == 0)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) red[k][tid >> 6] = q[k];
-  __syncthreads();
-  if (tid == 0) {
-    double f[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      f[k] = 0.0;
-      for (int w = 0; w < FNT / 64; ++w) f[k] += red[k][w];
-    }
-    const double ws = f[0], cs = f[1], sm = f[2];
-    const double er = f[3] + (double)a.esw * f[5] + (double)a.ecw * f[4];
-    a.out[0] = (float)(ws * a.w_wssim + cs * a.w_cons + sm * a.w_smooth);
-    a.out[1] = (float)(er * a.w_err);
-    a.out[2] = (float)ws;
-    a.out[3] = (float)cs;
-    a.out[4] = (float)sm;
-    a.out[5] = (float)er;
-  }
+  loss_partials<FNT>(a, acc, red);
 }
 
 // ------------------------------------------------------------ backward -----
@@ -759,13 +797,23 @@ __global__ void __launch_bounds__(FNT, 2) loss_fwd_kernel(LArgs a) {
 constexpr int STR = 8;
 constexpr int SCT = 1024;  // threads per scatter workgroup
 
+// COMBINE: the forward was loss_grad_kernel<true>; complete its per-unit-gout
+// partials: dpred = (gout_d * gpart.xy + scatter, gout_e * gpart.zw).
+template <bool COMBINE>
 __global__ void __launch_bounds__(SCT) loss_scatter_kernel(LArgs a) {
   // The warp's row taps do not depend on the shift (row_w), so the scatter
   // is separable: each source row r first scatters along x into its own
   // accumulator X_r[ch][x] (2 LDS adds per term instead of 4), then target
   // row T sums (1-n_r) X_r over the rows with y0(r) = T and n_r X_r over
   // those with y0(r) + 1 = T.
-  extern __shared__ float acc[];  // [STR + 2 source rows][2 target ch][W]
+  // The row accumulators are fixed point (int32 LDS atomics, which run at
+  // the LDS's integer rate; f32 LDS atomics measured 2x slower for the whole
+  // kernel): every contribution is gg * e with |gg| <= kmax = max(|kcd|, |kce|)
+  // and e + w = 1 per source, so a row sums at most W * kmax into one target.
+  // Units of kmax * 2^-sh with sh = 30 - ceil(log2 W) keep that below 2^30;
+  // the quantum is kmax * 2^-sh (5e-7 kmax at W = 512) and the integer sums
+  // are exact, i.e. independent of the atomics' order.
+  extern __shared__ int acc[];  // [STR + 2 source rows][2 target ch][W]
   const int tid = threadIdx.x;
   const int s = scale_of(a, blockIdx.x);
   const LScale S = scale_desc(a, s);
@@ -775,14 +823,18 @@ __global__ void __launch_bounds__(SCT) loss_scatter_kernel(LArgs a) {
   const int n = lb / S.tiles_y, y0 = (lb - n * S.tiles_y) * STR;
   const float* pp = S.pred + (long)n * HW * 4;
   const double np = (double)a.N * HW;
-  const float kcd = (float)(a.gout[0] * a.w_cons / np);
-  const float kce = (float)(a.gout[1] * a.w_err * a.ecw / np);
+  const float kcd = (float)(gval(a.gout_d) * a.w_cons / np);
+  const float kce = (float)(gval(a.gout_e) * a.w_err * a.ecw / np);
   const float Wh = (float)W * 0.5f;
   const float stepx = W > 1 ? 1.f / (float)(W - 1) : 0.f;
   const int halfw = W / 2;
   const int r0 = max(0, y0 - 1), r1 = min(H, y0 + STR + 1);
   const int nr = r1 - r0;
-  for (int i = tid; i < nr * 2 * W; i += SCT) acc[i] = 0.f;
+  const float kmax = fmaxf(fabsf(kcd), a.ecw != 0.f ? fabsf(kce) : 0.f);
+  const int sh = 30 - (W > 1 ? 32 - __clz(W - 1) : 0);
+  const float toq = kmax > 0.f ? ldexpf(1.f, sh) / kmax : 0.f;
+  const float fromq = ldexpf(kmax, -sh);
+  for (int i = tid; i < nr * 2 * W; i += SCT) acc[i] = 0;
   __syncthreads();
   for (int i = tid; i < nr * W; i += SCT) {
     const int ri = i / W, x = i - ri * W;
@@ -805,21 +857,23 @@ __global__ void __launch_bounds__(SCT) loss_scatter_kernel(LArgs a) {
       cons_samples<1>(pp + 1, H, W, t + 2, wv + 2, nullptr);
       cons_samples<1>(pp + 0, H, W, t + 3, wv + 3, nullptr);
     }
-    float* X = acc + ri * 2 * W;
+    int* X = acc + ri * 2 * W;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j >= 2 && a.ecw == 0.f) break;
       const int v = j & 1;
-      const float gg = -sgnf(val[j] - wv[j]) * (j < 2 ? kcd : kce);
+      const float gg = -sgnf(val[j] - wv[j]) * (j < 2 ? kcd : kce) * toq;
       if (gg == 0.f) continue;
-      float* Xc = X + (1 - v) * W;  // target channel = the warped (opposite) disparity
+      int* Xc = X + (1 - v) * W;  // target channel = the warped (opposite) disparity
       const int xa = t[j].x0;
-      if (xa >= 0 && xa < W) atomicAdd(&Xc[xa], gg * t[j].e);
-      if (xa + 1 >= 0 && xa + 1 < W) atomicAdd(&Xc[xa + 1], gg * t[j].w);
+      if (xa >= 0 && xa < W) atomicAdd(&Xc[xa], __float2int_rn(gg * t[j].e));
+      if (xa + 1 >= 0 && xa + 1 < W) atomicAdd(&Xc[xa + 1], __float2int_rn(gg * t[j].w));
     }
   }
   __syncthreads();
   float* sa = S.dpred + ((long)n * HW + (long)y0 * W) * 4;
+  const float* gp = COMBINE ? S.gpart + ((long)n * HW + (long)y0 * W) * 4 : nullptr;
+  const float gd = COMBINE ? gval(a.gout_d) : 0.f, ge = COMBINE ? gval(a.gout_e) : 0.f;
   const int rows = min(STR, H - y0);
   for (int i = tid; i < rows * W; i += SCT) {
     const int T = y0 + i / W, x = i % W;
@@ -828,18 +882,34 @@ __global__ void __launch_bounds__(SCT) loss_scatter_kernel(LArgs a) {
       const RowW rw = row_w(r, H);
       const float wgt = rw.y0 == T ? 1.f - rw.n : (rw.y0 + 1 == T ? rw.n : 0.f);
       if (wgt == 0.f) continue;
-      const float* X = acc + (r - r0) * 2 * W;
-      g0 += wgt * X[x];
-      g1 += wgt * X[W + x];
+      const int* X = acc + (r - r0) * 2 * W;
+      g0 += wgt * (float)X[x];
+      g1 += wgt * (float)X[W + x];
     }
-    *reinterpret_cast<float2*>(sa + i * 4) = make_float2(g0, g1);
+    g0 *= fromq;
+    g1 *= fromq;
+    if (COMBINE) {
+      const float4 p = *reinterpret_cast<const float4*>(gp + i * 4);
+      *reinterpret_cast<float4*>(sa + i * 4) =
+          make_float4(gd * p.x + g0, gd * p.y + g1, ge * p.z, ge * p.w);
+    } else {
+      *reinterpret_cast<float2*>(sa + i * 4) = make_float2(g0, g1);
+    }
   }
 }
 
-// (2) every other gradient, per TY x TX tile (both views), plus the scatter sums
+// (2) every other gradient, per TY x TX tile (both views), plus the scatter sums.
+// FUSED: the forward pass of a step that will differentiate the loss.  The
+// same tile work also yields the six loss terms (loss_fwd_kernel's sums), and
+// the gradient is stored per unit gout -- channels 0/1 the d(disp_loss)/d(d_v)
+// part without the scatter, channels 2/3 d(error_loss)/d(sigma_v) -- into
+// gpart; the backward's scatter launch scales and completes it
+// (loss_scatter_kernel<true>).  Every gradient term is linear in exactly one
+// of gout_d / gout_e, so this is the backward at any gout.
 constexpr int BTY = 16, BTX = 32, BNT = 512;
 using BT = Tile<BTY, BTX>;
 
+template <bool FUSED>
 __global__ void __launch_bounds__(BNT, 2) loss_grad_kernel(LArgs a) {
   __shared__ float4 sP[BT::RY][BT::RX];
   __shared__ float sI[3][BT::RY][BT::RX], sR[3][BT::RY][BT::RX];
@@ -848,6 +918,7 @@ __global__ void __launch_bounds__(BNT, 2) loss_grad_kernel(LArgs a) {
   __shared__ float sD[BT::GY][BT::GX];
   __shared__ float sUy[BT::GY], sUx[BT::GX];
   __shared__ Tabs<BTY, BTX> tb;
+  __shared__ double red[FUSED ? 6 : 1][BNT / 64];
   const int tid = threadIdx.x;
   const int s = scale_of(a, blockIdx.x);
   const LScale S = scale_desc(a, s);
@@ -862,7 +933,7 @@ __global__ void __launch_bounds__(BNT, 2) loss_grad_kernel(LArgs a) {
   const int gh = H - 2, gw = W - 2;
   const float Wh = (float)W * 0.5f;
   const double np = (double)a.N * HW;
-  const float gd = a.gout[0], ge = a.gout[1];
+  const float gd = FUSED ? 1.f : gval(a.gout_d), ge = FUSED ? 1.f : gval(a.gout_e);
   const float kW = (float)(gd * a.w_wssim / np);  // d total / d sum_p (e_L + e_R)
   const float kcd = (float)(gd * a.w_cons / np);
   const float kce = (float)(ge * a.w_err * a.ecw / np);
@@ -874,8 +945,10 @@ __global__ void __launch_bounds__(BNT, 2) loss_grad_kernel(LArgs a) {
   const int y = ty0 + ly, x = tx0 + lx;
   const bool ok = y < H && x < W;
   const int rr = ly + 2, qq = lx + 2;
-  float* dslot = S.dpred + ((long)n * HW + (long)min(y, H - 1) * W + min(x, W - 1)) * 4;
-  const float2 sav = *reinterpret_cast<const float2*>(dslot);
+  float* dslot = (FUSED ? S.gpart : S.dpred) + ((long)n * HW + (long)min(y, H - 1) * W + min(x, W - 1)) * 4;
+  const float2 sav = FUSED ? make_float2(0.f, 0.f) : *reinterpret_cast<const float2*>(dslot);
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // FUSED: the forward's loss terms
+  float* const recp = FUSED ? pick(a.rec, s) : nullptr;
 
   stage_pred<BTY, BTX, BNT>(pp, H, W, ty0, tx0, sP);
   init_tabs<BTY, BTX>(tb, H, W, ty0, tx0);
@@ -959,8 +1032,12 @@ __global__ void __launch_bounds__(BNT, 2) loss_grad_kernel(LArgs a) {
       }
       // ---- disparity consistency, own operand (the warped one came from the scatter)
       gdv += sgnf(dv - wv[0]) * kcd * (1.f - dx[0] * sign * (float)W);
+      if (FUSED) acc[1] += fabsf(dv - wv[0]);
       // ---- error consistency: sigma_v vs warp(d_opp, sign*sigma_v) (F5)
-      if (a.ecw != 0.f) gsv += sgnf(sg - wv[1]) * kce * (1.f - dx[1] * sign * (float)W);
+      if (a.ecw != 0.f) {
+        gsv += sgnf(sg - wv[1]) * kce * (1.f - dx[1] * sign * (float)W);
+        if (FUSED) acc[4] += fabsf(sg - wv[1]);
+      }
       // ---- smoothness (loss.py:191-264) of d_v (and sigma_v if weighted)
       {
         auto wgt = [&](int ry, int rx, int dy, int dxx) {
@@ -988,12 +1065,27 @@ __global__ void __launch_bounds__(BNT, 2) loss_grad_kernel(LArgs a) {
           if (y > 0) g -= sgnf((comp(pym, ch) - d0) * wy1) * wy1;
           if (k == 0) gdv += ksd * g;
           else gsv += kse * g;
+          if (FUSED) {  // forward smoothness (wx0 / wy0 are 0 at the far edges, as dgx / dgy are)
+            const float dgx = x < W - 1 ? d0 - comp(pxp, ch) : 0.f;
+            const float dgy = y < H - 1 ? d0 - comp(pyp, ch) : 0.f;
+            acc[k == 0 ? 2 : 5] += fabsf(dgx * wx0) + fabsf(dgy * wy0);
+          }
         }
       }
       // ---- NLL on sigma_v with the detached error map (loss.py:389-403)
       {
         const float up = dssim_up<BT::GX>(sD, tb.uy[ly], tb.ux[lx]);
         const float ev = a.alpha * up + (1.f - a.alpha) * (l1 * (1.f / 3.f));
+        if (FUSED) {
+          acc[0] += ev;
+          if (a.loss_type == 1) acc[3] += fdiv(ev, sg) + __logf(sg);
+          else if (a.loss_type == 2) acc[3] += fdiv(ev, __expf(-sg)) + sg;
+          else acc[3] += fabsf(sg - ev);
+          if (a.emap != nullptr && s == a.nscales - 1) a.emap[(n * 2 + v) * HW + y * W + x] = ev;
+          if (recp != nullptr)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) recp[(n * 6 + v * 3 + c) * HW + y * W + x] = sR[c][rr][qq];
+        }
         float g;
         if (a.loss_type == 1) g = fdiv(1.f, sg) - fdiv(ev, sg * sg);
         else if (a.loss_type == 2) g = 0.5f * (ev * __expf(sg) + 1.f);
@@ -1006,6 +1098,7 @@ __global__ void __launch_bounds__(BNT, 2) loss_grad_kernel(LArgs a) {
     __syncthreads();
   }
   if (ok) *reinterpret_cast<float4*>(dslot) = outv;
+  if constexpr (FUSED) loss_partials<BNT>(a, acc, red);
 }
 
 constexpr int ETY = 16, ETX = 64;
@@ -1176,54 +1269,75 @@ long um_loss_ws(int nscales, int N, int H, int W) {
   LArgs a{};
   const float* dummy[MAXS] = {};
   if (nscales < 1 || nscales > MAXS) return 0;
-  return (long)loss_setup(a, nscales, N, H, W, dummy, dummy, nullptr, FTY, FTX) * 8 *
+  // partials for the smaller tiles of the fused forward (>= the plain forward's)
+  return (long)loss_setup(a, nscales, N, H, W, dummy, dummy, nullptr, BTY, BTX) * 8 *
          sizeof(double);
 }
 
 int um_loss_fwd(int nscales, int N, int H, int W, const float* const* img,
                 const float* const* pred, float alpha, int loss_type, float esw, float ecw,
                 float w_wssim, float w_cons, float w_smooth, float w_err, double* ws,
-                float* emap_last, float* const* recon_out, float* out, hipStream_t st) {
+                float* emap_last, float* const* recon_out, float* out, float* disp_loss,
+                float* error_loss, float* const* gpart, hipStream_t st) {
   UM_CHECK_ARG(nscales >= 1 && nscales <= MAXS, "um_loss_fwd: %d scales (1..%d)", nscales, MAXS);
   UM_CHECK_ARG((H >> (nscales - 1)) >= 3 && (W >> (nscales - 1)) >= 3,
                "um_loss_fwd: image %dx%d too small for %d scales", H, W, nscales);
   LArgs a{};
-  const int blocks = loss_setup(a, nscales, N, H, W, img, pred, nullptr, FTY, FTX);
+  const int blocks = gpart ? loss_setup(a, nscales, N, H, W, img, pred, nullptr, BTY, BTX)
+                           : loss_setup(a, nscales, N, H, W, img, pred, nullptr, FTY, FTX);
   a.alpha = alpha; a.loss_type = loss_type; a.esw = esw; a.ecw = ecw;
   a.w_wssim = w_wssim; a.w_cons = w_cons; a.w_smooth = w_smooth; a.w_err = w_err;
   a.parts = ws;
   a.emap = emap_last;
   for (int l = 0; l < nscales; ++l) a.rec[l] = recon_out ? recon_out[l] : nullptr;
   a.out = out;
-  hipLaunchKernelGGL(loss_fwd_kernel, dim3(blocks), dim3(FNT), 0, st, a);
+  a.disp_loss = disp_loss;
+  a.error_loss = error_loss;
+  if (gpart) {
+    for (int l = 0; l < nscales; ++l) a.gpart[l] = gpart[l];
+    hipLaunchKernelGGL(loss_grad_kernel<true>, dim3(blocks), dim3(BNT), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(loss_fwd_kernel, dim3(blocks), dim3(FNT), 0, st, a);
+  }
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(RNT), 0, st, a);
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
 
 int um_loss_bwd(int nscales, int N, int H, int W, const float* const* img,
                 const float* const* pred, float alpha, int loss_type, float esw, float ecw,
-                float w_wssim, float w_cons, float w_smooth, float w_err, const float* gout,
+                float w_wssim, float w_cons, float w_smooth, float w_err,
+                const float* gout_disp, const float* gout_err, const float* const* gpart,
                 float* const* dpred, hipStream_t st) {
   UM_CHECK_ARG(nscales >= 1 && nscales <= MAXS, "um_loss_bwd: %d scales (1..%d)", nscales, MAXS);
   UM_CHECK_ARG((H >> (nscales - 1)) >= 3 && (W >> (nscales - 1)) >= 3,
                "um_loss_bwd: image %dx%d too small for %d scales", H, W, nscales);
-  const size_t lds = (size_t)(STR + 2) * W * 2 * sizeof(float);
+  const size_t lds = (size_t)(STR + 2) * W * 2 * sizeof(int);
   UM_CHECK_ARG(lds <= 128 * 1024, "um_loss_bwd: width %d too large", W);
   LArgs a{};
   a.alpha = alpha; a.loss_type = loss_type; a.esw = esw; a.ecw = ecw;
   a.w_wssim = w_wssim; a.w_cons = w_cons; a.w_smooth = w_smooth; a.w_err = w_err;
-  a.gout = gout;
+  a.gout_d = gout_disp;
+  a.gout_e = gout_err;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&loss_scatter_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&loss_scatter_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&loss_scatter_kernel<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
     attr = true;
   }
-  // (1) consistency scatter sums into channels 0/1 of dpred, (2) the rest
   int blocks = loss_setup(a, nscales, N, H, W, img, pred, dpred, STR, 0);
-  hipLaunchKernelGGL(loss_scatter_kernel, dim3(blocks), dim3(SCT), lds, st, a);
-  blocks = loss_setup(a, nscales, N, H, W, img, pred, dpred, BTY, BTX);
-  hipLaunchKernelGGL(loss_grad_kernel, dim3(blocks), dim3(BNT), 0, st, a);
+  if (gpart) {
+    // the fused forward computed every other term: the scatter completes them
+    for (int l = 0; l < nscales; ++l) a.gpart[l] = const_cast<float*>(gpart[l]);
+    hipLaunchKernelGGL(loss_scatter_kernel<true>, dim3(blocks), dim3(SCT), lds, st, a);
+  } else {
+    // (1) consistency scatter sums into channels 0/1 of dpred, (2) the rest
+    hipLaunchKernelGGL(loss_scatter_kernel<false>, dim3(blocks), dim3(SCT), lds, st, a);
+    blocks = loss_setup(a, nscales, N, H, W, img, pred, dpred, BTY, BTX);
+    hipLaunchKernelGGL(loss_grad_kernel<false>, dim3(blocks), dim3(BNT), 0, st, a);
+  }
   UM_LAUNCH_CHECK();
   return UM_OK;
 }

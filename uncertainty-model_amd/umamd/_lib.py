@@ -136,8 +136,9 @@ _SIG = {
     'um_recon_pyramid': (_I, [_I, _I, _I, _I, _P, _P, _P, _P, 's']),
     'um_loss_ws': (_L, [_I, _I, _I, _I]),
     'um_loss_fwd': (_I, [_I, _I, _I, _I, _P, _P, _F, _I, _F, _F, _F, _F, _F, _F, _P, _P, _P,
+                         _P, _P, _P, _P, 's']),
+    'um_loss_bwd': (_I, [_I, _I, _I, _I, _P, _P, _F, _I, _F, _F, _F, _F, _F, _F, _P, _P, _P,
                          _P, 's']),
-    'um_loss_bwd': (_I, [_I, _I, _I, _I, _P, _P, _F, _I, _F, _F, _F, _F, _F, _F, _P, _P, 's']),
     'um_image_error': (_I, [_P, _P, _I, _I, _I, _F, _P, 's']),
     'um_nhwc_to_image': (_I, [_I, _P, _I, _I, _I, _I, _I, _P, 's']),
     'um_disc_head_fwd': (_I, [_I, _P, _I, _I, _I, _P, _P, _P, 's']),

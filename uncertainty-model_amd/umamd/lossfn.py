@@ -220,7 +220,7 @@ def _check_levels(preds, pyr):
 
 class TukraLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cfg, n, recon_out, *tensors):
+    def forward(ctx, cfg, n, recon_out, grad, *tensors):
         preds = [_pred_nhwc(t) for t in tensors[:n]]
         pyr = [_f32c(t) for t in tensors[n:2 * n]]
         N, H, W = _check_levels(preds, pyr)
@@ -239,16 +239,20 @@ class TukraLossFn(torch.autograd.Function):
         dl = torch.empty((), dtype=torch.float32, device=dev)
         el = torch.empty_like(dl)
 
-        def launch():
-            call('um_loss_fwd', n, N, H, W, _parr(pyr), _parr(preds), cfg['alpha'],
-                 cfg['loss_type'], cfg['esw'], cfg['ecw'], cfg['w_wssim'], cfg['w_cons'],
-                 cfg['w_smooth'], cfg['w_err'], ptr(ws), ptr(emap), rarr, ptr(out))
-            dl.copy_(out[0])
-            el.copy_(out[1])
-        launch()
+        # a step that will differentiate the loss gets the gradient partials
+        # from the same tile pass (um_loss_fwd gpart); backward = the scatter
+        gpart = None
+        if grad:
+            gpart = [torch.empty((N, H >> i, W >> i, 4), dtype=torch.float32, device=dev)
+                     for i in range(n)]
+        call('um_loss_fwd', n, N, H, W, _parr(pyr), _parr(preds), cfg['alpha'],
+             cfg['loss_type'], cfg['esw'], cfg['ecw'], cfg['w_wssim'], cfg['w_cons'],
+             cfg['w_smooth'], cfg['w_err'], ptr(ws), ptr(emap), rarr, ptr(out), ptr(dl),
+             ptr(el), _parr(gpart) if gpart is not None else None)
         ctx.cfg = cfg
         ctx.n = n
         ctx.geom = (N, H, W)
+        ctx.gpart = gpart
         ctx.save_for_backward(*preds, *pyr)
         ctx.mark_non_differentiable(out, emap)
         return dl, el, out, emap
@@ -260,15 +264,19 @@ class TukraLossFn(torch.autograd.Function):
         sv = ctx.saved_tensors
         preds, pyr = sv[:n], sv[n:2 * n]
         dev = preds[0].device
-        zero = torch.zeros((), dtype=torch.float32, device=dev)
-        gout = torch.stack([(gd if gd is not None else zero).reshape(()).float(),
-                            (ge if ge is not None else zero).reshape(()).float()]).contiguous()
+        # the two upstream gradients stay device scalars (None = 0): no stack
+        gd = gd.float().contiguous() if gd is not None else None
+        ge = ge.float().contiguous() if ge is not None else None
         grads = [torch.empty((N, H >> i, W >> i, 4), dtype=torch.float32, device=dev)
                  for i in range(n)]
+        gpart, ctx.gpart = ctx.gpart, None
         call('um_loss_bwd', n, N, H, W, _parr(pyr), _parr(preds), cfg['alpha'],
              cfg['loss_type'], cfg['esw'], cfg['ecw'], cfg['w_wssim'], cfg['w_cons'],
-             cfg['w_smooth'], cfg['w_err'], ptr(gout), _parr(grads))
-        return (None, None, None, *[g.permute(0, 3, 1, 2) for g in grads], *([None] * n))
+             cfg['w_smooth'], cfg['w_err'], ptr(gd) if gd is not None else None,
+             ptr(ge) if ge is not None else None,
+             _parr(gpart) if gpart is not None else None, _parr(grads))
+        return (None, None, None, None, *[g.permute(0, 3, 1, 2) for g in grads],
+                *([None] * n))
 
 
 def tukra_loss(cfg: dict, preds, pyramid, recon_out=None):
@@ -278,7 +286,9 @@ def tukra_loss(cfg: dict, preds, pyramid, recon_out=None):
     n = len(preds)
     if not 1 <= n <= MAX_LEVELS:
         raise L.UmamdError(f'tukra_loss: {n} scales (1..{MAX_LEVELS})')
-    out = TukraLossFn.apply(cfg, n, recon_out, *preds, *[p.detach() for p in pyramid])
+    # the gradient partials are computed with the forward when it will be differentiated
+    grad = torch.is_grad_enabled() and any(p.requires_grad for p in preds)
+    out = TukraLossFn.apply(cfg, n, recon_out, grad, *preds, *[p.detach() for p in pyramid])
     if recon_out is not None:
         for r in recon_out:
             r._umamd_pending = False
