@@ -730,16 +730,22 @@ def test_tappack(dtype, case, pack):
 
 
 # stride-2 data gradient: the four parity classes in one launch (knob cls4,
-# default) and as four launches, odd and even image sizes (classes of
-# different sizes), 8-channel dy (tap packing), against f64 torch
+# default: 64x64 LDS-DMA tiles when C is a multiple of 64 and K of 64, with
+# per-class split-K; else 256-row register tiles), the register form forced
+# (cls_glds 0), and as four launches; odd and even image sizes (classes of
+# different sizes), both pad parities, 8-channel dy (tap packing), against f64
+# torch
 @pytest.mark.parametrize('case', [(32, 64, 5, 2, 32, 64), (64, 128, 3, 2, 16, 32),
                                   (16, 32, 3, 2, 15, 21), (48, 8, 3, 2, 18, 26),
-                                  (24, 16, 7, 1, 9, 13)])
-@pytest.mark.parametrize('cls4', [0, 1])
-def test_dgrad_stride2_classes(case, cls4):
+                                  (24, 16, 7, 1, 9, 13), (128, 256, 3, 2, 8, 16),
+                                  (64, 64, 3, 2, 15, 21), (64, 64, 5, 2, 12, 20),
+                                  (256, 512, 3, 8, 16, 32)])
+@pytest.mark.parametrize('mode', [(0, 1), (1, 1), (1, 0)])
+def test_dgrad_stride2_classes(case, mode):
     from umamd import functional as U
     from umamd._lib import PAD_ZERO, lib
     C, K, R, N, H, W = case
+    cls4, glds = mode
     pad = (R - 1) // 2
     dtype = torch.bfloat16
     g = torch.Generator().manual_seed(17)
@@ -751,11 +757,13 @@ def test_dgrad_stride2_classes(case, cls4):
     ref = torch.nn.grad.conv2d_input((N, C, H, W), wq, dyq, stride=2, padding=pad)
     _, wT = U._pack(w.to(DEV), C, dtype, wf=False)
     old = lib().um_set_tuning(b'cls4', cls4)
+    old_g = lib().um_set_tuning(b'cls_glds', glds)
     try:
         dx = U._conv_dgrad(_nhwc(dy).to(dtype), wT, (N, H, W, C), K, R, 2, pad, PAD_ZERO)
         torch.cuda.synchronize()
     finally:
         lib().um_set_tuning(b'cls4', old)
+        lib().um_set_tuning(b'cls_glds', old_g)
     assert _rel(_nchw(dx), ref) < 1e-2
 
 

@@ -872,6 +872,18 @@ long um_conv_dgrad_ws(int dtype, int N, int H, int W, int C, int R, int K, int s
   long b = 0;  // the largest parity class (the launches reuse one workspace)
   const int taps = ((R + 1) / 2) * ((R + 1) / 2);
   b = std::max(b, umamd::igemm_ws_bytes(dtype, N * ((H + 1) / 2) * ((W + 1) / 2), C, taps, K));
+  // ... or the four classes in one launch, each with its own slice (both pad
+  // parities: the tap counts per class swap with it)
+  for (int pad = 0; pad < 2; ++pad) {
+    int M[4], tp[4];
+    for (int ay = 0; ay < 2; ++ay)
+      for (int ax = 0; ax < 2; ++ax) {
+        const int r0y = (ay + pad) & 1, r0x = (ax + pad) & 1;
+        M[2 * ay + ax] = N * ((H - ay + 1) / 2) * ((W - ax + 1) / 2);
+        tp[2 * ay + ax] = ((R - r0y + 1) / 2) * ((R - r0x + 1) / 2);
+      }
+    b = std::max(b, umamd::igemm_cls4_ws_bytes(dtype, M, tp, C, K));
+  }
   return b;
 }
 
@@ -1198,7 +1210,7 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
       a.epilogue = UM_EPI_NONE; a.accumulate = accumulate; a.epi_scale = 1.f;
       a.residual = nullptr; a.ldr = 0; a.stats = nullptr;
     }
-  const int one = umamd::igemm_run_cls4(dtype, cls, st);
+  const int one = umamd::igemm_run_cls4(dtype, cls, (float*)ws, ws_bytes, st);
   if (one < 0) return -one;
   if (one == 1) return UM_OK;
   for (auto& a : cls) {

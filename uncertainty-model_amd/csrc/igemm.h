@@ -82,7 +82,9 @@ int igemm_run(int dtype, const IgArgs& a, float* ws, long ws_bytes, hipStream_t 
 
 // the four parity classes of a stride-2 data gradient in one launch: 1 =
 // launched, 0 = not eligible (launch them one by one), < 0 = -error code
-int igemm_run_cls4(int dtype, IgArgs (&as)[4], hipStream_t st);
+int igemm_run_cls4(int dtype, IgArgs (&as)[4], float* ws, long ws_bytes, hipStream_t st);
+// workspace of the 4-class LDS-DMA form (0 when it does not apply or needs none)
+long igemm_cls4_ws_bytes(int dtype, const int (&M)[4], const int (&taps)[4], int NC, int ach);
 
 // reflect data gradients with more input channels than this run as one fold
 // pass, the others as a zero-pad pass + the border-list pass (knob

@@ -635,10 +635,19 @@ __device__ __forceinline__ const bf16_t* gather_ptr(const IgArgs& a, const bf16_
 // NST stages: 3 (48 KB for 64x64, several blocks per CU) or deeper for grids
 // of at most ~1-2 blocks per CU, whose k-loop is pure load latency (knob
 // glds_deep: 6 stages = 5 k-steps in flight, 96 KB).
+// XCD-aware tile order: the dispatcher deals workgroups round-robin over the
+// 8 XCDs, so give each XCD a contiguous range of tiles (shared rows in its L2)
+__device__ __forceinline__ int glds_xcd_tile(int t, int nb) {
+  if (nb < 16) return t;
+  const int xcd = t & 7, q = nb >> 3, rr = nb & 7;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
+}
+
+// one 64-deep-k tile t of ntiles (the launch's own grid, or one parity class's
+// share of a 4-class launch); split index blockIdx.z
 template <int BM, int BN, int NW, bool SPLIT, int MODE, int NST>
-__global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __restrict__ ws,
-                                                              int steps, int steps_per_split,
-                                                              int ntn) {
+__device__ __forceinline__ void glds_tile(const IgArgs& a, float* __restrict__ ws, int steps,
+                                          int steps_per_split, int ntn, int t, int ntiles) {
   constexpr bool CLS = MODE == 1;
   static_assert(MODE != 2, "the reflect fold gathers through registers");
   constexpr int BK = 64, WM = NW == 8 ? 4 : 2, WN = 2;
@@ -654,21 +663,13 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  int t = blockIdx.x;
-  {
-    const int nb = gridDim.x;
-    if (nb >= 16) {
-      const int xcd = t & 7, q = nb >> 3, rr = nb & 7;
-      t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (t >> 3);
-    }
-  }
   // row-major tile order (an XCD's contiguous t range shares row tiles, so
   // reads a slice of A and all of B) unless the weights outweigh the
   // gathered image (deep layers): then column-major, each XCD's L2 holds a
   // slice of B and the whole (small) A
   int bm, bn;
   if (a.colmajor) {
-    const int ntm = gridDim.x / ntn;
+    const int ntm = ntiles / ntn;
     bn = (t / ntm) * BN;
     bm = (t - (t / ntm) * ntm) * BM;
   } else {
@@ -784,16 +785,56 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
   static_assert(WM * WN == NW, "waves");
 }
 
+template <int BM, int BN, int NW, bool SPLIT, int MODE, int NST>
+__global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __restrict__ ws,
+                                                              int steps, int steps_per_split,
+                                                              int ntn) {
+  glds_tile<BM, BN, NW, SPLIT, MODE, NST>(a, ws, steps, steps_per_split, ntn,
+                                          glds_xcd_tile(blockIdx.x, gridDim.x), gridDim.x);
+}
+
+// The four parity classes of a stride-2 data gradient as ONE launch of 64x64
+// LDS-DMA tiles: class c owns tiles [start[c], start[c+1]) and splits
+// [0, splits[c]) of the z range, with its own workspace slice.  The class is
+// chosen by uniform branches on kernel arguments (indexing the four by-value
+// IgArgs through a pointer spilled ~200 SGPRs in the register-path variant).
+template <bool SPLIT, int NST>
+__global__ void __launch_bounds__(512) igemm_glds_cls4_kernel(IgArgs a0, IgArgs a1, IgArgs a2,
+                                                               IgArgs a3, int4 start, int4 steps,
+                                                               int4 per, int4 splits, int4 ntiles,
+                                                               int ntn, float* __restrict__ ws,
+                                                               long4 wsoff) {
+  const int t = glds_xcd_tile(blockIdx.x, gridDim.x);
+  const int z = blockIdx.z;
+  if (t < start.y) {
+    if (z < splits.x)
+      glds_tile<64, 64, 8, SPLIT, 1, NST>(a0, ws + wsoff.x, steps.x, per.x, ntn, t - start.x,
+                                          ntiles.x);
+  } else if (t < start.z) {
+    if (z < splits.y)
+      glds_tile<64, 64, 8, SPLIT, 1, NST>(a1, ws + wsoff.y, steps.y, per.y, ntn, t - start.y,
+                                          ntiles.y);
+  } else if (t < start.w) {
+    if (z < splits.z)
+      glds_tile<64, 64, 8, SPLIT, 1, NST>(a2, ws + wsoff.z, steps.z, per.z, ntn, t - start.z,
+                                          ntiles.z);
+  } else {
+    if (z < splits.w)
+      glds_tile<64, 64, 8, SPLIT, 1, NST>(a3, ws + wsoff.w, steps.w, per.w, ntn, t - start.w,
+                                          ntiles.w);
+  }
+}
+
 // sum the split-K partials and apply the epilogue.  Block = a.stats_rows rows x
 // 64 columns: thread (g, lane) owns columns 4g..4g+3 and rows lane, lane+16, ...
 constexpr int EPI_COLS = 64;
 template <typename T, int MODE>
-__global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const float* __restrict__ ws,
-                                                               int splits) {
+__device__ __forceinline__ void splitk_epi_rows(const IgArgs& a, const float* __restrict__ ws,
+                                                int splits, int bx) {
   __shared__ float red[16][16][8];
   const int g = threadIdx.x & 15, lane = threadIdx.x >> 4;
   const int n = blockIdx.y * EPI_COLS + g * 4;  // NC % 4 == 0 (host-checked)
-  const long m0 = (long)blockIdx.x * a.stats_rows;
+  const long m0 = (long)bx * a.stats_rows;
   const long m1 = min((long)a.M, m0 + a.stats_rows);
   const long zs = (long)a.M * a.NC;
   const bool act = n < a.NC;
@@ -846,7 +887,7 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const fl
 #pragma unroll
       for (int e = 0; e < 4; ++e) { sm[e] += red[l][g][e]; sq[e] += red[l][g][4 + e]; }
     if (!a.stat_slots) {
-      float* o = a.stats + ((long)blockIdx.x * a.NC + n) * 2;
+      float* o = a.stats + ((long)bx * a.NC + n) * 2;
 #pragma unroll
       for (int e = 0; e < 4; ++e) { o[2 * e] = sm[e]; o[2 * e + 1] = sq[e]; }
     }
@@ -859,9 +900,30 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const fl
     __syncthreads();
     const int c0 = blockIdx.y * EPI_COLS;
     stat_slots_count(reinterpret_cast<double*>(a.stats), a.NC, a.M);
-    stat_slots_add_row(reinterpret_cast<double*>(a.stats), blockIdx.x, a.NC, c0,
+    stat_slots_add_row(reinterpret_cast<double*>(a.stats), bx, a.NC, c0,
                        min(EPI_COLS, a.NC - c0), [&](int i) { return tot[i]; });
   }
+}
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const float* __restrict__ ws,
+                                                               int splits) {
+  splitk_epi_rows<T, MODE>(a, ws, splits, blockIdx.x);
+}
+
+// the split-K sums of igemm_glds_cls4_kernel: class c owns row blocks
+// [rstart[c], rstart[c+1])
+template <typename T>
+__global__ void __launch_bounds__(256) splitk_epilogue_cls4_kernel(IgArgs a0, IgArgs a1, IgArgs a2,
+                                                                    IgArgs a3, int4 rstart,
+                                                                    int4 splits,
+                                                                    const float* __restrict__ ws,
+                                                                    long4 wsoff) {
+  const int b = blockIdx.x;
+  if (b < rstart.y) splitk_epi_rows<T, 1>(a0, ws + wsoff.x, splits.x, b - rstart.x);
+  else if (b < rstart.z) splitk_epi_rows<T, 1>(a1, ws + wsoff.y, splits.y, b - rstart.y);
+  else if (b < rstart.w) splitk_epi_rows<T, 1>(a2, ws + wsoff.z, splits.z, b - rstart.z);
+  else splitk_epi_rows<T, 1>(a3, ws + wsoff.w, splits.w, b - rstart.w);
 }
 
 struct Plan {
@@ -878,6 +940,7 @@ struct Knobs {
   int xcd_col;
   int tappack;
   int cls4;
+  int cls_glds;
   int pad_dgrad;
   int fold_split_nc;
   int halo_max_nc;
@@ -931,6 +994,12 @@ struct Knobs {
     tappack = env("tappack", 1);
     // the four parity classes of a stride-2 data gradient as one launch
     cls4 = env("cls4", 1);
+    // the four parity classes of a stride-2 data gradient as one launch of
+    // 64x64 LDS-DMA tiles (NC a multiple of 64) instead of 256-row register
+    // tiles: 64x128 C64 K128 59 -> 28 us, 32x64 C128 K256 50 -> 24, 16x32
+    // C256 K512 57 -> 28 (MI355X, tools/gpu_s2_micro.sh); at NC = 32 the
+    // half-empty 64-column tiles lost (77 -> 84 us)
+    cls_glds = env("cls_glds", 1);
     // reflect data gradient as a zero-pad transposed conv onto the padded
     // input + a fold pass (0 off, 1 the wide layers, 2 all)
     pad_dgrad = env("pad_dgrad", 1);
@@ -1186,10 +1255,122 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
   return dispatch_tiles<float>(a, p, ws, st);
 }
 
+// the four parity classes of a stride-2 data gradient on 64x64 LDS-DMA tiles
+// in one launch (+ one split-K epilogue launch): per-class tile ranges,
+// per-class split counts (the split target over the classes' tiles together,
+// each class capped by its own k-steps) and workspace slices
+struct Cls4Plan {
+  int ntn;
+  int start[5], ntiles[4], steps[4], per[4], splits[4];
+  long wsoff[4];  // f32 elements
+  long ws;        // bytes (0: no split)
+};
+
+static Cls4Plan cls4_glds_plan(const int (&M)[4], const int (&taps)[4], int NC, int ach,
+                               long ws_bytes) {
+  const Knobs& kn = knobs();
+  Cls4Plan p{};
+  p.ntn = ceil_div(NC, 64);
+  long tiles = 0, rows = 0;
+  for (int c = 0; c < 4; ++c) {
+    p.ntiles[c] = ceil_div(M[c], 64) * p.ntn;
+    p.start[c + 1] = p.start[c] + p.ntiles[c];
+    p.steps[c] = taps[c] * ceil_div(ach, 64);
+    tiles += p.ntiles[c];
+    rows += M[c];
+  }
+  long sp = 1;
+  if (tiles < kn.glds_split_below && NC % 4 == 0 && rows > 0) {
+    sp = (kn.glds_split_target + tiles - 1) / tiles;
+    sp = std::min<long>(sp, (32l << 20) / (rows * NC * 4));
+    if (ws_bytes >= 0) sp = std::min<long>(sp, ws_bytes / (rows * NC * 4));
+  }
+  long off = 0;
+  bool split = false;
+  for (int c = 0; c < 4; ++c) {
+    long sc = sp >= 2 ? std::min<long>(sp, p.steps[c] / kn.split_minsteps) : 1;
+    if (sc < 1) sc = 1;
+    p.per[c] = std::max(1, ceil_div(p.steps[c], sc));
+    p.splits[c] = std::max(1, ceil_div(p.steps[c], p.per[c]));
+    split |= p.splits[c] > 1;
+    p.wsoff[c] = off;
+    off += (long)p.splits[c] * M[c] * NC;
+  }
+  p.ws = split ? off * 4 : 0;
+  return p;
+}
+
+static bool cls4_glds_ok(int dtype, const IgArgs (&as)[4]) {
+  if (!knobs().cls4 || !knobs().cls_glds || !(knobs().glds & 1) || dtype != UM_BF16) return false;
+  for (const auto& a : as)
+    if (a.M <= 0 || a.NC % 64 || a.ach % 64 || a.pmode != IG_PAD_ZERO) return false;
+  return true;
+}
+
+long igemm_cls4_ws_bytes(int dtype, const int (&M)[4], const int (&taps)[4], int NC, int ach) {
+  if (!knobs().cls4 || !knobs().cls_glds || dtype != UM_BF16 || NC % 64 || ach % 64) return 0;
+  return cls4_glds_plan(M, taps, NC, ach, -1).ws;
+}
+
+static int run_cls4_glds(IgArgs (&as)[4], float* ws, long ws_bytes, hipStream_t st) {
+  int M[4], taps[4];
+  for (int c = 0; c < 4; ++c) {
+    M[c] = as[c].M;
+    taps[c] = as[c].R * as[c].Rx;
+  }
+  const int NC = as[0].NC, ach = as[0].ach;
+  const Cls4Plan p = cls4_glds_plan(M, taps, NC, ach, ws ? ws_bytes : 0);
+  const bool split = p.ws > 0;
+  int zmax = 1;
+  int rstart[5] = {0, 0, 0, 0, 0};
+  for (int c = 0; c < 4; ++c) {
+    IgArgs& a = as[c];
+    a.stats_rows = igemm_stats_rows(a.M, a.NC);
+    const int xc = knobs().xcd_col;
+    const long abytes = (long)a.M * a.ach, bbytes = (long)a.NC * a.R * a.Rx * a.ach;
+    a.colmajor = xc == 2 || (xc == 1 && bbytes > abytes);
+    a.tappack = 0;
+    zmax = std::max(zmax, p.splits[c]);
+    rstart[c + 1] = rstart[c] + ceil_div(a.M, a.stats_rows);
+  }
+  const dim3 grid(p.start[4], 1, split ? zmax : 1);
+  const int4 s4 = make_int4(p.start[0], p.start[1], p.start[2], p.start[3]);
+  const int4 k4 = make_int4(p.steps[0], p.steps[1], p.steps[2], p.steps[3]);
+  const int4 per4 = make_int4(p.per[0], p.per[1], p.per[2], p.per[3]);
+  const int4 sp4 = split ? make_int4(p.splits[0], p.splits[1], p.splits[2], p.splits[3])
+                         : make_int4(1, 1, 1, 1);
+  const int4 nt4 = make_int4(p.ntiles[0], p.ntiles[1], p.ntiles[2], p.ntiles[3]);
+  const long4 off4 = make_long4(p.wsoff[0], p.wsoff[1], p.wsoff[2], p.wsoff[3]);
+  const long blocks = (long)p.start[4] * (split ? zmax : 1);
+  const bool deep = knobs().glds_deep > 3 && blocks <= knobs().glds_deep_blocks;
+#define UM_GC4(SP_, NST_)                                                                         \
+  hipLaunchKernelGGL((igemm_glds_cls4_kernel<SP_, NST_>), grid, dim3(512), 0, st, as[0], as[1],  \
+                     as[2], as[3], s4, k4, per4, sp4, nt4, p.ntn, ws, off4)
+  if (split && deep) UM_GC4(true, 6);
+  else if (split) UM_GC4(true, 3);
+  else if (deep) UM_GC4(false, 6);
+  else UM_GC4(false, 3);
+#undef UM_GC4
+  if (split) {
+    const int4 r4 = make_int4(rstart[0], rstart[1], rstart[2], rstart[3]);
+    hipLaunchKernelGGL(splitk_epilogue_cls4_kernel<bf16_t>, dim3(rstart[4], ceil_div(NC, EPI_COLS)),
+                       dim3(256), 0, st, as[0], as[1], as[2], as[3], r4, sp4, (const float*)ws,
+                       off4);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("igemm_run_cls4: %s", hipGetErrorString(e));
+    return -UM_ERR_HIP;
+  }
+  return 1;
+}
+
 // the four parity classes of a stride-2 data gradient in one launch (bf16,
-// 256-row tiles); returns 1 when launched, 0 when the caller should launch
-// the classes one by one, or an error code < 0
-int igemm_run_cls4(int dtype, IgArgs (&as)[4], hipStream_t st) {
+// 256-row register tiles when the LDS-DMA form does not apply); returns 1
+// when launched, 0 when the caller should launch the classes one by one, or
+// an error code < 0
+int igemm_run_cls4(int dtype, IgArgs (&as)[4], float* ws, long ws_bytes, hipStream_t st) {
+  if (cls4_glds_ok(dtype, as)) return run_cls4_glds(as, ws, ws_bytes, st);
   if (!knobs().cls4 || dtype != UM_BF16) return 0;
   for (auto& a : as)
     if (a.M <= 0) return 0;
@@ -1249,6 +1430,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "xcd_col")) f = &k.xcd_col;
   else if (!strcmp(key, "tappack")) f = &k.tappack;
   else if (!strcmp(key, "cls4")) f = &k.cls4;
+  else if (!strcmp(key, "cls_glds")) f = &k.cls_glds;
   else if (!strcmp(key, "pad_dgrad")) f = &k.pad_dgrad;
   else if (!strcmp(key, "glds_deep_blocks")) f = &k.glds_deep_blocks;
   else if (!strcmp(key, "fold_split_nc")) f = &k.fold_split_nc;

@@ -99,6 +99,9 @@ class CapturedTrainStep:
         if os.environ.get('UMAMD_WGRAD_OVERLAP', '1') != '0':
             self.overlap = overlap.WgradStream(p for p in model.parameters() if p.requires_grad)
         self.left = left.detach().clone().contiguous()
+        # the backward's seed d total / d (disp_loss, error_loss) = (1, 1),
+        # made once: no add and no ones-fill launch inside the step
+        self._seed = torch.ones((), dtype=torch.float32, device=left.device)
         self.right = right.detach().clone().contiguous()
         cur = torch.cuda.current_stream()
         side = stream if stream is not None else torch.cuda.Stream()
@@ -187,7 +190,9 @@ class CapturedTrainStep:
         disp_loss, error_loss = self.loss_function(pyramid, disparities, recon, 0, None)
 
         def backward():
-            (disp_loss + error_loss).backward()
+            seeds = tuple(self._seed if t.dtype == self._seed.dtype and t.dim() == 0
+                          else torch.ones_like(t) for t in (disp_loss, error_loss))
+            torch.autograd.backward((disp_loss, error_loss), seeds)
         if self.overlap is None:
             if self._buckets is not None:
                 self._buckets.arm()
