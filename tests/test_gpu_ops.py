@@ -409,6 +409,14 @@ def test_conv_large(dtype, case):
     (256, 512, 3, 1, 'zero', 4, 8),
     (32, 96, 1, 1, 'zero', 12, 40),
     (128, 256, 3, 2, 'zero', 9, 17),
+    # 1x1 VALU streaming pass (K, C in {8..64}, K*C <= 512; the rest on the
+    # MFMA tiles), ragged pixel counts
+    (8, 32, 1, 1, 'zero', 32, 64),
+    (64, 32, 1, 1, 'zero', 16, 40),
+    (32, 32, 1, 1, 'zero', 9, 17),
+    (16, 8, 1, 1, 'zero', 5, 7),
+    (32, 64, 1, 1, 'zero', 10, 30),
+    (64, 64, 1, 1, 'zero', 8, 24),
 ])
 def test_wgrad(case):
     from umamd import functional as U

@@ -400,6 +400,98 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgradArgs a) {
       }
 }
 
+// ---- 1x1 weight gradient of narrow layers (K, C in {8, 16, 32, 64}, K*C <=
+// W1_MAX), a VALU streaming pass: lane (kb, cb) of the L = K/8 * C/8 lanes
+// that share a pixel owns the 8x8 block dW[kb*8 .. +7][cb*8 .. +7]; a wave
+// covers 64/L pixels per step and reads each pixel's dy and x rows once, as
+// 16-byte loads (HBM-bound; the MFMA tiles above are 128 columns wide, 1/16
+// full at C = 8).  One f32 partial [K][C] per workgroup into the slabs.
+// MI355X (tools/conv_micro.py, wgrad + slab reduce): 256x512 C8 K32 120 ->
+// 27 us; past K*C = 512 the FMAs per pixel make it VALU/latency-bound
+// (128x256 C32 K32 41 -> 37, C64 K32 41 -> 63 us), so those keep the MFMA tiles.
+constexpr int W1_NT = 256, W1_MAX = 512;
+
+__device__ __forceinline__ void bf16x8_to_f32(const uint4& u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+template <int L>
+__global__ void __launch_bounds__(W1_NT) wgrad_1x1_kernel(WgradArgs a) {
+  constexpr int PW = 64 / L, U = 4;
+  __shared__ float red[W1_MAX];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = lane / L, sub = lane - (lane / L) * L;
+  const int ncb = a.C / 8;
+  const int kb = sub / ncb, cb = sub - (sub / ncb) * ncb;
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(a.x) + cb * 8;
+  const bf16_t* __restrict__ DY = reinterpret_cast<const bf16_t*>(a.dy) + kb * 8;
+  float acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+  const long step = (long)gridDim.x * (W1_NT / 64) * PW;
+  long p = ((long)blockIdx.x * (W1_NT / 64) + wave) * PW + slot;
+  for (; p < a.M; p += U * step) {
+    uint4 dv[U], xv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long q = p + u * step;
+      const bool ok = q < a.M;
+      dv[u] = ok ? *reinterpret_cast<const uint4*>(DY + q * a.ldy) : make_uint4(0, 0, 0, 0);
+      xv[u] = ok ? *reinterpret_cast<const uint4*>(X + q * a.ldx) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float d[8], x[8];
+      bf16x8_to_f32(dv[u], d);
+      bf16x8_to_f32(xv[u], x);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(d[i], x[j], acc[i][j]);
+    }
+  }
+  // sum the wave's pixel slots (lanes sub, sub + L, ...), then the 4 waves in turn
+#pragma unroll
+  for (int o = L; o < 64; o <<= 1)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] += __shfl_xor(acc[i][j], o, 64);
+  const int KC = a.K * a.C;
+  for (int w = 0; w < W1_NT / 64; ++w) {
+    if (wave == w && slot == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float* r = &red[(kb * 8 + i) * a.C + cb * 8 + j];
+          *r = (w == 0 ? 0.f : *r) + acc[i][j];
+        }
+    }
+    __syncthreads();
+  }
+  float* out = a.slabs + (long)blockIdx.x * KC;
+  for (int i = threadIdx.x; i < KC; i += W1_NT) out[i] = red[i];
+}
+
+static bool wgrad_1x1_ok(int dtype, int C, int K, int R, int stride, int pad, int ldx, int ldy) {
+  auto p2 = [](int v) { return v == 8 || v == 16 || v == 32 || v == 64; };
+  return dtype == UM_BF16 && umamd::tuning_env("w1x1", 1) && R == 1 && stride == 1 && pad == 0 &&
+         p2(C) && p2(K) && K * C <= W1_MAX && ldx % 8 == 0 && ldy % 8 == 0;
+}
+
+// workgroups (= slabs) of the 1x1 pass: ~4 pixel steps per wave at least
+static int wgrad_1x1_blocks(long M) {
+  return (int)std::max<long>(1, std::min<long>(512, (M + 2047) / 2048));
+}
+
 template <int BM>
 int launch_wgrad_bf16(const WgradArgs& a, int splits, hipStream_t st) {
   dim3 grid(ceil_div(a.K, BM), ceil_div(a.RRC, 128), splits);
@@ -1239,6 +1331,7 @@ static int generic_wgrad_splits(int M, int K, int RRC, bool tr) {
 
 int um_conv_wgrad_splits(int dtype, int N, int H, int W, int C, int ldx, int K, int R,
                          int stride, int pad, int pad_mode, int P, int Q, int ldy) {
+  if (wgrad_1x1_ok(dtype, C, K, R, stride, pad, ldx, ldy)) return wgrad_1x1_blocks((long)N * P * Q);
   if (dtype == UM_BF16 && ldx % 8 == 0 && ldy % 8 == 0) {
     const int h = umamd::hwgrad_splits(N, H, W, C, ldx, K, R, stride, pad,
                                        pad_mode == UM_PAD_REFLECT, P, Q, ldy);
@@ -1264,7 +1357,7 @@ int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* 
     umamd::set_error("um_conv2d_wgrad: halo kernel launch failed");
     return UM_ERR_HIP;
   }
-  if (dtype == UM_BF16 && K > 32) {
+  if (dtype == UM_BF16 && K > 32 && !wgrad_1x1_ok(dtype, C, K, R, stride, pad, ldx, ldy)) {
     UM_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0, "um_conv2d_wgrad: ld %% 8");
     return umamd::wgrad_tr_run(x, N, H, W, C, ldx, K, R, stride, pad, pad_mode == UM_PAD_REFLECT,
                                P, Q, dy, ldy, slabs, splits, st);
@@ -1275,6 +1368,20 @@ int um_conv2d_wgrad(int dtype, int N, int H, int W, int C, int ldx, const void* 
   a.x = x; a.dy = dy; a.slabs = slabs;
   a.M = N * P * Q; a.RRC = R * R * C;
   a.m_per_split = ceil_div(ceil_div(a.M, splits), WBK) * WBK;
+  if (wgrad_1x1_ok(dtype, C, K, R, stride, pad, ldx, ldy)) {
+    const int L = (K / 8) * (C / 8);
+    const dim3 grid(splits);
+    switch (L) {
+      case 1: hipLaunchKernelGGL(wgrad_1x1_kernel<1>, grid, dim3(W1_NT), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(wgrad_1x1_kernel<2>, grid, dim3(W1_NT), 0, st, a); break;
+      case 4: hipLaunchKernelGGL(wgrad_1x1_kernel<4>, grid, dim3(W1_NT), 0, st, a); break;
+      case 8: hipLaunchKernelGGL(wgrad_1x1_kernel<8>, grid, dim3(W1_NT), 0, st, a); break;
+      case 16: hipLaunchKernelGGL(wgrad_1x1_kernel<16>, grid, dim3(W1_NT), 0, st, a); break;
+      default: hipLaunchKernelGGL(wgrad_1x1_kernel<32>, grid, dim3(W1_NT), 0, st, a); break;
+    }
+    UM_LAUNCH_CHECK();
+    return UM_OK;
+  }
   if (dtype == UM_BF16) {
     UM_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0, "um_conv2d_wgrad: ld %% 8");
     const int bm = wgrad_bm(K);
