@@ -260,6 +260,9 @@ struct HwPlan {
   size_t lds;
 };
 
+int blocks_per_cu(const HwPlan& h);
+int cu_count();
+
 HwPlan plan(int N, int H, int W, int C, int ldx, int K, int R, int stride, int pad, int reflect,
             int P, int Q, int ldy) {
   HwPlan h{};
@@ -310,9 +313,13 @@ HwPlan plan(int N, int H, int W, int C, int ldx, int K, int R, int stride, int p
   a.tiles_y = (P + a.TH - 1) / a.TH;
   a.ntiles = N * a.tiles_x * a.tiles_y;
   a.taps_per_group = 8 * tpw;
-  // splits: ~2 blocks per CU overall, >= 2 tiles per block, <= 64 MB of slabs
+  // splits: ONE round of resident workgroups (occupancy x CUs; the wide
+  // instances hold ~200 VGPRs, one workgroup per CU: 327 workgroups of the
+  // 128x256 7x7 layer ran as 1.3 rounds), >= 2 tiles per block, <= 64 MB of
+  // slabs
   const long slab = (long)K * RR * C * 4;
-  long sp = std::max<long>(1, 512 / h.groups);
+  const long resident = (long)std::max(1, blocks_per_cu(h)) * cu_count();
+  long sp = std::max<long>(1, resident / h.groups);
   sp = std::min<long>(sp, (a.ntiles + 1) / 2);
   sp = std::min<long>(sp, std::max<long>(1, (64l << 20) / slab));
   h.splits = (int)std::max<long>(1, sp);
@@ -357,6 +364,42 @@ int dispatch(const HwPlan& h, float* slabs, hipStream_t st) {
 bool exists(const HwPlan& h) {
   HW_INSTANCES(HW_EXISTS)
   return false;
+}
+
+template <int KT, int CT, int TPW>
+int occupancy_hw(size_t lds) {
+  const void* f = reinterpret_cast<const void*>(&hwgrad_kernel<KT, CT, TPW>);
+  (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 512, lds) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 1;
+  }
+  return n;
+}
+
+#define HW_OCC(kt, ct, tpw) \
+  if (h.KT == kt && h.CT == ct && h.TPW == tpw) return occupancy_hw<kt, ct, tpw>(h.lds);
+
+// resident 512-thread workgroups per CU of the plan's instance (VGPRs, LDS)
+int blocks_per_cu(const HwPlan& h) {
+  HW_INSTANCES(HW_OCC)
+  return 1;
+}
+
+int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        v > 0)
+      n = v;
+    else
+      n = 256;
+    (void)hipGetLastError();
+  }
+  return n;
 }
 
 }  // namespace
