@@ -1314,13 +1314,31 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
 
 static int wgrad_bm(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
 
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    n = (hipGetDevice(&dev) == hipSuccess &&
+         hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            ? v
+            : 256;
+    (void)hipGetLastError();
+  }
+  return n;
+}
+
 static int generic_wgrad_splits(int M, int K, int RRC, bool tr) {
   // tiles of the bf16 kernels (the f32 kernel uses 64x64 tiles; same split count)
   const int bm = tr ? umamd::wgrad_tr_bm(K) : wgrad_bm(K);
   const long tiles = (long)ceil_div(K, bm) * ceil_div(RRC, 128);
-  // target workgroups over the chip (UMAMD_TUNING wsplit_blocks for sweeps)
-  static const long target = umamd::tuning_env("wsplit_blocks", 768);
-  long splits = (target + tiles - 1) / tiles;
+  // target workgroups over the chip: for the transposed-read kernel ONE round
+  // of resident workgroups (occupancy x CUs; 768 was 1.5 rounds of the
+  // 2-per-CU instance), else 768 (UMAMD_TUNING wsplit_blocks for sweeps)
+  static const long fixed = umamd::tuning_env("wsplit_blocks", 0);
+  const long target = fixed > 0 ? fixed
+                      : tr      ? (long)umamd::wgrad_tr_blocks_per_cu(K) * cu_count()
+                                : 768;
+  long splits = tr && fixed <= 0 ? std::max<long>(1, target / tiles) : (target + tiles - 1) / tiles;
   const long max_by_m = (M + 255) / 256;  // >= 256 pixels per split
   if (splits > max_by_m) splits = max_by_m;
   const long max_by_bytes = (32l << 20) / ((long)K * RRC * 4);  // <= 32 MB of slabs

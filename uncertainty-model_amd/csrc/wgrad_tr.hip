@@ -263,6 +263,23 @@ int wgrad_tr_tbk() {
   return v;
 }
 
+// resident 256-thread workgroups per CU of the instance wgrad_tr_run picks for K
+int wgrad_tr_blocks_per_cu(int K) {
+  const int bm = wgrad_tr_bm(K), tbk = wgrad_tr_tbk();
+  const void* f = nullptr;
+#define UM_WTRF(BM_, TBK_) \
+  if (bm == BM_ && tbk == TBK_) f = reinterpret_cast<const void*>(&wgrad_tr_kernel<BM_, TBK_>);
+  UM_WTRF(64, 32) UM_WTRF(64, 64) UM_WTRF(64, 128)
+  UM_WTRF(128, 32) UM_WTRF(128, 64) UM_WTRF(128, 128)
+#undef UM_WTRF
+  int n = 0;
+  if (f == nullptr || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 1;
+  }
+  return std::max(1, n);
+}
+
 int wgrad_tr_run(const void* x, int N, int H, int W, int C, int ldx, int K, int R, int stride,
                  int pad, int reflect, int P, int Q, const void* dy, int ldy, float* slabs,
                  int splits, hipStream_t st) {
