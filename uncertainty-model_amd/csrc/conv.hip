@@ -1585,7 +1585,43 @@ __device__ __forceinline__ void pack_tile(const um_pack_desc& d, int t, float* t
   const int nct = (d.C + CT - 1) / CT;
   const int k0 = (t / nct) * PK, c0 = (t % nct) * CT;
   const int K2 = d.split ? 2 * d.K : d.K;  // packed rows (split: [hi | lo])
-  for (int i = threadIdx.x; i < n; i += 256) {
+  // whole channel block present and no segment map: each k row of the tile is
+  // one contiguous, 16-byte aligned run of CT*RR floats -> float4 loads, four
+  // independent ones in flight per thread (the scalar gather below ran the
+  // 180 MB repack at 1.8 TB/s)
+  const bool vec = d.nseg <= 0 && c0 + CT <= d.Creal && (d.Creal * RR) % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(d.w) & 15) == 0;
+  if (vec) {
+    constexpr int Q4 = per_k / 4;  // float4 per k row
+    static_assert(per_k % 4 == 0, "k row of float4");
+    constexpr int N4 = PK * Q4, U = 4;
+    for (int i0 = threadIdx.x; i0 < N4; i0 += U * 256) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * 256;
+        const int kk = i / Q4, q = i - kk * Q4;
+        const int k2 = k0 + kk;
+        const int k = k2 < d.K ? k2 : k2 - d.K;
+        v[u] = (i < N4 && k2 < K2)
+                   ? *reinterpret_cast<const float4*>(d.w + ((long)k * d.Creal + c0) * RR + 4 * q)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * 256;
+        if (i >= N4) break;
+        const int kk = i / Q4, q = i - kk * Q4;
+        const bool lo = k0 + kk >= d.K;
+        float* t = tile + kk * ldt + 4 * q;
+        t[0] = split_part<T>(v[u].x, lo);
+        t[1] = split_part<T>(v[u].y, lo);
+        t[2] = split_part<T>(v[u].z, lo);
+        t[3] = split_part<T>(v[u].w, lo);
+      }
+    }
+  }
+  for (int i = vec ? n : threadIdx.x; i < n; i += 256) {
     const int kk = i / per_k, rem = i - kk * per_k;
     const int cc = rem / RR, tap = rem - cc * RR;
     const int k2 = k0 + kk, c = c0 + cc;
