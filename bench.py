@@ -181,7 +181,10 @@ def loss_pixels(n, N, H, W):
 # also writes the 4 gradient channels.  SURVEY 8d prices the whole fused
 # stack (fwd + bwd as one pass) at 56 B/px all-f32.
 LOSS_BYTES_PER_PX = {'um_loss_fwd': 4 * (6 + 4), 'um_loss_bwd': 4 * (6 + 4 + 4)}
-LOSS_KERNELS = {'um_loss_fwd': 'loss_fwd_kernel', 'um_loss_bwd': 'loss_bwd_kernel'}
+# (a differentiated step: the forward launch computes the loss terms and the
+# gradient partials, the backward is the scatter that completes them)
+LOSS_KERNELS = {'um_loss_fwd': 'loss_grad_kernel<true> + loss_reduce_kernel',
+                'um_loss_bwd': 'loss_scatter_kernel<true>'}
 
 
 CONV_ENTRIES = {
@@ -190,27 +193,6 @@ CONV_ENTRIES = {
     'um_conv2d_dgrad': 'igemm_kernel<T,...,CLS> (parity classes) / halo_conv_kernel<R,BN,1,...>',
     'um_conv2d_wgrad': 'hwgrad (wgrad_halo) / wgrad_tr_kernel + wgrad_reduce',
 }
-
-
-HEAD_ENTRIES = {'um_head_fwd': 'head_fwd_kernel', 'um_head_dgrad': 'head_dgrad_kernel',
-                'um_head_wgrad': 'head_wgrad_kernel'}
-
-
-def head_min_bytes(name, a):
-    """compulsory HBM bytes of a disparity-head launch (csrc/head.hip):
-    forward reads x (Cp channels) and writes 4 f32; the data gradient reads
-    dl (4 of its 8 channels) and writes dx (read-modify-write when
-    accumulating).  x / dl / dx in the activation dtype."""
-    es = 4 if a[0] == 0 else 2
-    N, H, W = a[1], a[2], a[3]
-    px = N * H * W
-    if name == 'um_head_wgrad':  # reads x and dl (4 of its 8 channels)
-        return px * ((a[4] + 7) // 8 * 8 * es + 4 * es)
-    Cp = a[5]
-    if name == 'um_head_fwd':
-        return px * (Cp * es + 16)
-    acc = a[11]
-    return px * (4 * es + Cp * es * (2 if acc else 1))
 
 
 def conv_min_bytes(name, a):
@@ -262,7 +244,7 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     the dominant kernel.  Conv work = algorithmic FLOPs with the real channel
     counts (2*N*P*Q*K*R*R*C per pass, attached at each call site)."""
     from umamd import _lib
-    rec = _lib.Recorder(set(CONV_ENTRIES) | set(LOSS_KERNELS) | set(HEAD_ENTRIES))
+    rec = _lib.Recorder(set(CONV_ENTRIES) | set(LOSS_KERNELS))
     with rec:
         step(m, lf, opt, left, right, scale)
     torch.cuda.synchronize()
@@ -271,18 +253,6 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
         groups.setdefault(name, []).append((args, ms, work))
     peak = BF16_PEAK_TFLOPS if dtype == 'bf16' else F32_PEAK_TFLOPS
     table = {}
-    heads = {}
-    for name in HEAD_ENTRIES:
-        items = groups.pop(name, [])
-        if not items:
-            continue
-        tot_ms = sum(ms for _, ms, _ in items)
-        b = sum(head_min_bytes(name, a) for a, _, _ in items)
-        ach = b / (tot_ms * 1e-3) / 1e9
-        heads[name] = {'kernel': HEAD_ENTRIES[name], 'bound': 'hbm', 'launches_per_step': len(items),
-                       'total_ms_per_step': round(tot_ms, 4), 'achieved': round(ach, 1),
-                       'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(ach / HBM_PEAK_GBS, 4),
-                       'per_launch_us': [round(ms * 1e3, 1) for _, ms, _ in items]}
     for name, items in groups.items():
         tot_ms = sum(ms for _, ms, _ in items)
         if name in LOSS_KERNELS:
@@ -331,7 +301,6 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
                                                   'launches_per_step', 'total_ms_per_step')}
                          for k, v in table.items()}
     out['conv1x1'] = conv1x1_report(groups, peak)
-    out['disp_heads'] = heads or None  # the 4-output heads (VALU, HBM-bound)
     if all(k in groups for k in LOSS_KERNELS):
         # the fused loss stack (forward + backward launches) priced as SURVEY
         # 8d does: 56 B/px all-f32 (6 image + 4 prediction reads, 4 gradient
@@ -340,7 +309,7 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
         px = loss_pixels(a0[0], a0[1], a0[2], a0[3])
         t = table['um_loss_fwd']['total_ms_per_step'] + table['um_loss_bwd']['total_ms_per_step']
         ach = 56 * px / (t * 1e-3) / 1e9
-        out['loss_stack'] = {'kernels': 'loss_fwd_kernel + loss_bwd_kernel', 'bound': 'hbm',
+        out['loss_stack'] = {'kernels': ' + '.join(LOSS_KERNELS.values()), 'bound': 'hbm',
                              'bytes_per_px': 56, 'pixels': px, 'ms_per_step': round(t, 4),
                              'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                              'frac': round(ach / HBM_PEAK_GBS, 4)}
