@@ -1011,9 +1011,10 @@ __global__ void __launch_bounds__(256) conv1x1_up2_kernel(
     const T* __restrict__ x, int ldx, const T* __restrict__ wf, const float* __restrict__ bias,
     int K, int H, int W, long M, TY* __restrict__ y, int ldy, const TY* __restrict__ z, int h,
     int w, int ldz, double* __restrict__ slots) {
-  extern __shared__ float sm[];  // W [K][C] f32, then the statistics [4 waves][K][2]
+  extern __shared__ float sm[];  // W [K][C] f32, the statistics [4 waves][K][2], zr [w][K]
   float* sW = sm;
   float* sS = sm + K * C;
+  float* zr = sS + 8 * K;  // this row's vertical interpolation of z (f32)
   for (int i = threadIdx.x; i < K * C; i += 256) sW[i] = to_f32(wf[i]);
   __syncthreads();
   const int G = K / 8;  // 256 % G == 0 (host): a thread keeps its group
@@ -1034,8 +1035,25 @@ __global__ void __launch_bounds__(256) conv1x1_up2_kernel(
     const int y0 = min((int)fy, h - 1);
     const int y1 = y0 + (y0 < h - 1 ? 1 : 0);
     const float ly = fy - (float)y0;
-    const TY* __restrict__ z0 = z + ((long)n * h + y0) * w * ldz + k0;
-    const TY* __restrict__ z1 = z + ((long)n * h + y1) * w * ldz + k0;
+    // the two z rows of this output row, interpolated vertically ONCE into
+    // LDS (each z value was re-read by ~4 output pixels through the L1)
+    {
+      const TY* __restrict__ z0 = z + ((long)n * h + y0) * w * ldz;
+      const TY* __restrict__ z1 = z + ((long)n * h + y1) * w * ldz;
+      __syncthreads();  // the previous row's readers are done
+      for (int i = threadIdx.x; i < w * G; i += 256) {
+        const int x = i >> gs, kk = (i & (G - 1)) * 8;
+        float a[8], c[8];
+        load8(z0 + (long)x * ldz + kk, a);
+        load8(z1 + (long)x * ldz + kk, c);
+        float4* d = reinterpret_cast<float4*>(zr + x * K + kk);
+        d[0] = make_float4((1.f - ly) * a[0] + ly * c[0], (1.f - ly) * a[1] + ly * c[1],
+                           (1.f - ly) * a[2] + ly * c[2], (1.f - ly) * a[3] + ly * c[3]);
+        d[1] = make_float4((1.f - ly) * a[4] + ly * c[4], (1.f - ly) * a[5] + ly * c[5],
+                           (1.f - ly) * a[6] + ly * c[6], (1.f - ly) * a[7] + ly * c[7]);
+      }
+      __syncthreads();
+    }
     const long mrow = (long)row * W;
     for (int i = threadIdx.x; i < items; i += 256) {
       const int ox = i >> gs;  // G is a power of two
@@ -1063,15 +1081,13 @@ __global__ void __launch_bounds__(256) conv1x1_up2_kernel(
       const int x0 = min((int)fx, w - 1);
       const int x1 = x0 + (x0 < w - 1 ? 1 : 0);
       const float lx = fx - (float)x0;
-      float a00[8], a01[8], a10[8], a11[8];
-      load8(z0 + (long)x0 * ldz, a00);
-      load8(z0 + (long)x1 * ldz, a01);
-      load8(z1 + (long)x0 * ldz, a10);
-      load8(z1 + (long)x1 * ldz, a11);
+      const float4* r0 = reinterpret_cast<const float4*>(zr + x0 * K + k0);
+      const float4* r1 = reinterpret_cast<const float4*>(zr + x1 * K + k0);
+      const float4 p0 = r0[0], p1 = r0[1], q0 = r1[0], q1 = r1[1];
+      const float a0[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+      const float a1[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        v[e] += (1.f - ly) * ((1.f - lx) * a00[e] + lx * a01[e]) +
-                ly * ((1.f - lx) * a10[e] + lx * a11[e]);
+      for (int e = 0; e < 8; ++e) v[e] += (1.f - lx) * a0[e] + lx * a1[e];
       store8(y + m * ldy + k0, v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -1107,7 +1123,16 @@ int launch_conv1x1_up2(int C, const void* x, int ldx, const void* wf, const floa
                        double* slots, hipStream_t st) {
   const long M = (long)N * H * W;
   const int grid = std::min(N * H, 4096);
-  const size_t shm = ((size_t)K * C + 8 * (size_t)K) * sizeof(float);
+  const size_t shm = ((size_t)K * C + 8 * (size_t)K + (size_t)w * K) * sizeof(float);
+  UM_CHECK_ARG(shm <= 160 * 1024, "um_conv2d_fwd_up2: low-resolution row too wide (%d x %d)", w, K);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_up2_kernel<T, TY, 8>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_up2_kernel<T, TY, 16>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
 #define UM_C1UP(CC)                                                                            \
   hipLaunchKernelGGL((conv1x1_up2_kernel<T, TY, CC>), dim3(grid), dim3(256), shm, st,           \
                      (const T*)x, ldx, (const T*)wf, bias, K, H, W, M, (TY*)y, ldy, (const TY*)z, \
