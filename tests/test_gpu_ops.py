@@ -738,8 +738,9 @@ def test_tappack(dtype, case, pack):
 
 
 # stride-2 data gradient: the four parity classes in one launch (knob cls4,
-# default: 64x64 LDS-DMA tiles when C is a multiple of 64 and K of 64, with
-# per-class split-K; else 256-row register tiles), the register form forced
+# default: LDS-DMA tiles -- 64x64 when C is a multiple of 64, 64x32 when C is
+# 32 (cls_glds 3; 1: the 64-multiples only) -- with per-class split-K when K
+# is a multiple of 64; else 256-row register tiles), the register form forced
 # (cls_glds 0), and as four launches; odd and even image sizes (classes of
 # different sizes), both pad parities, 8-channel dy (tap packing), against f64
 # torch
@@ -748,7 +749,7 @@ def test_tappack(dtype, case, pack):
                                   (24, 16, 7, 1, 9, 13), (128, 256, 3, 2, 8, 16),
                                   (64, 64, 3, 2, 15, 21), (64, 64, 5, 2, 12, 20),
                                   (256, 512, 3, 8, 16, 32)])
-@pytest.mark.parametrize('mode', [(0, 1), (1, 1), (1, 0)])
+@pytest.mark.parametrize('mode', [(0, 3), (1, 3), (1, 1), (1, 0)])
 def test_dgrad_stride2_classes(case, mode):
     from umamd import functional as U
     from umamd._lib import PAD_ZERO, lib

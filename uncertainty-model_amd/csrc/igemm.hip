@@ -798,8 +798,8 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_kernel(IgArgs a, float* __
 // [0, splits[c]) of the z range, with its own workspace slice.  The class is
 // chosen by uniform branches on kernel arguments (indexing the four by-value
 // IgArgs through a pointer spilled ~200 SGPRs in the register-path variant).
-template <bool SPLIT, int NST>
-__global__ void __launch_bounds__(512) igemm_glds_cls4_kernel(IgArgs a0, IgArgs a1, IgArgs a2,
+template <int BN, int NW, bool SPLIT, int NST>
+__global__ void __launch_bounds__(NW * 64) igemm_glds_cls4_kernel(IgArgs a0, IgArgs a1, IgArgs a2,
                                                                IgArgs a3, int4 start, int4 steps,
                                                                int4 per, int4 splits, int4 ntiles,
                                                                int ntn, float* __restrict__ ws,
@@ -808,19 +808,19 @@ __global__ void __launch_bounds__(512) igemm_glds_cls4_kernel(IgArgs a0, IgArgs 
   const int z = blockIdx.z;
   if (t < start.y) {
     if (z < splits.x)
-      glds_tile<64, 64, 8, SPLIT, 1, NST>(a0, ws + wsoff.x, steps.x, per.x, ntn, t - start.x,
+      glds_tile<64, BN, NW, SPLIT, 1, NST>(a0, ws + wsoff.x, steps.x, per.x, ntn, t - start.x,
                                           ntiles.x);
   } else if (t < start.z) {
     if (z < splits.y)
-      glds_tile<64, 64, 8, SPLIT, 1, NST>(a1, ws + wsoff.y, steps.y, per.y, ntn, t - start.y,
+      glds_tile<64, BN, NW, SPLIT, 1, NST>(a1, ws + wsoff.y, steps.y, per.y, ntn, t - start.y,
                                           ntiles.y);
   } else if (t < start.w) {
     if (z < splits.z)
-      glds_tile<64, 64, 8, SPLIT, 1, NST>(a2, ws + wsoff.z, steps.z, per.z, ntn, t - start.z,
+      glds_tile<64, BN, NW, SPLIT, 1, NST>(a2, ws + wsoff.z, steps.z, per.z, ntn, t - start.z,
                                           ntiles.z);
   } else {
     if (z < splits.w)
-      glds_tile<64, 64, 8, SPLIT, 1, NST>(a3, ws + wsoff.w, steps.w, per.w, ntn, t - start.w,
+      glds_tile<64, BN, NW, SPLIT, 1, NST>(a3, ws + wsoff.w, steps.w, per.w, ntn, t - start.w,
                                           ntiles.w);
   }
 }
@@ -995,11 +995,11 @@ struct Knobs {
     // the four parity classes of a stride-2 data gradient as one launch
     cls4 = env("cls4", 1);
     // the four parity classes of a stride-2 data gradient as one launch of
-    // 64x64 LDS-DMA tiles (NC a multiple of 64) instead of 256-row register
-    // tiles: 64x128 C64 K128 59 -> 28 us, 32x64 C128 K256 50 -> 24, 16x32
-    // C256 K512 57 -> 28 (MI355X, tools/gpu_s2_micro.sh); at NC = 32 the
-    // half-empty 64-column tiles lost (77 -> 84 us)
-    cls_glds = env("cls_glds", 1);
+    // LDS-DMA tiles instead of 256-row register tiles (bit 0: NC a multiple
+    // of 64 on 64x64 tiles: 64x128 C64 K128 59 -> 28 us, 32x64 C128 K256
+    // 50 -> 24, 16x32 C256 K512 57 -> 28; bit 1: NC = 32 on 64x32 tiles with
+    // 4 waves: 128x256 C32 K64 5x5 79 -> 63 us; MI355X, tools/gpu_s2_micro.sh)
+    cls_glds = env("cls_glds", 3);
     // reflect data gradient as a zero-pad transposed conv onto the padded
     // input + a fold pass (0 off, 1 the wide layers, 2 all)
     pad_dgrad = env("pad_dgrad", 1);
@@ -1266,11 +1266,14 @@ struct Cls4Plan {
   long ws;        // bytes (0: no split)
 };
 
+// column tile of the 4-class launch: 64 (8 waves), or 32 (4 waves) when NC is 32
+static int cls4_bn(int NC) { return NC % 64 == 0 ? 64 : 32; }
+
 static Cls4Plan cls4_glds_plan(const int (&M)[4], const int (&taps)[4], int NC, int ach,
                                long ws_bytes) {
   const Knobs& kn = knobs();
   Cls4Plan p{};
-  p.ntn = ceil_div(NC, 64);
+  p.ntn = ceil_div(NC, cls4_bn(NC));
   long tiles = 0, rows = 0;
   for (int c = 0; c < 4; ++c) {
     p.ntiles[c] = ceil_div(M[c], 64) * p.ntn;
@@ -1303,12 +1306,16 @@ static Cls4Plan cls4_glds_plan(const int (&M)[4], const int (&taps)[4], int NC, 
 static bool cls4_glds_ok(int dtype, const IgArgs (&as)[4]) {
   if (!knobs().cls4 || !knobs().cls_glds || !(knobs().glds & 1) || dtype != UM_BF16) return false;
   for (const auto& a : as)
-    if (a.M <= 0 || a.NC % 64 || a.ach % 64 || a.pmode != IG_PAD_ZERO) return false;
+    if (a.M <= 0 || (a.NC % 64 && !(a.NC == 32 && (knobs().cls_glds & 2))) || a.ach % 64 ||
+        a.pmode != IG_PAD_ZERO)
+      return false;
   return true;
 }
 
 long igemm_cls4_ws_bytes(int dtype, const int (&M)[4], const int (&taps)[4], int NC, int ach) {
-  if (!knobs().cls4 || !knobs().cls_glds || dtype != UM_BF16 || NC % 64 || ach % 64) return 0;
+  if (!knobs().cls4 || !knobs().cls_glds || dtype != UM_BF16 || ach % 64 ||
+      (NC % 64 && !(NC == 32 && (knobs().cls_glds & 2))))
+    return 0;
   return cls4_glds_plan(M, taps, NC, ach, -1).ws;
 }
 
@@ -1344,8 +1351,14 @@ static int run_cls4_glds(IgArgs (&as)[4], float* ws, long ws_bytes, hipStream_t 
   const long blocks = (long)p.start[4] * (split ? zmax : 1);
   const bool deep = knobs().glds_deep > 3 && blocks <= knobs().glds_deep_blocks;
 #define UM_GC4(SP_, NST_)                                                                         \
-  hipLaunchKernelGGL((igemm_glds_cls4_kernel<SP_, NST_>), grid, dim3(512), 0, st, as[0], as[1],  \
-                     as[2], as[3], s4, k4, per4, sp4, nt4, p.ntn, ws, off4)
+  do {                                                                                            \
+    if (cls4_bn(NC) == 32)                                                                        \
+      hipLaunchKernelGGL((igemm_glds_cls4_kernel<32, 4, SP_, NST_>), grid, dim3(256), 0, st,      \
+                         as[0], as[1], as[2], as[3], s4, k4, per4, sp4, nt4, p.ntn, ws, off4);    \
+    else                                                                                          \
+      hipLaunchKernelGGL((igemm_glds_cls4_kernel<64, 8, SP_, NST_>), grid, dim3(512), 0, st,      \
+                         as[0], as[1], as[2], as[3], s4, k4, per4, sp4, nt4, p.ntn, ws, off4);    \
+  } while (0)
   if (split && deep) UM_GC4(true, 6);
   else if (split) UM_GC4(true, 3);
   else if (deep) UM_GC4(false, 6);
