@@ -704,6 +704,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ y, in
     const int g = g0 + rm.g;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (rm.active() && g < cg)
+#pragma unroll 4
       for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
         float v[8];
         load8(y + m * ld + g * 8, v);
@@ -763,6 +764,7 @@ __global__ void __launch_bounds__(256) colsum_batch_kernel(CsBatch b) {
     const int g = g0 + rm.g;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (rm.active() && g < cg)
+#pragma unroll 4
       for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
         float v[8];
         load8(y + m * ld + g * 8, v);

@@ -294,6 +294,27 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ x, int N, int C, 
   }
 }
 
+// bf16 with Cp a multiple of 8: thread = (pixel, 8-channel group), the
+// planar reads coalesced across the pixels, one 16-byte store
+__global__ void image_to_nhwc8_kernel(const float* __restrict__ x, int N, int C, long HW, int Cp,
+                                      bf16_t* __restrict__ out) {
+  const int G = Cp / 8;
+  const long total = (long)N * HW * G;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(i / ((long)N * HW));  // group-major: a wave reads consecutive pixels
+    const long pix = i - (long)g * N * HW;
+    const long n = pix / HW, p = pix - n * HW;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = g * 8 + e;
+      v[e] = c < C ? x[(n * C + c) * HW + p] : 0.f;
+    }
+    store8(out + pix * Cp + g * 8, v);
+  }
+}
+
 template <typename T>
 __global__ void axpy_kernel(long n, float alpha, const T* __restrict__ x, T* __restrict__ y) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
@@ -323,6 +344,27 @@ __global__ void sigmoid_scale_bwd_kernel(long M, int C, const float* __restrict_
   }
 }
 
+// the disparity heads' shape (C = 4 outputs in an 8-wide bf16 dlogit, float4-
+// aligned d / dd rows): thread = pixel, two float4 loads, one 16-byte store
+template <bool SPLIT>
+__global__ void sigmoid_scale_bwd4_kernel(long M, const float* __restrict__ d, int ldd,
+                                          const float* __restrict__ dd, int lddd, float scale,
+                                          bf16_t* __restrict__ dlogit) {
+  for (long m = blockIdx.x * (long)blockDim.x + threadIdx.x; m < M;
+       m += (long)gridDim.x * blockDim.x) {
+    const float4 dv = *reinterpret_cast<const float4*>(d + m * ldd);
+    const float4 g = *reinterpret_cast<const float4*>(dd + m * lddd);
+    float v[8];
+    v[0] = g.x * dv.x * (1.f - dv.x / scale);
+    v[1] = g.y * dv.y * (1.f - dv.y / scale);
+    v[2] = g.z * dv.z * (1.f - dv.z / scale);
+    v[3] = g.w * dv.w * (1.f - dv.w / scale);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[4 + e] = SPLIT ? v[e] : 0.f;
+    store8(dlogit + m * 8, v);
+  }
+}
+
 // the split-bf16 head's forward finish (um_head_split_fin)
 __global__ void head_split_fin_kernel(long M, int K, const float* __restrict__ z, int ldz,
                                       const float* __restrict__ bias, float scale,
@@ -336,6 +378,23 @@ __global__ void head_split_fin_kernel(long M, int K, const float* __restrict__ z
     d[m * ldd + k] = scale * sigmoidf_(zr[k] + zr[K + k] + (bias ? bias[k] : 0.f));
   }
 }
+
+// K = 4 with float4-aligned rows: thread = pixel
+__global__ void head_split_fin4_kernel(long M, const float* __restrict__ z, int ldz,
+                                       const float* __restrict__ bias, float scale,
+                                       float* __restrict__ d, int ldd) {
+  const float4 b = bias ? *reinterpret_cast<const float4*>(bias) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (long m = blockIdx.x * (long)blockDim.x + threadIdx.x; m < M;
+       m += (long)gridDim.x * blockDim.x) {
+    const float4 hi = *reinterpret_cast<const float4*>(z + m * ldz);
+    const float4 lo = *reinterpret_cast<const float4*>(z + m * ldz + 4);
+    *reinterpret_cast<float4*>(d + m * ldd) =
+        make_float4(scale * sigmoidf_(hi.x + lo.x + b.x), scale * sigmoidf_(hi.y + lo.y + b.y),
+                    scale * sigmoidf_(hi.z + lo.z + b.z), scale * sigmoidf_(hi.w + lo.w + b.w));
+  }
+}
+
+__host__ inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
 
@@ -452,7 +511,10 @@ int um_merge_wgrad_batch(const um_mwg_desc* descs, int n, hipStream_t st) {
 int um_image_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp, void* out,
                      hipStream_t st) {
   const long total = (long)N * H * W * Cp;
-  if (dtype == UM_BF16)
+  if (dtype == UM_BF16 && Cp % 8 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0)
+    hipLaunchKernelGGL(image_to_nhwc8_kernel, dim3(grid_for(total / 8)), dim3(256), 0, st, x, N,
+                       C, (long)H * W, Cp, (bf16_t*)out);
+  else if (dtype == UM_BF16)
     hipLaunchKernelGGL(image_to_nhwc_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, x, N,
                        C, H, W, Cp, (bf16_t*)out);
   else
@@ -476,7 +538,11 @@ int um_axpy(int dtype, long n, float alpha, const void* x, void* y, hipStream_t 
 int um_sigmoid_scale_bwd(int dtype, long M, int C, const float* d, int ldd, const float* dd,
                          int lddd, float scale, void* dlogit, int ldo, hipStream_t st) {
   const long total = M * ldo;
-  if (dtype == UM_BF16)
+  if (dtype == UM_BF16 && C == 4 && ldo == 8 && ldd % 4 == 0 && lddd % 4 == 0 && al16(d) &&
+      al16(dd) && al16(dlogit))
+    hipLaunchKernelGGL((sigmoid_scale_bwd4_kernel<false>), dim3(grid_for(M)), dim3(256), 0, st, M,
+                       d, ldd, dd, lddd, scale, (bf16_t*)dlogit);
+  else if (dtype == UM_BF16)
     hipLaunchKernelGGL((sigmoid_scale_bwd_kernel<bf16_t, false>), dim3(grid_for(total)), dim3(256),
                        0, st, M, C, d, ldd, dd, lddd, scale, (bf16_t*)dlogit, ldo);
   else
@@ -490,7 +556,11 @@ int um_sigmoid_scale_bwd_split(int dtype, long M, int C, const float* d, int ldd
                                int lddd, float scale, void* dlogit, int ldo, hipStream_t st) {
   UM_CHECK_ARG(ldo >= 2 * C, "um_sigmoid_scale_bwd_split: ldo < 2C");
   const long total = M * ldo;
-  if (dtype == UM_BF16)
+  if (dtype == UM_BF16 && C == 4 && ldo == 8 && ldd % 4 == 0 && lddd % 4 == 0 && al16(d) &&
+      al16(dd) && al16(dlogit))
+    hipLaunchKernelGGL((sigmoid_scale_bwd4_kernel<true>), dim3(grid_for(M)), dim3(256), 0, st, M,
+                       d, ldd, dd, lddd, scale, (bf16_t*)dlogit);
+  else if (dtype == UM_BF16)
     hipLaunchKernelGGL((sigmoid_scale_bwd_kernel<bf16_t, true>), dim3(grid_for(total)), dim3(256),
                        0, st, M, C, d, ldd, dd, lddd, scale, (bf16_t*)dlogit, ldo);
   else
@@ -504,6 +574,12 @@ int um_head_split_fin(long M, int K, const float* z, int ldz, const float* bias,
                       float* d, int ldd, hipStream_t st) {
   UM_CHECK_ARG(ldz >= 2 * K && ldd >= K, "um_head_split_fin: ld");
   const long total = M * K;
+  if (K == 4 && ldz % 4 == 0 && ldd % 4 == 0 && al16(z) && al16(d) && (!bias || al16(bias))) {
+    hipLaunchKernelGGL(head_split_fin4_kernel, dim3(grid_for(M)), dim3(256), 0, st, M, z, ldz, bias,
+                       scale, d, ldd);
+    UM_LAUNCH_CHECK();
+    return UM_OK;
+  }
   hipLaunchKernelGGL(head_split_fin_kernel, dim3(grid_for(total)), dim3(256), 0, st, M, K, z, ldz,
                      bias, scale, d, ldd);
   UM_LAUNCH_CHECK();
