@@ -443,6 +443,81 @@ __global__ void __launch_bounds__(256) cat_bwd_scalar_kernel(const T* __restrict
   }
 }
 
+// UP2 adjoint of a 4-channel source (the disparity maps) at 4-aligned channel
+// offsets: thread = one source pixel, all 4 channels per tap as one 8-byte
+// (bf16) / 16-byte (f32) load.  Only high-res taps X in [2x-1, 2x+2] (and Y
+// likewise) carry nonzero weight under the x2 align_corners upsample (the
+// scalar path scans 2x-2 .. 2x+4), so the 16 loads are issued together with
+// clamped addresses and zero weights, then summed in the scalar path's order
+// (u, then v; adding exact zeros leaves the sums bit-identical).
+template <typename T>
+__global__ void __launch_bounds__(256) cat_bwd_up2c4_kernel(const T* __restrict__ g, int ldg,
+                                                            int coff, int H, int W, CatSrc s,
+                                                            void* dsrc, int ldd, int dsd, int acc,
+                                                            float* __restrict__ dscale, int chunk) {
+  __shared__ float red[4][256];
+  const int n = blockIdx.z;
+  const long P = (long)s.h * s.w;
+  const long p0 = (long)blockIdx.x * chunk, p1 = min(P, p0 + chunk);
+  float sc[4] = {1.f, 1.f, 1.f, 1.f};
+  if (s.scale)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sc[c] = s.scale[n * 4 + c];
+  float ds[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long p = p0 + threadIdx.x; p < p1; p += 256) {
+    const int py = p / s.w, px = p % s.w;
+    float wy[4], wx[4];
+    int yy[4], xx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      wy[u] = up_w(2 * py - 1 + u, py, s.h, H);
+      yy[u] = min(max(2 * py - 1 + u, 0), H - 1);
+      wx[u] = up_w(2 * px - 1 + u, px, s.w, W);
+      xx[u] = min(max(2 * px - 1 + u, 0), W - 1);
+    }
+    float t[4][4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const long off = ((long)(n * H + yy[u]) * W + xx[v]) * ldg + coff;
+        if constexpr (sizeof(T) == 2) {
+          const uint2 q = *reinterpret_cast<const uint2*>(g + off);
+          t[u][v][0] = __uint_as_float(q.x << 16);
+          t[u][v][1] = __uint_as_float(q.x & 0xffff0000u);
+          t[u][v][2] = __uint_as_float(q.y << 16);
+          t[u][v][3] = __uint_as_float(q.y & 0xffff0000u);
+        } else {
+          const float4 f = *reinterpret_cast<const float4*>(g + off);
+          t[u][v][0] = f.x; t[u][v][1] = f.y; t[u][v][2] = f.z; t[u][v][3] = f.w;
+        }
+      }
+    float gv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) gv[c] += wy[u] * wx[v] * t[u][v][c];
+    const long sp = (long)n * P + p;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (dsrc) st_any(dsrc, sp * ldd + c, dsd, gv[c] * sc[c], acc);
+      if (dscale) ds[c] += gv[c] * ld_any(s.ptr, sp * s.ld + c, s.dtype);
+    }
+  }
+  if (dscale) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[c][threadIdx.x] = ds[c];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      float t = 0.f;
+      for (int i = 0; i < 256; ++i) t += red[threadIdx.x][i];
+      dscale[((long)n * gridDim.x + blockIdx.x) * 4 + threadIdx.x] = t;
+    }
+  }
+}
+
 template <typename T>
 __global__ void cat_bwd_pshuf_kernel(const T* __restrict__ g, int ldg, int coff, int H, int W,
                                      CatSrc s, void* dsrc, int ldd, int dsd, int acc) {
@@ -460,6 +535,36 @@ __global__ void cat_bwd_pshuf_kernel(const T* __restrict__ g, int ldg, int coff,
     const int c = cs >> 2, yy = 2 * py + ((cs >> 1) & 1), xx = 2 * px + (cs & 1);
     const float gv = to_f32(g[((long)(n * H + yy) * W + xx) * ldg + coff + c]);
     st_any(dsrc, ((long)n * P + p) * ldd + cs, dsd, gv, acc);
+  }
+}
+
+// the same with 8 concat channels per thread (C, coff, ldd multiples of 8):
+// four 16-byte loads (the 2x2 sub-pixels), the 32 source values of channels
+// [4*c0, 4*c0 + 32) as four 8-element stores
+template <typename T>
+__global__ void cat_bwd_pshuf8_kernel(const T* __restrict__ g, int ldg, int coff, int H, int W,
+                                      CatSrc s, void* dsrc, int ldd, int dsd, int acc) {
+  const int n = blockIdx.z;
+  const int C8 = s.C / 8;
+  const long P = (long)s.h * s.w;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < P * C8;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    const long p = i / C8;
+    const int py = p / s.w, px = p % s.w;
+    float v[4][8];
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      const int yy = 2 * py + (sub >> 1), xx = 2 * px + (sub & 1);
+      load8(g + ((long)(n * H + yy) * W + xx) * ldg + coff + c8 * 8, v[sub]);
+    }
+    const long base = ((long)n * P + p) * ldd + c8 * 32;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const float w[8] = {v[0][2 * o], v[1][2 * o], v[2][2 * o], v[3][2 * o],
+                          v[0][2 * o + 1], v[1][2 * o + 1], v[2][2 * o + 1], v[3][2 * o + 1]};
+      st8_any(dsrc, base + o * 8, dsd, w, acc);
+    }
   }
 }
 
@@ -735,6 +840,20 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
   UM_CHECK_ARG(ldg % 8 == 0, "um_concat_bwd_src: ldg %% 8");
   if (s.op == UM_CAT_PSHUF) {
     UM_CHECK_ARG(dsrc != nullptr && dscale == nullptr, "um_concat_bwd_src: pshuf args");
+    if (s.C % 8 == 0 && s.coff % 8 == 0 && ldd % 8 == 0) {
+      const long per_n8 = (long)s.h * s.w * s.C / 8;
+      dim3 grid8((unsigned)std::min<long>((per_n8 + 255) / 256, 2048), 1, N);
+      if (dtype == UM_BF16)
+        hipLaunchKernelGGL(cat_bwd_pshuf8_kernel<bf16_t>, grid8, dim3(256), 0, st,
+                           (const bf16_t*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
+                           accumulate);
+      else
+        hipLaunchKernelGGL(cat_bwd_pshuf8_kernel<float>, grid8, dim3(256), 0, st,
+                           (const float*)g, ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype,
+                           accumulate);
+      UM_LAUNCH_CHECK();
+      return UM_OK;
+    }
     const long per_n = (long)s.h * s.w * 4 * s.C;
     dim3 grid((unsigned)std::min<long>((per_n + 255) / 256, 2048), 1, N);
     if (dtype == UM_BF16)
@@ -753,7 +872,16 @@ int um_concat_bwd_src(int dtype, int N, int H, int W, const void* g, int ldg,
   const int nblk = ceil_div(P, chunk);
   UM_CHECK_ARG(!dscale || ws, "um_concat_bwd_src: gate gradient needs the workspace");
   float* parts = dscale ? ws : nullptr;
-  if (!vec) {
+  if (!vec && s.op == UM_CAT_UP2 && s.C == 4 && s.coff % 4 == 0 && H == 2 * s.h &&
+      W == 2 * s.w) {
+    dim3 grid(nblk, 1, N);
+    if (dtype == UM_BF16)
+      hipLaunchKernelGGL(cat_bwd_up2c4_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)g,
+                         ldg, s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, parts, chunk);
+    else
+      hipLaunchKernelGGL(cat_bwd_up2c4_kernel<float>, grid, dim3(256), 0, st, (const float*)g, ldg,
+                         s.coff, H, W, s, dsrc, ldd, dsrc_dtype, accumulate, parts, chunk);
+  } else if (!vec) {
     dim3 grid(nblk, 1, N);
 #define UM_CAT_SCALAR(T_, OP_)                                                               \
     hipLaunchKernelGGL((cat_bwd_scalar_kernel<T_, OP_>), grid, dim3(256), 0, st, (const T_*)g, \
