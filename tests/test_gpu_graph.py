@@ -479,3 +479,56 @@ def test_grad_slots_guard_unregistered_consumer(monkeypatch):
     torch.cuda.synchronize()
     assert not U.GradSlots.broken
     assert x.grad is not None and torch.isfinite(x.grad).all()
+
+
+@pytest.mark.parametrize('k,fs,acc', [(2, 0, (0, 1)), (3, 2, (1, 0, 1)), (4, 1, (0, 0, 1, 1)),
+                                      (5, 3, (1, 1, 0, 0, 1))])
+@pytest.mark.parametrize('dt,ydt', [(torch.bfloat16, torch.float32), (torch.bfloat16, torch.bfloat16),
+                                    (torch.float32, torch.float32)])
+def test_merge_bwd_bn_kernel(k, fs, acc, dt, ydt):
+    """um_merge_bwd_bn against torch: dsrc_s (+)= sigmoid(w_s) * dm (stored
+    in the activation dtype), the per-block dots sum(dm * src_s) and the
+    BN-ELU backward sums of source fs over its stored gradient.  k = 2..4
+    take the loads-first instances, k = 5 the runtime source loop."""
+    from umamd import _lib as L
+    from umamd._lib import call, ptr, query
+    M, C = 3000, 32
+    g = torch.Generator().manual_seed(11 + k)
+    rnd = lambda *s: torch.randn(*s, generator=g)  # noqa: E731
+    srcs = [rnd(M, C).to(dt).to(DEV) for _ in range(k)]
+    d0 = [rnd(M, C).to(dt) for _ in range(k)]
+    dsrcs = [t.clone().to(DEV) for t in d0]
+    dm = rnd(M, C).to(dt).to(DEV)
+    w = rnd(k).to(DEV)
+    widx = list(range(k))
+    y = rnd(M, C).to(ydt).to(DEV)
+    mean, invstd = rnd(C).to(DEV), (rnd(C).abs() + 0.5).to(DEV)
+    scale, shift = rnd(C).to(DEV), rnd(C).to(DEV)
+    slots = torch.zeros(L.STAT_SLOTS * C * 2 + 1, dtype=torch.float64, device=DEV)
+    nparts = query('um_merge_bn_parts', M * C)
+    parts = torch.zeros((nparts, k), dtype=torch.float32, device=DEV)
+    ci, cp = L.ctypes.c_int, L.ctypes.c_void_p
+    code = L.dtype_code(dt) | (L.Y_ACT if ydt != torch.float32 else 0)
+    call('um_merge_bwd_bn', code, k, (cp * k)(*[t.data_ptr() for t in srcs]),
+         (cp * k)(*[t.data_ptr() for t in dsrcs]), (ci * k)(*acc), (ci * k)(*widx), ptr(w), None,
+         M * C, ptr(dm), ptr(parts), fs, ptr(y), C, ptr(mean), ptr(invstd), ptr(scale), ptr(shift),
+         1, ptr(slots))
+    torch.cuda.synchronize()
+    coef = torch.sigmoid(w).cpu()
+    dmf = dm.float().cpu()
+    for s in range(k):
+        want = ((d0[s].float() if acc[s] else 0) + coef[s] * dmf).to(dt).float()
+        # one rounding of the activation dtype apart at most (fma vs mul + add)
+        tol = 1e-6 if dt == torch.float32 else 2 ** -7
+        torch.testing.assert_close(dsrcs[s].float().cpu(), want, rtol=tol, atol=1e-6)
+        dot = (dmf.double() * srcs[s].double().cpu()).sum()
+        assert abs(parts[:, s].double().sum().cpu() - dot) <= 1e-4 * (dmf.abs().sum() + 1), s
+    r = dsrcs[fs].double().cpu()
+    yc = y.double().cpu()
+    z = yc * scale.double().cpu() + shift.double().cpu()
+    dz = torch.where(z > 0, r, r * torch.exp(z))
+    xhat = (yc - mean.double().cpu()) * invstd.double().cpu()
+    got = slots[:L.STAT_SLOTS * C * 2].view(L.STAT_SLOTS, C, 2).sum(0).cpu()
+    torch.testing.assert_close(got[:, 0], dz.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(got[:, 1], (dz * xhat).sum(0), rtol=1e-4, atol=1e-3)
+    assert slots[-1].item() == M

@@ -107,7 +107,12 @@ __global__ void merge_bwd_kernel(MergeArgs a, int nsrc, const float* __restrict_
 // go into the layer's f64 statistics slots here, so the reduce launch and its
 // re-read of da are skipped.  C / 8 divides the block size: every thread of
 // the grid-stride loop keeps one 8-channel group.
-template <typename T, typename TY>
+// NS > 0: exactly NS sources, and every load of an element group (dm, y,
+// the sources, the gradients accumulated into) is issued before the first
+// store: the runtime source loop otherwise serialises one load -> store
+// round trip per source (the compiler cannot move a load past a store that
+// may alias it), at the 2 waves per SIMD this grid leaves.
+template <typename T, typename TY, int NS>
 __global__ void __launch_bounds__(256) merge_bwd_bn_kernel(
     MergeArgs a, int nsrc, const float* __restrict__ w, long n8, const T* __restrict__ dm,
     float* __restrict__ parts, int fsrc, const TY* __restrict__ y, int C,
@@ -128,6 +133,48 @@ __global__ void __launch_bounds__(256) merge_bwd_bn_kernel(
   load8(shift + g * 8, sh);
 #pragma unroll
   for (int e = 0; e < 8; ++e) { bs[e] = 0.f; bx[e] = 0.f; }
+  auto stats = [&](const float (&r)[8], const float (&yv)[8]) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float dz = r[e];
+      if (apply_elu) {
+        const float z = yv[e] * sc[e] + sh[e];
+        dz = z > 0.f ? dz : dz * __expf(z);
+      }
+      bs[e] += dz;
+      bx[e] += dz * (yv[e] - mu[e]) * is[e];
+    }
+  };
+  if constexpr (NS > 0) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8;
+         i += (long)gridDim.x * blockDim.x) {
+      float gv[8], yv[8], v[NS][8], o[NS][8];
+      load8(dm + i * 8, gv);
+      load8(y + i * 8, yv);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (parts) load8(reinterpret_cast<const T*>(a.src[s]) + i * 8, v[s]);
+        if (a.acc[s]) load8(reinterpret_cast<const T*>(a.dsrc[s]) + i * 8, o[s]);
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (parts)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dot[s] += gv[e] * v[s][e];
+        if (a.dsrc[s]) {
+          T* d = reinterpret_cast<T*>(a.dsrc[s]) + i * 8;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[s][e] = (a.acc[s] ? o[s][e] : 0.f) + coef[s] * gv[e];
+          store8(d, o[s]);
+          if (s == fsrc) {
+            float r[8];
+            load8_rounded(o[s], r, d);
+            stats(r, yv);
+          }
+        }
+      }
+    }
+  } else
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8;
        i += (long)gridDim.x * blockDim.x) {
     float gv[8], v[8], o[8];
@@ -148,16 +195,7 @@ __global__ void __launch_bounds__(256) merge_bwd_bn_kernel(
           float r[8], yv[8];
           load8_rounded(o, r, d);
           load8(y + i * 8, yv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float dz = r[e];
-            if (apply_elu) {
-              const float z = yv[e] * sc[e] + sh[e];
-              dz = z > 0.f ? dz : dz * __expf(z);
-            }
-            bs[e] += dz;
-            bx[e] += dz * (yv[e] - mu[e]) * is[e];
-          }
+          stats(r, yv);
         }
       }
     }
@@ -467,14 +505,26 @@ int um_merge_bwd_bn(int dtype, int nsrc, const void* const* srcs, void* const* d
     a.coef[i] = coefs ? coefs[i] : 1.f;
   }
   const long n8 = count / 8, M = count / C;
-#define UM_MBB(T_, TY_)                                                                           \
-  hipLaunchKernelGGL((merge_bwd_bn_kernel<T_, TY_>), dim3(merge_bn_grid(n8)), dim3(256), 0, st, a, nsrc, w, \
-                     n8, (const T_*)dm, parts, fsrc, (const TY_*)y, C, mean, invstd, scale, shift,   \
-                     apply_elu, slots, M)
+  // sources 2-4 on the loads-first instances (tuning key merge_ns = 0: the
+  // runtime source loop for all)
+  static const int ns_on = (int)umamd::tuning_env("merge_ns", 1);
+  const int ns = ns_on && nsrc >= 2 && nsrc <= 4 ? nsrc : 0;
+#define UM_MBB_NS(T_, TY_, NS_)                                                                   \
+  hipLaunchKernelGGL((merge_bwd_bn_kernel<T_, TY_, NS_>), dim3(merge_bn_grid(n8)), dim3(256), 0, st, a,  \
+                     nsrc, w, n8, (const T_*)dm, parts, fsrc, (const TY_*)y, C, mean, invstd, scale, \
+                     shift, apply_elu, slots, M)
+#define UM_MBB(T_, TY_)                      \
+  do {                                       \
+    if (ns == 2) UM_MBB_NS(T_, TY_, 2);      \
+    else if (ns == 3) UM_MBB_NS(T_, TY_, 3); \
+    else if (ns == 4) UM_MBB_NS(T_, TY_, 4); \
+    else UM_MBB_NS(T_, TY_, 0);              \
+  } while (0)
   if (dtype == (UM_BF16 | UM_Y_ACT)) UM_MBB(bf16_t, bf16_t);
   else if (dtype == UM_BF16) UM_MBB(bf16_t, float);
   else UM_MBB(float, float);
 #undef UM_MBB
+#undef UM_MBB_NS
   UM_LAUNCH_CHECK();
   return UM_OK;
 }
