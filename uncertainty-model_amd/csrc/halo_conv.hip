@@ -63,6 +63,9 @@ __device__ __forceinline__ int himg(int p, int c) { return p * CK + ((c ^ ((p >>
 // into (dynamic) LDS once per workgroup and reused by all its tiles -- no
 // weight load, register set or barrier inside the tap loop (3x3 layers whose
 // weights fit, umamd::halo_run).
+// staged epilogue switch (tuning key halo_staged, read on the host into the
+// launch's argument block)
+#define umamd_halo_staged (a.staged)
 template <int R, int BN, bool FLIP, bool REFLECT, int WM>
 __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, int tiles_y,
                                                         int ntiles) {
@@ -331,10 +334,25 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
     float csum[TN], csq[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+    // STAGED (bf16 output written once, no residual / sigmoid): the tile's
+    // values go through the (now free) halo LDS as [pixel][JP*16 columns],
+    // JP column blocks per pass, and leave as 16-byte rows of 8 channels --
+    // instead of 2-byte stores of one column at 4 pixels per lane
+    constexpr int JP = TN % 2 == 0 ? 2 : 1;
+    static_assert(TH * TW * JP * 16 <= HP * CK, "staged epilogue tile exceeds the halo LDS");
+    // not where the staging registers would cost a wave per SIMD (3x3 at 96
+    // columns streamed, 7x7 at 64 columns)
+    constexpr bool STG = !(R == 3 && BN == 96) && !(R == 7 && BN == 64);
+    const bool staged = STG && umamd_halo_staged && !a.out_f32 && !a.accumulate &&
+                        a.epilogue != UM_EPI_RESIDUAL && a.epilogue != UM_EPI_SIGMOID_SCALE &&
+                        a.NC % 8 == 0 && a.ld_out % 8 == 0 &&
+                        (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
+    bf16_t* sE = sH;
+    if (staged) __syncthreads();  // every wave's fragment reads of sH are done
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = bn + j * 16 + nc;
-      if (!nok[j]) continue;
+      if (nok[j]) {
       const float bv = a.bias != nullptr ? a.bias[n] : 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -353,7 +371,10 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
           if (a.epilogue == UM_EPI_RESIDUAL)
             v += to_f32(reinterpret_cast<const bf16_t*>(a.residual)[m * a.ldr + n]);
           if (a.epilogue == UM_EPI_SIGMOID_SCALE) v = a.epi_scale * sigmoidf_(v);
-          if (a.out_f32) {
+          if (staged) {
+            sE[(((2 * wave + (i >> 1)) * TW + (i & 1) * 16 + rg + q) * JP + j % JP) * 16 + nc] =
+                from_f32<bf16_t>(v);
+          } else if (a.out_f32) {
             float* o = reinterpret_cast<float*>(a.out) + off;
             if (a.accumulate) v += *o;
             *o = v;
@@ -365,6 +386,23 @@ __global__ void __launch_bounds__(256) halo_conv_kernel(IgArgs a, int tiles_x, i
           csum[j] += v;
           csq[j] += v * v;
         }
+      }
+      }
+      if (staged && j % JP == JP - 1) {
+        __syncthreads();
+        constexpr int GP = JP * 2;  // 8-channel groups per pixel in a pass
+#pragma unroll
+        for (int it = tid; it < TH * TW * GP; it += 256) {
+          const int pix = it / GP, g = it % GP;
+          const int py = ty0 + pix / TW, px = tx0 + pix % TW;
+          const int n0 = bn + (j / JP) * JP * 16 + g * 8;
+          if (py < a.oh && px < a.ow && n0 < a.NC) {
+            const long m = ((long)nimg * a.oh + py) * a.ow + px;
+            *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.out) + m * a.ld_out + n0) =
+                *reinterpret_cast<const uint4*>(&sE[(pix * JP) * 16 + g * 8]);
+          }
+        }
+        __syncthreads();  // the pass's LDS reads are done (next pass / next tile's halo)
       }
     }
     if (a.epilogue == UM_EPI_STATS) {
@@ -532,7 +570,9 @@ bool halo_applicable(int dtype, const IgArgs& a, int min_tiles, int max_nc) {
   return (long)a.on * ((a.oh + TH - 1) / TH) * ((a.ow + TW - 1) / TW) >= min_tiles;
 }
 
-int halo_run(const IgArgs& a, hipStream_t st) {
+int halo_run(const IgArgs& a0, hipStream_t st) {
+  IgArgs a = a0;
+  a.staged = igemm_halo_staged();
   if (a.R == 3) return launch_bn<3>(a, st);
   if (a.R == 5) return launch_bn<5>(a, st);
   return launch_bn<7>(a, st);

@@ -42,6 +42,7 @@ struct IgArgs {
   float* stats;     // [parts][NC][2] f32 partial rows, or (stat_slots) f64 slots
   int stats_rows;   // set by igemm_run (igemm_stats_rows)
   int stat_slots;   // UM_EPI_STAT_SLOTS: stats is double[UM_STAT_SLOTS][NC][2]
+  int staged;       // halo conv: LDS-staged 16-byte output rows (set by halo_run)
   int colmajor;     // tile order, set by igemm_run (knob xcd_col)
   int tappack;      // 4 taps x 8 channels per k-step (ach == 8), set by igemm_run
 };
@@ -104,6 +105,8 @@ int igemm_halo_persist();
 int igemm_halo_grid();
 // resident-weight LDS budget (KB) of the 3x3 halo convs ("halo_res_kb", 0 = off)
 int igemm_halo_res_kb();
+// halo conv bf16 outputs staged through LDS as 16-byte rows ("halo_staged")
+int igemm_halo_staged();
 // reflect fold of the split-form data gradient as a VALU pass ("border_valu")
 int igemm_border_valu();
 

@@ -946,6 +946,7 @@ struct Knobs {
   int halo_max_nc;
   int halo_pf2;
   int halo_persist, halo_grid, halo_res_kb;
+  int halo_staged;
   int border_valu;
   int s1x1;
   Knobs() {
@@ -1017,6 +1018,8 @@ struct Knobs {
     // 3x3 halo convs keep all their tap weights in LDS (per workgroup, for
     // all its tiles) when they need at most this many KB; 0 = stream rows
     halo_res_kb = env("halo_res_kb", 48);
+    // halo conv bf16 outputs through LDS as 16-byte rows (halo_conv.hip)
+    halo_staged = env("halo_staged", 1);
     // reflect fold of the split-form data gradient: a VALU pass over the
     // border list (conv.hip reflect_border_kernel) instead of the GEMM
     border_valu = env("border_valu", 1);
@@ -1198,6 +1201,7 @@ int igemm_halo_pf2() { return knobs().halo_pf2; }
 int igemm_halo_persist() { return knobs().halo_persist; }
 int igemm_halo_grid() { return knobs().halo_grid; }
 int igemm_halo_res_kb() { return knobs().halo_res_kb; }
+int igemm_halo_staged() { return knobs().halo_staged; }
 int igemm_border_valu() { return knobs().border_valu; }
 
 int igemm_border_list(IgArgs& a) {
@@ -1452,6 +1456,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "halo_persist")) f = &k.halo_persist;
   else if (!strcmp(key, "halo_grid")) f = &k.halo_grid;
   else if (!strcmp(key, "halo_res_kb")) f = &k.halo_res_kb;
+  else if (!strcmp(key, "halo_staged")) f = &k.halo_staged;
   else if (!strcmp(key, "border_valu")) f = &k.border_valu;
   else if (!strcmp(key, "s1x1")) f = &k.s1x1;
   if (!f) return -1;
