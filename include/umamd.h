@@ -357,6 +357,20 @@ int um_head_split_fin(long M, int K, const float* z, int ldz, const float* bias,
                       float* d, int ldd, hipStream_t stream);
 int um_sigmoid_scale_bwd_split(int dtype, long M, int C, const float* d, int ldd, const float* dd,
                                int lddd, float scale, void* dlogit, int ldo, hipStream_t stream);
+/* One-pass bf16 disparity heads (csrc/disphead.hip), reference
+ * model/layers/decoder.py:244-247 (ConvLayer: ReflectionPad2d(1) + Conv2d 3x3,
+ * 4 outputs) + :246 (scale * sigmoid).  x NHWC bf16 [N][H][W][ldx] with C in
+ * {32, 64, 128, 256} channels, W % 16 == 0 (um_disp_head_ok); wf / wT the
+ * split-bf16 weights of um_pack_weight_split with K = 4 ([8][3][3][C] and
+ * [C][3][3][8]).
+ * fwd  : d[m][k] = scale * sigmoid(sum (w_hi + w_lo) x + bias[k]), d f32 [M][ldd]
+ * dgrad: dx (+)= the reflect-pad conv adjoint of dlogit [M][ldl] bf16 (the 8
+ *        channels of um_sigmoid_scale_bwd_split), dx bf16 [M][ldx] */
+int um_disp_head_ok(int N, int H, int W, int C, int ldx);
+int um_disp_head_fwd(int N, int H, int W, int C, const void* x, int ldx, const void* wf,
+                     const float* bias, float scale, float* d, int ldd, hipStream_t stream);
+int um_disp_head_dgrad(int N, int H, int W, int C, const void* dl, int ldl, const void* wT,
+                       void* dx, int ldx, int accumulate, hipStream_t stream);
 
 /* ----------------------------------------------------------- attention ---
  * EfficientAttention core, reference model/layers/attention.py:42-76.

@@ -124,8 +124,13 @@ class _RecordingComm:
         self.order = rccl._Order(record=lambda s: ('event', s), wait=lambda s, ev: None)
         self.seq = []
 
+    @property
+    def world(self):
+        return dist.get_world_size(self.group)
+
     def all_reduce(self, t, average=False):
         self.order.before(self.stream)
+        self.order.sig.append((int(t.numel()), str(t.dtype)))
         self.seq.append((self.stream, tuple(t.shape), str(t.dtype), bool(average)))
         dist.all_reduce(t, group=self.group)
         if average:
@@ -206,6 +211,15 @@ def run_order(rank, world, out):
     allseq = [None] * world
     dist.all_gather_object(allseq, seqs)
     assert all(s == allseq[0] for s in allseq), 'collective order differs between ranks'
+    # umamd.rccl.check_order: passes on the recorded sequence; a rank that
+    # issued one collective more (or in another order) fails on every rank
+    rccl.check_order(rec)
+    rec.order.sig.append((rank + 1, 'torch.float64'))
+    try:
+        rccl.check_order(rec)
+        raise AssertionError('check_order missed a rank-dependent collective sequence')
+    except RuntimeError as e:
+        assert 'different order' in str(e), e
     torch.save({'seq': [[list(map(str, e)) for e in s] for s in seqs],
                 'grads': [p.grad.clone() for p in layers.parameters()]},
                os.path.join(out, f'order_{rank}.pt'))

@@ -827,6 +827,66 @@ def test_disp_head_split(C, H, W, monkeypatch):
     assert _rel(dx_s, dx_ref) <= _rel(dx_p, dx_ref) * 1.5 + 1e-4
 
 
+@pytest.mark.parametrize('C,H,W', [(32, 16, 32), (64, 8, 16), (128, 4, 48), (256, 6, 16),
+                                   (32, 32, 64), (32, 12, 16), (64, 6, 32), (64, 4, 16)])
+def test_disp_head_onepass(C, H, W, monkeypatch):
+    """The one-pass head kernels (csrc/disphead.hip: strip MFMA with direct
+    operand loads, the reflect adjoint folded into the dlogit load) against
+    the f64 reference with the unrounded weights, and against the
+    implicit-GEMM head path (UMAMD_ONEPASS_HEAD=0) on the same inputs; the
+    data gradient's accumulate mode through the C entry.  Shapes cover
+    W = 16 (the border columns 1 and W-2 in one strip) and H = 4 (mirror
+    rows 1 and H-2 adjacent)."""
+    import umamd.functional as U
+    from umamd._lib import call, ptr, query
+    N, K, scale = 2, 4, 0.3
+    assert query('um_disp_head_ok', N, H, W, C, C) == 1
+    torch.manual_seed(C + H + W)
+    x = F.elu(torch.randn(N, C, H, W)).to(torch.bfloat16).float()
+    conv = nn.Conv2d(C, K, 3)
+    nn.init.xavier_uniform_(conv.weight)
+    conv.bias.data.uniform_(-0.5, 0.5)
+    conv = conv.to(DEV)
+    dd = torch.randn(N, K, H, W)
+
+    xr = x.double().requires_grad_(True)
+    z = F.conv2d(F.pad(xr, (1, 1, 1, 1), mode='reflect'), conv.weight.detach().double().cpu(),
+                 conv.bias.detach().double().cpu())
+    d_ref = scale * torch.sigmoid(z)
+    d_ref.backward(dd.double())
+
+    def run(onepass):
+        monkeypatch.setattr(U, '_ONEPASS_HEAD', onepass)
+        xd = _nhwc(x).to(torch.bfloat16).requires_grad_(True)
+        conv.weight.grad = None
+        d = U.disp_head(xd, conv, scale)
+        d.backward(_nhwc(dd))
+        return _nchw(d), _nchw(xd.grad), conv.weight.grad.cpu()
+
+    d_o, dx_o, dw_o = run(True)
+    d_g, dx_g, dw_g = run(False)
+    assert _rel(d_o, d_ref.detach()) <= 2e-5, _rel(d_o, d_ref.detach())
+    assert _rel(d_o, d_g) <= 2e-5
+    assert _rel(dx_o, xr.grad) <= 1e-2, _rel(dx_o, xr.grad)
+    # the GEMM path rounds the same bf16 dlogit; the two differ by the bf16
+    # rounding of dx (1-2 ulp at the max: <= 8e-3) and the border-pixel
+    # mirror sums (f32 sum -> bf16 operand): no worse against the reference
+    assert _rel(dx_o, dx_g) <= 8e-3, _rel(dx_o, dx_g)
+    assert _rel(dx_o, xr.grad) <= 1.25 * _rel(dx_g, xr.grad) + 1e-3
+    assert _rel(dw_o, dw_g) <= 1e-6
+
+    # accumulate: dx += adjoint(dlogit), straight through the C entry
+    wf, wT = U._pack(conv.weight, C, torch.bfloat16, ldT=8, split=True)
+    dl = torch.randn(N, H, W, 8, device=DEV).to(torch.bfloat16)
+    base = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    d0 = torch.empty_like(base)
+    call('um_disp_head_dgrad', N, H, W, C, ptr(dl), 8, ptr(wT), ptr(d0), C, 0)
+    d1 = base.clone()
+    call('um_disp_head_dgrad', N, H, W, C, ptr(dl), 8, ptr(wT), ptr(d1), C, 1)
+    torch.cuda.synchronize()
+    assert _rel(d1.float(), base.float() + d0.float()) <= 5e-3
+
+
 @pytest.mark.parametrize('case', [CONV_CASES[1], CONV_CASES[3], CONV_CASES[7], CONV_CASES[4]])
 def test_conv_bn_elu_ybf16(case, monkeypatch):
     """bf16 activations with the pre-BN y stored in bf16 (UM_Y_ACT, the

@@ -483,7 +483,8 @@ __global__ void __launch_bounds__(W1_NT) wgrad_1x1_kernel(WgradArgs a) {
 
 static bool wgrad_1x1_ok(int dtype, int C, int K, int R, int stride, int pad, int ldx, int ldy) {
   auto p2 = [](int v) { return v == 8 || v == 16 || v == 32 || v == 64; };
-  return dtype == UM_BF16 && umamd::tuning_env("w1x1", 1) && R == 1 && stride == 1 && pad == 0 &&
+  static const bool on = umamd::tuning_env("w1x1", 1) != 0;  // read once (common.h)
+  return dtype == UM_BF16 && on && R == 1 && stride == 1 && pad == 0 &&
          p2(C) && p2(K) && K * C <= W1_MAX && ldx % 8 == 0 && ldy % 8 == 0;
 }
 

@@ -808,9 +808,11 @@ __global__ void __launch_bounds__(SCT) loss_scatter_kernel(LArgs a) {
   // those with y0(r) + 1 = T.
   // The row accumulators are fixed point (int32 LDS atomics, which run at
   // the LDS's integer rate; f32 LDS atomics measured 2x slower for the whole
-  // kernel): every contribution is gg * e with |gg| <= kmax = max(|kcd|, |kce|)
-  // and e + w = 1 per source, so a row sums at most W * kmax into one target.
-  // Units of kmax * 2^-sh with sh = 30 - ceil(log2 W) keep that below 2^30;
+  // kernel): a source pixel adds gg_d * e (|gg_d| <= |kcd|) and, with an
+  // error-consistency weight, gg_s * e (|gg_s| <= |kce|) into the SAME target
+  // channel, e + w = 1 per source, so a row sums at most W * kmax into one
+  // target with kmax = |kcd| + |kce|.  Units of kmax * 2^-sh with
+  // sh = 30 - ceil(log2 W) keep that at most 2^30 (int32 headroom 2x);
   // the quantum is kmax * 2^-sh (5e-7 kmax at W = 512) and the integer sums
   // are exact, i.e. independent of the atomics' order.
   extern __shared__ int acc[];  // [STR + 2 source rows][2 target ch][W]
@@ -830,7 +832,9 @@ __global__ void __launch_bounds__(SCT) loss_scatter_kernel(LArgs a) {
   const int halfw = W / 2;
   const int r0 = max(0, y0 - 1), r1 = min(H, y0 + STR + 1);
   const int nr = r1 - r0;
-  const float kmax = fmaxf(fabsf(kcd), a.ecw != 0.f ? fabsf(kce) : 0.f);
+  // the d term (kcd) and the sigma term (kce) of one source land in the same
+  // target channel: their magnitudes add in the bound
+  const float kmax = fabsf(kcd) + (a.ecw != 0.f ? fabsf(kce) : 0.f);
   const int sh = 30 - (W > 1 ? 32 - __clz(W - 1) : 0);
   const float toq = kmax > 0.f ? ldexpf(1.f, sh) / kmax : 0.f;
   const float fromq = ldexpf(kmax, -sh);

@@ -27,6 +27,9 @@
 // model/layers/encoder.py:36-41 and model/layers/decoder.py:37-41.
 #include <algorithm>
 
+#include <map>
+#include <mutex>
+
 #include "common.h"
 #include "wgrad_halo.h"
 
@@ -366,8 +369,15 @@ bool exists(const HwPlan& h) {
   return false;
 }
 
+// cached per (instance, dynamic LDS): plan() runs several times per conv on
+// every eager step, the runtime queries only once
 template <int KT, int CT, int TPW>
 int occupancy_hw(size_t lds) {
+  static std::mutex mu;
+  static std::map<size_t, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  const auto it = cache.find(lds);
+  if (it != cache.end()) return it->second;
   const void* f = reinterpret_cast<const void*>(&hwgrad_kernel<KT, CT, TPW>);
   (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   int n = 0;
@@ -375,6 +385,7 @@ int occupancy_hw(size_t lds) {
     (void)hipGetLastError();
     n = 1;
   }
+  cache[lds] = n;
   return n;
 }
 

@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <atomic>
+
 #include "common.h"
 #include "wgrad_tr.h"
 
@@ -266,6 +268,10 @@ int wgrad_tr_tbk() {
 // resident 256-thread workgroups per CU of the instance wgrad_tr_run picks for K
 int wgrad_tr_blocks_per_cu(int K) {
   const int bm = wgrad_tr_bm(K), tbk = wgrad_tr_tbk();
+  // cached per instance (bm, tbk): queried on every weight-gradient plan
+  static std::atomic<int> cache[2][3] = {{{0}, {0}, {0}}, {{0}, {0}, {0}}};
+  std::atomic<int>& slot = cache[bm == 128][tbk == 32 ? 0 : (tbk == 64 ? 1 : 2)];
+  if (const int c = slot.load(std::memory_order_relaxed)) return c;
   const void* f = nullptr;
 #define UM_WTRF(BM_, TBK_) \
   if (bm == BM_ && tbk == TBK_) f = reinterpret_cast<const void*>(&wgrad_tr_kernel<BM_, TBK_>);
@@ -277,7 +283,9 @@ int wgrad_tr_blocks_per_cu(int K) {
     (void)hipGetLastError();
     n = 1;
   }
-  return std::max(1, n);
+  n = std::max(1, n);
+  slot.store(n, std::memory_order_relaxed);
+  return n;
 }
 
 int wgrad_tr_run(const void* x, int N, int H, int W, int C, int ldx, int K, int R, int stride,

@@ -134,6 +134,10 @@ class CapturedTrainStep:
         # autograd graph alive (its AccumulateGrad nodes remember the capture
         # stream, and an eager step on another stream would synchronise with it)
         self.disp_loss, self.error_loss = self.disp_loss.detach(), self.error_loss.detach()
+        if self._comm is not None and self.world > 1:
+            # the captured collective sequence must be the same on every rank
+            # (one ordered communicator, umamd.rccl): checked once, eagerly
+            rccl.check_order(self._comm)
         optimiser.prepare()  # tables for the graph-pool gradients, outside capture
         # the captured Adam reads these device tables by address: keep them
         # alive even if an eager step (another batch shape) replaces them
@@ -231,7 +235,7 @@ class CapturedTrainStep:
         self.g_fb = self.g_opt = None
         self._opt_tables = []
         if self._comm is not None:  # after the graphs that recorded its collectives
-            torch.cuda.synchronize()
+            self._comm.sync()
             rccl.release(self._comm)
             self._comm = None
 
@@ -240,6 +244,8 @@ class CapturedTrainStep:
             self.left.copy_(left)
         if right is not None:
             self.right.copy_(right)
+        if self._comm is not None:  # the collectives recorded in g_fb run on this stream
+            self._comm.note_stream(torch.cuda.current_stream())
         self.g_fb.replay()
         self.g_opt.replay()
         return self.disp_loss, self.error_loss

@@ -117,6 +117,9 @@ _SIG = {
     'um_sigmoid_scale_bwd': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
     'um_sigmoid_scale_bwd_split': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
     'um_head_split_fin': (_I, [_L, _I, _P, _I, _P, _F, _P, _I, 's']),
+    'um_disp_head_ok': (_I, [_I, _I, _I, _I, _I]),
+    'um_disp_head_fwd': (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, 's']),
+    'um_disp_head_dgrad': (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _I, _I, 's']),
     'um_pack_weight_split': (_I, [_P, _I, _I, _I, _I, _P, _P, _I, 's']),
     'um_attn_ws_kstats': (_L, [_I, _I, _I]),
     'um_attn_ws_ctx': (_L, [_I, _I, _I, _I]),

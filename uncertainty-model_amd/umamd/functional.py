@@ -1461,6 +1461,9 @@ def concat(sources: Sequence[CatSource], N, H, W, dtype):
 # (tools/bf16_arms.py, step-0 error loss vs the reference): 1.9e-3 -> 1.2e-3.
 # The 4 outputs pad to 8 GEMM columns anyway, so the split rows are free.
 _SPLIT_HEAD = os.environ.get('UMAMD_SPLIT_HEAD', '1') == '1'
+# round 6: the split heads on the one-pass kernels of csrc/disphead.hip
+# (UMAMD_ONEPASS_HEAD=0: the implicit-GEMM path of rounds 4-5)
+_ONEPASS_HEAD = os.environ.get('UMAMD_ONEPASS_HEAD', '1') == '1'
 
 
 class DispHeadFn(torch.autograd.Function):
@@ -1474,13 +1477,21 @@ class DispHeadFn(torch.autograd.Function):
         Kp = ceil8(K)
         bias_f = bias.detach().float().contiguous()
         split = _SPLIT_HEAD and x.dtype == torch.bfloat16 and 2 * K <= Kp
+        # the one-pass head kernels (csrc/disphead.hip): split weights, 4
+        # outputs, 3x3 reflect, C in {32..256}
+        onepass = split and _ONEPASS_HEAD and K == 4 and R == 3 and Kp == 8 and \
+            query('um_disp_head_ok', N, H, W, Cp, Cp) == 1
         if split:
             wf, wT = _pack(weight, Cp, x.dtype, ldT=Kp, split=True)
-            z = _conv_fwd(x, wf, None, 2 * K, R, 1, 1, L.PAD_REFLECT, out_dtype=torch.float32,
-                          creal=Creal)
             d = torch.empty((N, H, W, K), dtype=torch.float32, device=x.device)
-            call('um_head_split_fin', N * H * W, K, ptr(z), 2 * K, ptr(bias_f), float(scale),
-                 ptr(d), K)
+            if onepass:
+                call('um_disp_head_fwd', N, H, W, Cp, ptr(x), Cp, ptr(wf), ptr(bias_f),
+                     float(scale), ptr(d), K, work=_conv_flops(N, H, W, K, R, Creal))
+            else:
+                z = _conv_fwd(x, wf, None, 2 * K, R, 1, 1, L.PAD_REFLECT,
+                              out_dtype=torch.float32, creal=Creal)
+                call('um_head_split_fin', N * H * W, K, ptr(z), 2 * K, ptr(bias_f),
+                     float(scale), ptr(d), K)
             # the GEMM's algorithmic work is the 4-output conv (the split
             # rows are padding columns of the same MFMA tiles)
         else:
@@ -1489,6 +1500,7 @@ class DispHeadFn(torch.autograd.Function):
                           epi=L.EPI_SIGMOID_SCALE, epi_scale=scale, creal=Creal)
         ctx.scale = float(scale)
         ctx.split = split
+        ctx.onepass = onepass if split else False
         _use(ctx, x)
         ctx.save_for_backward(x, wT, d)
         ctx.geom = (K, Kp, Creal, R)
@@ -1511,9 +1523,17 @@ class DispHeadFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             tgt = _slot(ctx, 0)
-            dx = _give(ctx, 0, _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1, L.PAD_REFLECT,
-                                           dx=tgt, accumulate=tgt is not None, creal=Creal,
-                                           kreal=K))
+            if ctx.onepass:
+                dx = tgt if tgt is not None else torch.empty((N, H, W, Cp), dtype=x.dtype,
+                                                             device=x.device)
+                call('um_disp_head_dgrad', N, H, W, Cp, ptr(dl), Kp, ptr(wT), ptr(dx), Cp,
+                     int(tgt is not None), work=_conv_flops(N, H, W, K, R, Creal))
+                dx = _give(ctx, 0, dx)
+            else:
+                dx = _give(ctx, 0, _conv_dgrad(dl, wT, (N, H, W, Cp), Kp, R, 1, 1,
+                                               L.PAD_REFLECT, dx=tgt,
+                                               accumulate=tgt is not None, creal=Creal,
+                                               kreal=K))
         return dx, dW, db, None
 
 

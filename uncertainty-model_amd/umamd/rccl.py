@@ -47,6 +47,7 @@ communicator, ``release`` (CapturedTrainStep.close) destroys it
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 from typing import Dict, List, Optional
 
@@ -105,6 +106,7 @@ class _Order:
         self.last = None          # the stream of the previous collective
         self.events: List = []
         self.log: List = []       # ('wait', dst, src) / ('coll', stream) for tests
+        self.sig: List = []       # (numel, dtype) per collective: check_order
         self._record = record or _cuda_record
         self._wait = wait or _cuda_wait
 
@@ -112,6 +114,7 @@ class _Order:
         self.last = None
         self.events = []
         self.log = []
+        self.sig = []
 
     def before(self, stream):
         if self.last is not None and self.last != stream:
@@ -153,6 +156,13 @@ class Comm:
         self.comm = ctypes.c_void_p()
         _check(lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank),
                'ncclCommInitRank')
+        # every stream that issued (eagerly) or replayed (graphs) one of this
+        # communicator's collectives: close() waits for these streams only
+        self._streams: Dict[int, torch.cuda.Stream] = {}
+
+    def note_stream(self, stream):
+        """``stream`` runs (or replays) collectives of this communicator"""
+        self._streams[stream.cuda_stream] = stream
 
     def all_reduce(self, t: torch.Tensor, average: bool = False):
         """In-place sum (or average) of ``t`` over the ranks, on the current
@@ -166,19 +176,49 @@ class Comm:
         if dt is None:
             raise TypeError(f'umamd.rccl.all_reduce: dtype {t.dtype}')
         cur = torch.cuda.current_stream(t.device)
+        self.note_stream(cur)
         self.order.before(cur)
+        self.order.sig.append((int(t.numel()), str(t.dtype)))
         _check(_rccl().ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), dt,
                                      _AVG if average else _SUM, self.comm, cur.cuda_stream),
                'ncclAllReduce')
 
+    def sync(self):
+        """wait for every collective of this communicator issued so far: the
+        streams that issued or replayed them, not the whole device"""
+        for st in self._streams.values():
+            st.synchronize()
+
     def close(self):
-        """ncclCommDestroy (after the device has finished every collective
-        of this communicator; graphs that recorded them must be gone)."""
+        """ncclCommDestroy (after every collective of this communicator has
+        finished; graphs that recorded them must be gone)."""
         if self.comm is not None:
-            torch.cuda.synchronize()
+            self.sync()
             _check(_rccl().ncclCommDestroy(self.comm), 'ncclCommDestroy')
             self.comm = None
+        self._streams = {}
         self.order.reset()
+
+
+def check_order(comm, what='captured step'):
+    """Compare this communicator's collective sequence since its last
+    ``use`` (sizes and dtypes, in issue order) across the ranks, eagerly over
+    the process group: a rank whose host issued its collectives in another
+    order (hook or flush timing) fails here with the position of the first
+    difference, instead of the replayed graph hanging in RCCL."""
+    sig = list(comm.order.sig)
+    h = hashlib.sha256(repr(sig).encode()).hexdigest()
+    allh = [None] * comm.world
+    dist.all_gather_object(allh, (h, len(sig)), group=comm.group)
+    if any(x != allh[0] for x in allh):
+        sigs = [None] * comm.world
+        dist.all_gather_object(sigs, sig, group=comm.group)
+        first = next((i for i in range(max(map(len, sigs)))
+                      if len({repr(q[i]) if i < len(q) else None for q in sigs}) > 1), -1)
+        raise RuntimeError(f'umamd.rccl: the {what} issues its collectives in a different order '
+                           f'on different ranks (lengths {[len(q) for q in sigs]}, first '
+                           f'difference at collective {first}); its graph would deadlock')
+    return h
 
 
 # group key -> [Comm, users]
