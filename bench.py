@@ -374,7 +374,9 @@ def cpu_baseline(config, steps):
     warm-up + best of 2) and the best one times C2 (B=8 256x512 bayesian, the
     GPU workload's shape: ``value``), 1 warm-up + best of ``steps``.  On the
     GPU box os.cpu_count() shows the whole machine while a job's share is
-    smaller, so the sweep, not the core count, picks the threads."""
+    smaller, so the sweep, not the core count, picks the threads.  The C1
+    winner and its neighbours in the sweep (half, double) are then tried on
+    C2 itself (1 warm-up + 1 step each): C2's own best count times ``value``."""
     ncpu = os.cpu_count() or 1
     counts = [t for t in (4, 8, 16, 32, 64) if t <= ncpu] or [ncpu]
     sweep = {}
@@ -383,9 +385,17 @@ def cpu_baseline(config, steps):
         torch.set_num_threads(t)
         r, _, _ = _cpu_step_rate(cfg1, 128, 256, 2, 2)
         sweep[t] = round(r, 3)
-    threads = max(sweep, key=sweep.get)
+    best1 = max(sweep, key=sweep.get)
+    i1 = counts.index(best1)
+    cfg2 = load_cfg(config, 'bayesian')
+    sweep2 = {}
+    for t in counts[max(0, i1 - 1):i1 + 2]:
+        torch.set_num_threads(t)
+        r, _, _ = _cpu_step_rate(cfg2, 256, 512, 8, 1)
+        sweep2[t] = round(r, 3)
+    threads = max(sweep2, key=sweep2.get)
     torch.set_num_threads(threads)
-    c2, t2, ref0 = _cpu_step_rate(load_cfg(config, 'bayesian'), 256, 512, 8, steps)
+    c2, t2, ref0 = _cpu_step_rate(cfg2, 256, 512, 8, steps)
     cpu = ''
     try:
         with open('/proc/cpuinfo') as f:
@@ -404,8 +414,9 @@ def cpu_baseline(config, steps):
             'threads': threads, 'host_cpu_count': ncpu, 'affinity_physical_cores': phys,
             'host_physical_cores': host_phys, 'kind': 'port',
             'sample': f'oracle fp32 train step, C2 B=8 256x512 bayesian, 1 warm-up + best of '
-                      f'{steps} ({t2:.2f} s/step) at the best thread count of a C1 sweep; {cpu}',
-            'c1_thread_sweep_pairs_per_s': sweep}, ref0
+                      f'{steps} ({t2:.2f} s/step) at the best thread count of a C2 sweep '
+                      f'around the C1 sweep\'s winner; {cpu}',
+            'c1_thread_sweep_pairs_per_s': sweep, 'c2_thread_sweep': sweep2}, ref0
 
 
 # ---------------------------------------------------------- loader line ----

@@ -7,28 +7,29 @@
 // GEMM tiles it needed split-K plus a partial-sum epilogue (the 32x64 head:
 // 15.9 us GEMM + 21.7 us epilogue + 4.9 us finish) and the data gradient
 // padded the 8 dlogit channels of each tap to a 32-deep MFMA step (55-86 us
-// + a border pass of 11-15 us).  Here both directions are one pass over
-// their activations:
+// + a border pass of 11-15 us).  Here both directions are one pass:
 //   - 16-pixel strips (W % 16 == 0), MFMA operands loaded straight from
-//     global into registers (lane = pixel, 16 contiguous bytes of channels;
-//     the 9-fold tap re-reads hit L1/L2), the weights staged once per
-//     persistent workgroup in LDS (stream1x1's conflict-free 64-byte rows);
+//     global into registers (lane = pixel, 16 contiguous bytes of channels),
+//     the weights staged once per persistent workgroup in LDS (stream1x1's
+//     conflict-free 64-byte rows) or held in registers;
 //   - forward: D = W . X^T (v_mfma_f32_16x16x32_bf16, weights as the A
 //     operand, 8 of 16 rows live): a lane ends with 4 hi rows (kq = 0) or 4
 //     lo rows (kq = 1) of one pixel; one shuffle adds the halves, the
 //     epilogue adds the bias and applies scale*sigmoid, and the 4 disparity
 //     channels leave as one 16-byte store -- no f32 z round trip, no finish
-//     launch.  Narrow inputs (C <= 64) give every wave its own strips; wide
-//     ones (C = 128, 256: 64k / 16k pixels) split the 9*C/32 k-steps of a
-//     strip over the 4 waves of a workgroup and meet in LDS, so the grid has
-//     work for every SIMD;
-//   - data gradient: D = W^T . dL^T with 4 taps x 8 dlogit channels per
-//     32-deep k-step (3 steps for 9 taps), the reflect adjoint folded into
-//     the operand load: the tap source of an interior pixel is one 16-byte
-//     load; the pixels next to the border (rows/cols 1 and n-2) add their
-//     mirror sources (f32 sum, rounded once to bf16) -- no zero-pad pass +
-//     border pass.  Output: 4 consecutive channels per lane per 16-channel
-//     block (8-byte stores), optional accumulate.
+//     launch.  C <= 64: a wave walks a column of U output rows x 16 pixels,
+//     loading each of its U + 2 input rows ONCE per channel chunk; the
+//     column taps are that row moved one lane by DPP row shifts (the strip's
+//     outer neighbours loaded by lanes 0 / 15 only).  C = 128 / 256 (64k /
+//     16k pixels): the 9 C/32 k-steps of a strip are split over the 4 waves
+//     of a workgroup and meet in LDS, so the small grids reach every SIMD;
+//   - data gradient: D = W^T . dL^T with one tap ROW per 32-deep k-step (kq =
+//     tap column x 8 dlogit channels), so a column of U output rows needs U + 2
+//     input-row loads; the reflect adjoint is folded into the operand load
+//     (interior pixels: one 16-byte load; rows/cols 1 and n-2 add their
+//     mirror sources, f32 sum rounded once to bf16) -- no zero-pad pass +
+//     border pass.  Output rows go through LDS and leave as 16-byte rows
+//     (1 KB per instruction at C = 32), optional accumulate.
 #include <algorithm>
 
 #include "common.h"
@@ -268,6 +269,15 @@ __global__ void __launch_bounds__(256) dhead_fwd_dpp_kernel(DHFwd a, int units) 
     *reinterpret_cast<uint4*>(&sW[dh_img(kstep, 8, r, c8)]) = v;
   }
   __syncthreads();
+  // one channel chunk: the 9 tap fragments of this lane's weight row stay in
+  // registers for the whole persistent loop (no LDS read per MFMA)
+  constexpr bool AREG = KS == 1;
+  bf16x8_t wa[AREG ? DH_NTAP : 1];
+  if constexpr (AREG) {
+#pragma unroll
+    for (int k = 0; k < DH_NTAP; ++k)
+      wa[k] = px < 8 ? *reinterpret_cast<const bf16x8_t*>(&sW[dh_img(k, 8, px, kq)]) : bf16x8_t{};
+  }
   float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a.bias) bv = *reinterpret_cast<const float4*>(a.bias);
   for (; t < units; t += gridDim.x * 4) {
@@ -289,7 +299,9 @@ __global__ void __launch_bounds__(256) dhead_fwd_dpp_kernel(DHFwd a, int units) 
 #pragma unroll
           for (int tc = 0; tc < 3; ++tc) {
             bf16x8_t af = bf16x8_t{};
-            if (px < 8)
+            if constexpr (AREG)
+              af = wa[tr * 3 + tc];
+            else if (px < 8)
               af = *reinterpret_cast<const bf16x8_t*>(
                   &sW[dh_img((tr * 3 + tc) * KS + ks, 8, px, kq)]);
             acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, tc == 0 ? f0 : (tc == 1 ? f1 : f2),
@@ -490,6 +502,13 @@ __global__ void __launch_bounds__(256) dhead_dgrad_col_kernel(DHDgrad a, int uni
       return f;
     };
     if constexpr (STG) {
+      // the 3 x NB weight fragments of this lane, in registers (NB <= 4)
+      bf16x8_t wa[3][NB];
+#pragma unroll
+      for (int tr = 0; tr < 3; ++tr)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          wa[tr][nb] = *reinterpret_cast<const bf16x8_t*>(&sA[dh_img(tr, NR, nb * 16 + px, kq)]);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -497,8 +516,7 @@ __global__ void __launch_bounds__(256) dhead_dgrad_col_kernel(DHDgrad a, int uni
           f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int tr = 0; tr < 3; ++tr) {
-            const bf16x8_t af =
-                *reinterpret_cast<const bf16x8_t*>(&sA[dh_img(tr, NR, nb * 16 + px, kq)]);
+            const bf16x8_t af = wa[tr][nb];
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfrag(u, tr), acc, 0, 0, 0);
           }
           const float v[4] = {acc[0], acc[1], acc[2], acc[3]};
@@ -581,48 +599,38 @@ int um_disp_head_fwd(int N, int H, int W, int C, const void* x, int ldx, const v
   DHFwd a{(const bf16_t*)x, (const bf16_t*)wf, bias, d, N, H, W, C, ldx, ldd, scale};
   const long nstrips = (long)N * H * W / 16;
   const size_t lds = (size_t)DH_NTAP * (C / 32) * 8 * 32 * sizeof(bf16_t);
+  // measured (tools/head_micro.py, B=8 C2 heads): the DPP column kernel for
+  // C = 32 / 64 / 128 (28.5 -> 25.4 / 27.6 -> 19.7 us over the tap-shift
+  // loads; 21.3 -> 12.1 us over the k-split strips at C = 128), the k-split
+  // strip kernel for C = 256 (16k pixels).  dh_fwd = 1: the shift-load column
+  // kernel; dh_fwd128 = 0: the k-split strips at C = 128
+  static const int var = (int)umamd::tuning_env("dh_fwd", 0);
+  static const int var128 = (int)umamd::tuning_env("dh_fwd128", 1);
+  auto col_units = [&](int U) { return N * ((H + U - 1) / U) * (W / 16); };
   switch (C) {
-    case 32: {
-      static const int var = (int)umamd::tuning_env("dh_fwd", 0);
-      if (var == 1) {
-        const int units = N * ((H + 1) / 2) * (W / 16);
-        hipLaunchKernelGGL((dhead_fwd_col_kernel<1, 2>), dim3(dh_grid((units + 3) / 4)), dim3(256),
-                           lds, st, a, units);
-      } else if (var == 2) {
-        const int units = N * ((H + 7) / 8) * (W / 16);
-        hipLaunchKernelGGL((dhead_fwd_col_kernel<1, 8>), dim3(dh_grid((units + 3) / 4)), dim3(256),
-                           lds, st, a, units);
-      } else if (var == 3 || var == 4) {
-        const int units = N * ((H + 3) / 4) * (W / 16);
-        const int g = var == 3 ? dh_grid((units + 3) / 4) : std::min((units + 3) / 4, 768);
-        hipLaunchKernelGGL((dhead_fwd_dpp_kernel<1, 4>), dim3(g), dim3(256), lds, st, a, units);
-      } else if (var == 5) {
-        const int units = N * ((H + 7) / 8) * (W / 16);
-        hipLaunchKernelGGL((dhead_fwd_dpp_kernel<1, 8>), dim3(dh_grid((units + 3) / 4)), dim3(256),
-                           lds, st, a, units);
-      } else {
-        const int units = N * ((H + 3) / 4) * (W / 16);
-        hipLaunchKernelGGL((dhead_fwd_col_kernel<1, 4>), dim3(dh_grid((units + 3) / 4)), dim3(256),
-                           lds, st, a, units);
-      }
+    case 32:
+      if (var == 1)
+        hipLaunchKernelGGL((dhead_fwd_col_kernel<1, 4>), dim3(dh_grid((col_units(4) + 3) / 4)),
+                           dim3(256), lds, st, a, col_units(4));
+      else
+        hipLaunchKernelGGL((dhead_fwd_dpp_kernel<1, 4>), dim3(dh_grid((col_units(4) + 3) / 4)),
+                           dim3(256), lds, st, a, col_units(4));
       break;
-    }
-    case 64: {
-      static const int var = (int)umamd::tuning_env("dh_fwd", 0);
-      if (var >= 3) {
-        const int units = N * ((H + 3) / 4) * (W / 16);
-        hipLaunchKernelGGL((dhead_fwd_dpp_kernel<2, 4>), dim3(dh_grid((units + 3) / 4)), dim3(256),
-                           lds, st, a, units);
-      } else {
-        const int units = N * ((H + 1) / 2) * (W / 16);
-        hipLaunchKernelGGL((dhead_fwd_col_kernel<2, 2>), dim3(dh_grid((units + 3) / 4)), dim3(256),
-                           lds, st, a, units);
-      }
+    case 64:
+      if (var == 1)
+        hipLaunchKernelGGL((dhead_fwd_col_kernel<2, 2>), dim3(dh_grid((col_units(2) + 3) / 4)),
+                           dim3(256), lds, st, a, col_units(2));
+      else
+        hipLaunchKernelGGL((dhead_fwd_dpp_kernel<2, 4>), dim3(dh_grid((col_units(4) + 3) / 4)),
+                           dim3(256), lds, st, a, col_units(4));
       break;
-    }
     case 128:
-      hipLaunchKernelGGL((dhead_fwd_kernel<4, 4, 1>), dim3(dh_grid(nstrips)), dim3(256), lds, st, a,
-                         (int)nstrips);
+      if (var128 == 1)
+        hipLaunchKernelGGL((dhead_fwd_dpp_kernel<4, 2>), dim3(dh_grid((col_units(2) + 3) / 4)),
+                           dim3(256), lds, st, a, col_units(2));
+      else
+        hipLaunchKernelGGL((dhead_fwd_kernel<4, 4, 1>), dim3(dh_grid(nstrips)), dim3(256), lds, st,
+                           a, (int)nstrips);
       break;
     default:
       hipLaunchKernelGGL((dhead_fwd_kernel<8, 4, 1>), dim3(dh_grid(nstrips)), dim3(256), lds, st, a,
@@ -651,13 +659,15 @@ int um_disp_head_dgrad(int N, int H, int W, int C, const void* dl, int ldl, cons
     hipLaunchKernelGGL((dhead_dgrad_col_kernel<NB_, U_, S_>), dim3(dh_grid((units + 3) / 4)),    \
                        dim3(256), lds, st, a, units);                                           \
   }
+  // measured: LDS-staged 16-byte rows (STG) 36.8 -> 23.6 us (C = 32, U = 8) and
+  // 21.2 -> 12.1 us (C = 64, U = 4) over 8-byte stores; dh_dgrad = 0: unstaged
   static const int var = (int)umamd::tuning_env("dh_dgrad", 1);
   switch (C) {
     case 32:
-      if (var == 1) UM_DHC(2, 8, true) else if (var == 2) UM_DHC(2, 4, false) else if (var == 3) UM_DHC(2, 4, true) else UM_DHC(2, 8, false)
+      if (var == 0) UM_DHC(2, 8, false) else UM_DHC(2, 8, true)
       break;
     case 64:
-      if (var == 1 || var == 3) UM_DHC(4, 4, true) else if (var == 2) UM_DHC(4, 4, false) else if (var == 4) UM_DHC(4, 8, true) else UM_DHC(4, 8, false)
+      if (var == 0) UM_DHC(4, 8, false) else UM_DHC(4, 4, true)
       break;
     case 128: UM_DHD(8, 1); break;
     default: UM_DHD(16, 1); break;
