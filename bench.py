@@ -313,7 +313,47 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
                              'bytes_per_px': 56, 'pixels': px, 'ms_per_step': round(t, 4),
                              'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                              'frac': round(ach / HBM_PEAK_GBS, 4)}
+        out['loss_stack']['valu'] = loss_valu_report(
+            {k: (table[k]['launches_per_step'], table[k]['total_ms_per_step'])
+             for k in LOSS_KERNELS})
     return out
+
+
+# VALU issue peak (MI355X_MICROARCH.md: a wave issues each VALU instruction
+# over 2 cycles on its SIMD): CUs x 4 SIMDs x clock / 2 wave-instructions/s
+CU_COUNT, SIMDS_PER_CU, VALU_CYCLES_PER_INST, CLOCK_GHZ = 256, 4, 2, 2.4
+
+
+def loss_valu_report(launches):
+    """The loss stack against its VALU-issue bound (the counters say it is
+    VALU-bound): SQ_INSTS_VALU wave-instructions per launch from
+    the committed rocprofv3 pass (tools/gpu_pmc_valu.sh, digest-checked like
+    ``traffic``) over the HIP-event time of the same launches.
+    ``launches``: entry -> (launches per step, ms per step)."""
+    path = os.path.join(REPO, 'profiles', 'pmc_loss_valu.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pmc = json.load(f)
+    lib = lib_digest()
+    peak = CU_COUNT * SIMDS_PER_CU * CLOCK_GHZ * 1e9 / VALU_CYCLES_PER_INST  # wave-inst/s
+    rows, insts, ms = {}, 0.0, 0.0
+    for k, (n, t) in launches.items():
+        e = pmc.get(k)
+        if e is None or e.get('lib_digest') != lib:
+            return {'note': f'VALU counters of {k} missing or taken on another library build '
+                            f'({None if e is None else e.get("lib_digest")} vs loaded {lib})'}
+        i = e['per_launch'] * n
+        rows[k] = {'valu_insts_per_launch': round(e['per_launch']),
+                   'frac': round(i / (peak * t * 1e-3), 4)}
+        insts += i
+        ms += t
+    return {'bound': 'valu', 'valu_insts_per_step': round(insts), 'ms_per_step': round(ms, 4),
+            'peak_insts_per_s': peak, 'frac': round(insts / (peak * ms * 1e-3), 4),
+            'entries': rows,
+            'peak_basis': f'{CU_COUNT} CUs x {SIMDS_PER_CU} SIMDs x {CLOCK_GHZ} GHz / '
+                          f'{VALU_CYCLES_PER_INST} cycles per wave64 VALU instruction',
+            'source': pmc[next(iter(launches))].get('source')}
 
 
 def lib_digest():

