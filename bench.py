@@ -211,6 +211,44 @@ def conv_min_bytes(name, a):
     return None
 
 
+# the one-pass disparity heads (csrc/disphead.hip), HBM-bound
+HEAD_ENTRIES = {'um_disp_head_fwd': 'dhead_fwd_dpp_kernel / dhead_fwd_kernel',
+                'um_disp_head_dgrad': 'dhead_dgrad_col_kernel / dhead_dgrad_kernel',
+                'um_disp_head_wgrad': 'dhead_wgrad_kernel (+ um_conv_wgrad_reduce_seg)'}
+
+
+def head_min_bytes(name, a):
+    """compulsory HBM bytes of one head launch: fwd reads x (bf16, C) and
+    writes d (4 f32); dgrad reads dlogit (8 bf16) and writes dx (read too
+    when accumulating); wgrad reads x and dlogit (its slabs are an
+    implementation choice)"""
+    N, H, W, C = a[0], a[1], a[2], a[3]
+    M = N * H * W
+    if name == 'um_disp_head_fwd':
+        return M * (2 * C + 16)
+    if name == 'um_disp_head_dgrad':
+        return M * (16 + 2 * C * (2 if a[9] else 1))
+    return M * (2 * C + 16)
+
+
+def heads_report(groups):
+    rows, tot = [], 0.0
+    for name in HEAD_ENTRIES:
+        for a, ms, _ in groups.get(name, []):
+            b = head_min_bytes(name, a)
+            gbs = b / (ms * 1e-3) / 1e9
+            rows.append({'entry': name, 'N': a[0], 'H': a[1], 'W': a[2], 'C': a[3],
+                         'ms': round(ms, 4), 'min_hbm_bytes': b, 'achieved_gbs': round(gbs, 1),
+                         'frac': round(gbs / HBM_PEAK_GBS, 4)})
+            tot += ms
+    if not rows:
+        return None
+    return {'bound': 'hbm', 'launches_per_step': len(rows), 'total_ms_per_step': round(tot, 4),
+            'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'launches': rows,
+            'note': 'HIP events around each entry on the launch stream (one eager step); the '
+                    'wgrad entry is timed without its slab reduce launch'}
+
+
 def conv1x1_report(groups, peak):
     """Every 1x1 conv launch (forward and data gradient) against its own
     attainable rate min(P, AI * BW), AI = algorithmic FLOPs / compulsory
@@ -244,7 +282,7 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     the dominant kernel.  Conv work = algorithmic FLOPs with the real channel
     counts (2*N*P*Q*K*R*R*C per pass, attached at each call site)."""
     from umamd import _lib
-    rec = _lib.Recorder(set(CONV_ENTRIES) | set(LOSS_KERNELS))
+    rec = _lib.Recorder(set(CONV_ENTRIES) | set(LOSS_KERNELS) | set(HEAD_ENTRIES))
     with rec:
         step(m, lf, opt, left, right, scale)
     torch.cuda.synchronize()
@@ -254,6 +292,8 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
     peak = BF16_PEAK_TFLOPS if dtype == 'bf16' else F32_PEAK_TFLOPS
     table = {}
     for name, items in groups.items():
+        if name in HEAD_ENTRIES:
+            continue
         tot_ms = sum(ms for _, ms, _ in items)
         if name in LOSS_KERNELS:
             # args: nscales, N, H, W, ...
@@ -301,6 +341,7 @@ def measure_roofline(m, lf, opt, left, right, scale, dtype):
                                                   'launches_per_step', 'total_ms_per_step')}
                          for k, v in table.items()}
     out['conv1x1'] = conv1x1_report(groups, peak)
+    out['disp_heads'] = heads_report(groups)
     if all(k in groups for k in LOSS_KERNELS):
         # the fused loss stack (forward + backward launches) priced as SURVEY
         # 8d does: 56 B/px all-f32 (6 image + 4 prediction reads, 4 gradient
