@@ -212,23 +212,20 @@ def conv_min_bytes(name, a):
 
 
 # the one-pass disparity heads (csrc/disphead.hip), HBM-bound
+# (their weight gradients stay in um_conv2d_wgrad, the MFMA paths)
 HEAD_ENTRIES = {'um_disp_head_fwd': 'dhead_fwd_dpp_kernel / dhead_fwd_kernel',
-                'um_disp_head_dgrad': 'dhead_dgrad_col_kernel / dhead_dgrad_kernel',
-                'um_disp_head_wgrad': 'dhead_wgrad_kernel (+ um_conv_wgrad_reduce_seg)'}
+                'um_disp_head_dgrad': 'dhead_dgrad_col_kernel / dhead_dgrad_kernel'}
 
 
 def head_min_bytes(name, a):
     """compulsory HBM bytes of one head launch: fwd reads x (bf16, C) and
     writes d (4 f32); dgrad reads dlogit (8 bf16) and writes dx (read too
-    when accumulating); wgrad reads x and dlogit (its slabs are an
-    implementation choice)"""
+    when accumulating)"""
     N, H, W, C = a[0], a[1], a[2], a[3]
     M = N * H * W
     if name == 'um_disp_head_fwd':
         return M * (2 * C + 16)
-    if name == 'um_disp_head_dgrad':
-        return M * (16 + 2 * C * (2 if a[9] else 1))
-    return M * (2 * C + 16)
+    return M * (16 + 2 * C * (2 if a[9] else 1))
 
 
 def heads_report(groups):
@@ -245,8 +242,7 @@ def heads_report(groups):
         return None
     return {'bound': 'hbm', 'launches_per_step': len(rows), 'total_ms_per_step': round(tot, 4),
             'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'launches': rows,
-            'note': 'HIP events around each entry on the launch stream (one eager step); the '
-                    'wgrad entry is timed without its slab reduce launch'}
+            'note': 'HIP events around each entry on the launch stream (one eager step)'}
 
 
 def conv1x1_report(groups, peak):
