@@ -546,6 +546,27 @@ int um_stereo_prep(int N, int Hs, int Ws, const unsigned char* left,
                    const float* params, unsigned char* tmp, float* out_left, float* out_right,
                    hipStream_t stream);
 
+/* ------------------------------------------------ SyncBN exchange (IPC) ---
+ * SyncBatchNorm statistics exchanged device-side over IPC-mapped per-rank
+ * arenas instead of one RCCL all-reduce per layer and direction (reference
+ * parallel_main.py:156-158: torch SyncBatchNorm's all-reduce).  Host-only:
+ * um_bnx_bytes (arena size for nslots exchanges of <= max_c channels),
+ * um_bnx_alloc (uncached arena, zeroed, + its 64-byte hipIpcMemHandle_t),
+ * um_bnx_open / um_bnx_close (a peer's arena), um_bnx_free, um_bnx_status
+ * (1 if an exchange timed out waiting for a peer).  um_bnx_allreduce: the
+ * statistics slots `stats` ([UM_STAT_SLOTS][C][2] f64 + count) of this rank
+ * become the rank-ordered sum over all ranks (slot 0; slots 1.. zero; the
+ * global count after them) -- the in-place all-reduce of the slots.
+ * table: device array of the world arena base addresses (own at [rank]). */
+long um_bnx_bytes(int nslots, int max_c);
+int um_bnx_alloc(long bytes, void** base, void* handle64);
+int um_bnx_open(const void* handle64, void** ptr);
+int um_bnx_close(void* ptr);
+int um_bnx_free(void* base);
+int um_bnx_status(const void* base);
+int um_bnx_allreduce(double* stats, int C, const unsigned long long* table, int world, int rank,
+                     int slot, int nslots, int max_c, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -225,6 +225,51 @@ def run_order(rank, world, out):
                os.path.join(out, f'order_{rank}.pt'))
 
 
+def run_bnx(rank, world, out):
+    """umamd.bnx on two processes sharing cuda:0: statistics-slot tensors of
+    several widths exchanged over the IPC arenas, three steps of 5 slots;
+    every rank must end with the rank-ordered sum of the ranks' slot sums
+    (computed here from the same seeded draws), bit for bit."""
+    from umamd import bnx
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    x = bnx.BNExchange(dist.group.WORLD)
+    widths = [16, 64, 512, 1024, 40]
+    results = []
+    for step in range(3):
+        x.begin_forward()
+        outs = []
+        for i, C in enumerate(widths):
+            def draw(r):
+                g = torch.Generator().manual_seed(1000 * step + 10 * i + r)
+                t = torch.randn(16 * C * 2 + 1, generator=g, dtype=torch.float64)
+                t[-1] = 100 + r
+                return t
+            mine = draw(rank).to(dev)
+            x.all_reduce_slots(mine, C)
+            # expected: per rank the 16 slots summed in slot order, then the
+            # ranks in rank order (the kernel's order)
+            exp = torch.zeros(2 * C + 1, dtype=torch.float64)
+            for r in range(world):
+                d = draw(r)
+                v = torch.zeros(2 * C, dtype=torch.float64)
+                for sl in range(16):
+                    v = v + d[sl * 2 * C:(sl + 1) * 2 * C]
+                exp[:2 * C] = exp[:2 * C] + v
+                exp[2 * C] = exp[2 * C] + d[-1]
+            outs.append((mine.cpu(), exp))
+        torch.cuda.synchronize()
+        for got, exp in outs:
+            C2 = exp.numel() - 1
+            assert torch.equal(got[:C2], exp[:C2]), (step, float((got[:C2] - exp[:C2]).abs().max()))
+            assert torch.equal(got[C2:16 * C2], torch.zeros(15 * C2, dtype=torch.float64))
+            assert float(got[-1]) == float(exp[-1])
+        results.append(len(outs))
+    x.check()
+    x.close()
+    torch.save({'steps': torch.tensor(len(results))}, os.path.join(out, f'bnx_{rank}.pt'))
+
+
 def run_step(mode, rank, world, out):
     from train.loss import TukraUncertaintyLoss
     from train.parallel import data_parallel, unwrap
@@ -251,20 +296,29 @@ def run_step(mode, rank, world, out):
     # all-reduced (averaged) bucket views
     grads = {n: p.grad.detach().clone().cpu() for n, p in unwrap(m).named_parameters()}
     sd = {k: v.detach().clone().cpu() for k, v in unwrap(m).state_dict().items()}
+    from umamd import bnx
+    nx = 0
+    for x in bnx._exchanges.values():  # UMAMD_SYNCBN_IPC=1: the exchanges this step used
+        x.check()
+        nx += x.slot
+    bnx.close_all()
     torch.save({'disp': torch.tensor(float(dl)), 'err': torch.tensor(float(el)),
-                'grads': grads, 'state': sd}, os.path.join(out, f'{mode}_{rank}.pt'))
+                'grads': grads, 'state': sd, 'bnx_exchanges': torch.tensor(nx)},
+               os.path.join(out, f'{mode}_{rank}.pt'))
 
 
 def main():
     mode, out = sys.argv[1], sys.argv[2]
     rank = int(os.environ.get('RANK', '0'))
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    if mode in ('cpu', 'order', 'ddp', 'ddp_uneven'):
+    if mode in ('cpu', 'order', 'ddp', 'ddp_uneven', 'bnx'):
         dist.init_process_group('gloo', init_method='env://', rank=rank, world_size=world)
     if mode == 'cpu':
         run_cpu(rank, world, out)
     elif mode == 'order':
         run_order(rank, world, out)
+    elif mode == 'bnx':
+        run_bnx(rank, world, out)
     else:
         run_step(mode, rank, world, out)
     if dist.is_initialized():

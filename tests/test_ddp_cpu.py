@@ -18,9 +18,9 @@ def free_port():
         return s.getsockname()[1]
 
 
-def launch(mode, world, out, timeout=300):
+def launch(mode, world, out, timeout=300, **extra_env):
     env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(free_port()),
-               WORLD_SIZE=str(world))
+               WORLD_SIZE=str(world), **extra_env)
     procs = []
     for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r))

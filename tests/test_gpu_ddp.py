@@ -14,11 +14,14 @@ from test_gpu_model import _pre_bn_bias
 pytestmark = pytest.mark.gpu
 
 
-def test_syncbn_ddp_matches_single_process(tmp_path):
+def test_syncbn_ddp_matches_single_process(tmp_path, ipc=False):
     launch('single', 1, str(tmp_path))
-    launch('ddp', 2, str(tmp_path))
+    launch('ddp', 2, str(tmp_path), **({'UMAMD_SYNCBN_IPC': '1'} if ipc else {}))
     s = torch.load(tmp_path / 'single_0.pt', weights_only=True)
     r = [torch.load(tmp_path / f'ddp_{i}.pt', weights_only=True) for i in range(2)]
+    # every BN statistics exchange on the IPC path (40 forward + 40
+    # backward) or none of them
+    assert [int(x['bnx_exchanges']) for x in r] == ([80, 80] if ipc else [0, 0])
     for key in ('disp', 'err'):
         mean = (float(r[0][key]) + float(r[1][key])) / 2
         assert abs(mean - float(s[key])) <= 1e-4 * abs(float(s[key])), (key, mean, float(s[key]))

@@ -118,6 +118,13 @@ _SIG = {
     'um_sigmoid_scale_bwd_split': (_I, [_I, _L, _I, _P, _I, _P, _I, _F, _P, _I, 's']),
     'um_head_split_fin': (_I, [_L, _I, _P, _I, _P, _F, _P, _I, 's']),
     'um_disp_head_ok': (_I, [_I, _I, _I, _I, _I]),
+    'um_bnx_bytes': (_L, [_I, _I]),
+    'um_bnx_alloc': (_I, [_L, _P, _P]),
+    'um_bnx_open': (_I, [_P, _P]),
+    'um_bnx_close': (_I, [_P]),
+    'um_bnx_free': (_I, [_P]),
+    'um_bnx_status': (_I, [_P]),
+    'um_bnx_allreduce': (_I, [_P, _I, _P, _I, _I, _I, _I, _I, 's']),
     'um_disp_head_fwd': (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, 's']),
     'um_disp_head_dgrad': (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _I, _I, 's']),
     'um_pack_weight_split': (_I, [_P, _I, _I, _I, _I, _P, _P, _I, 's']),

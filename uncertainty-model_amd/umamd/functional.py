@@ -31,6 +31,7 @@ import torch.distributed as dist
 from . import _lib as L
 from . import overlap as _overlap
 from . import packer as _packer
+from . import bnx as _bnx
 from . import rccl as _rccl
 from ._lib import call, ptr, query
 
@@ -351,6 +352,7 @@ def stat_scope(arena: Optional[StatArena], device):
     try:
         if _ARENA is not None:
             _ARENA.begin(device)
+            _bnx.begin_forward()  # SyncBN IPC exchange slots count from each forward
         yield
     finally:
         if _ARENA is not None:
@@ -516,6 +518,18 @@ class BNSync:
             else:
                 dist.all_reduce(t, group=self.group)
 
+    def all_reduce_slots(self, t: torch.Tensor, C: int):
+        """in-place all-reduce of a statistics-slot tensor ([16][C][2] f64 +
+        count): over the IPC exchange (umamd.bnx, UMAMD_SYNCBN_IPC=1) -- one
+        kernel, no RCCL call -- else as all_reduce"""
+        if not self.collective:
+            return
+        x = _bnx.get(self.group) if self.world > 1 else None
+        if x is not None:
+            x.all_reduce_slots(t, C)
+        else:
+            self.all_reduce(t)
+
 
 def _bn_forward_coeffs(parts, nparts, K, count, bn, sync: BNSync, training: bool, device):
     mean = torch.empty(K, dtype=torch.float32, device=device)
@@ -615,7 +629,7 @@ def _cbe_fwd(x, weight, bias, gamma, beta, w1, w2, spec: ConvSpec, merge=None, y
                       out_dtype=_ydtype(x.dtype), epi=L.EPI_STAT_SLOTS, stats=slots_f,
                       creal=Creal) if yconv is None else yconv(L.EPI_STAT_SLOTS, slots_f, bias_f)
         if sync.collective:  # the conv stored this rank's count after the slots
-            sync.all_reduce(slots_f)
+            sync.all_reduce_slots(slots_f, K)
             count = -1.0  # read the all-reduced count after the slots
         mean = torch.empty(K, dtype=torch.float32, device=dev)
         invstd = torch.empty_like(mean)
@@ -752,7 +766,7 @@ def _cbe_bwd(ctx, da, ds=None, need_x=True, need_b=True, dx=None, dx_accumulate=
             # reference, parallel_main.py:156-158).  A caller that SUMS the
             # ranks' gradients gets G from both forms: also equal; one that
             # keeps per-rank gradients without any reduction is not supported
-            ctx.sync.all_reduce(slots_b)
+            ctx.sync.all_reduce_slots(slots_b, K)
             bcount, bscale = -1.0, 1.0 / ctx.sync.world
     elif ctx.has_bn:
         k1 = torch.empty(K, dtype=torch.float32, device=dev)
