@@ -265,9 +265,24 @@ def run_bnx(rank, world, out):
             assert torch.equal(got[C2:16 * C2], torch.zeros(15 * C2, dtype=torch.float64))
             assert float(got[-1]) == float(exp[-1])
         results.append(len(outs))
+    # time: 40 exchanges (one step's forward) of C = 256, both ranks in lockstep
+    t = torch.zeros(16 * 256 * 2 + 1, dtype=torch.float64, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for rep in range(3):
+        x.begin_forward()
+        dist.barrier()
+        torch.cuda.synchronize()
+        ev[0].record()
+        for _ in range(40):
+            x.all_reduce_slots(t, 256)
+        ev[1].record()
+        ev[1].synchronize()
+    us = ev[0].elapsed_time(ev[1]) * 1e3 / 40
+    print(f'bnx rank {rank}: {us:.2f} us per exchange (C=256, 2 processes on one GPU)', flush=True)
     x.check()
     x.close()
-    torch.save({'steps': torch.tensor(len(results))}, os.path.join(out, f'bnx_{rank}.pt'))
+    torch.save({'steps': torch.tensor(len(results)), 'us_per_exchange': torch.tensor(us)},
+               os.path.join(out, f'bnx_{rank}.pt'))
 
 
 def run_step(mode, rank, world, out):

@@ -18,7 +18,9 @@ def test_bnx_exchange_two_processes(tmp_path):
     count; no exchange timed out (um_bnx_status)"""
     launch('bnx', 2, str(tmp_path), timeout=240)
     for r in range(2):
-        assert int(torch.load(tmp_path / f'bnx_{r}.pt', weights_only=True)['steps']) == 3
+        z = torch.load(tmp_path / f'bnx_{r}.pt', weights_only=True)
+        assert int(z['steps']) == 3
+        print(f'rank {r}: {float(z["us_per_exchange"]):.2f} us per exchange')
 
 
 def test_syncbn_ddp_ipc_matches_single_process(tmp_path):
