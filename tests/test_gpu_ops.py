@@ -943,6 +943,25 @@ def test_conv_bn_elu_ybf16(case, monkeypatch):
                                   (1, 129, 131, 96, 32, 'dgrad'), (2, 64, 128, 64, 192, 'bias'),
                                   (1, 128, 130, 192, 64, 'dgrad'), (2, 64, 128, 128, 128, 'up2stats')])
 def test_stream1x1(case):
+    _check_1x1(case, b's1x1')
+
+
+# the small-M 1x1 kernel (stream1x1.hip s1x1_small_kernel, tuning key
+# s1x1_small, M in [256, 16384) pixels) against the GEMM tiles it replaces and
+# f64 torch: the deep layers' shapes (attention K/Q/V and reprojection at
+# 8x16 .. 32x64, C up to 512 = 16 k-steps held in registers), ragged pixel
+# counts, reduction widths padded to the next power-of-two k-step count, the
+# same epilogues; M < 256 stays on the GEMM (both arms)
+@pytest.mark.parametrize('case', [(2, 16, 32, 256, 512, 'bias'), (2, 16, 32, 512, 256, 'residual'),
+                                  (1, 33, 35, 64, 32, 'f32'), (2, 32, 64, 128, 64, 'up2stats'),
+                                  (1, 31, 33, 96, 32, 'dgrad'), (2, 8, 16, 512, 512, 'dgrad'),
+                                  (2, 16, 32, 320, 64, 'bias'), (1, 8, 16, 64, 32, 'bias'),
+                                  (1, 62, 64, 256, 512, 'up2stats'), (2, 8, 32, 512, 48, 'residual')])
+def test_s1x1_small(case):
+    _check_1x1(case, b's1x1_small')
+
+
+def _check_1x1(case, key):
     from umamd import functional as U
     from umamd import _lib as L
     from umamd._lib import PAD_ZERO, call, lib, ptr
@@ -979,13 +998,13 @@ def test_stream1x1(case):
         _, wTd = U._pack(wfw, K, torch.bfloat16)
         outs = []
         for flag in (1, 0):
-            old = lib().um_set_tuning(b's1x1', flag)
+            old = lib().um_set_tuning(key, flag)
             try:
                 dx = prev[..., :K].contiguous().clone()
                 U._conv_dgrad(x, wTd, (N, H, W, K), C, 1, 1, 0, PAD_ZERO, dx=dx, accumulate=True)
                 torch.cuda.synchronize()
             finally:
-                lib().um_set_tuning(b's1x1', old)
+                lib().um_set_tuning(key, old)
             outs.append(dx.double())
         ref = prev[..., :K].double() + torch.einsum('nhwc,ck->nhwk', x.double(),
                                                     wfw.to(torch.bfloat16).double()[:, :, 0, 0])
@@ -993,12 +1012,12 @@ def test_stream1x1(case):
         return
     outs = []
     for flag in (1, 0):
-        old = lib().um_set_tuning(b's1x1', flag)
+        old = lib().um_set_tuning(key, flag)
         try:
             outs.append(run())
             torch.cuda.synchronize()
         finally:
-            lib().um_set_tuning(b's1x1', old)
+            lib().um_set_tuning(key, old)
     ref = torch.einsum('nhwc,kc->nhwk', x.double(), wq)
     if mode != 'f32':
         ref = ref + bias.double()

@@ -262,21 +262,36 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_reduce_kernel(
       load8(invstd + c, is);
       load8(scale + c, sc);
       load8(shift + c, sh);
-#pragma unroll 4
-      for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
-        float dv[8], yv[8], ad[8];
+      // SE layers: add[n][c] (n = m / HW) is one vector for a block inside one
+      // image (the row blocks are 16..1024 rows, the images 1k..128k pixels):
+      // loaded once, no per-row 64-bit division and table load
+      const bool one_img = add_nc && m0 / HW == (m1 - 1) / HW;
+      float ad0[8];
+      if (one_img) load8(add_nc + (m0 / HW) * C + c, ad0);
+      auto row = [&](long m, const float* ad) {
+        float dv[8], yv[8];
         load8(da + m * ldda + c, dv);
         load8(y + m * ldy + c, yv);
-        if (add_nc) load8(add_nc + (m / HW) * C + c, ad);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float d = dv[e] + (add_nc ? ad[e] : 0.f);
+          float d = dv[e] + (ad ? ad[e] : 0.f);
           if (apply_elu) {
             const float z = yv[e] * sc[e] + sh[e];
             d = z > 0.f ? d : d * __expf(z);
           }
           acc[e] += d;
           acc[8 + e] += d * (yv[e] - mu[e]) * is[e];
+        }
+      };
+      if (!add_nc || one_img) {
+#pragma unroll 4
+        for (long m = m0 + rm.lane; m < m1; m += rm.lanes) row(m, add_nc ? ad0 : nullptr);
+      } else {
+#pragma unroll 2
+        for (long m = m0 + rm.lane; m < m1; m += rm.lanes) {
+          float ad[8];
+          load8(add_nc + (m / HW) * C + c, ad);
+          row(m, ad);
         }
       }
     }
@@ -427,9 +442,18 @@ __global__ void __launch_bounds__(256) bn_elu_bwd_apply_kernel(
           D[e] = -a1[e] * a2[e] + a1[e] * a3[e] * mu[e] * is[e];
         }
       }
+      // SE add vector hoisted for a block inside one image (as the reduce)
+      const bool one_img = add_nc && m0 / HW == (m1 - 1) / HW;
+      float ad0[8];
+      if (one_img) load8(add_nc + (m0 / HW) * C + c, ad0);
       auto row = [&](long m, const float* dv, const float* yv) {
         float ad[8], o[8];
-        if (add_nc) load8(add_nc + (m / HW) * C + c, ad);
+        if (one_img) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ad[e] = ad0[e];
+        } else if (add_nc) {
+          load8(add_nc + (m / HW) * C + c, ad);
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float d = dv[e] + (add_nc ? ad[e] : 0.f);

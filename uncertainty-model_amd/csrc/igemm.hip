@@ -948,7 +948,7 @@ struct Knobs {
   int halo_persist, halo_grid, halo_res_kb;
   int halo_staged;
   int border_valu;
-  int s1x1;
+  int s1x1, s1x1_small;
   Knobs() {
     auto env = [](const char* n, int d) { return (int)umamd::tuning_env(n, d); };
     small = env("small", 1);
@@ -1026,6 +1026,8 @@ struct Knobs {
     // high-resolution 1x1 convs (M >= 16k, C <= 256, N <= 192) on the
     // streaming kernel (stream1x1.hip) instead of 256-row GEMM tiles
     s1x1 = env("s1x1", 1);
+    // small-M 1x1 convs (stream1x1.hip s1x1_small_kernel, M < 16k pixels)
+    s1x1_small = env("s1x1_small", 1);
   }
 };
 Knobs& knobs() {
@@ -1244,6 +1246,7 @@ int igemm_run(int dtype, const IgArgs& a_in, float* ws, long ws_bytes, hipStream
     return launch_cls<float, 32, 64, 64, 2, 2, 2>(a, p, ws, st);
   }
   if (knobs().s1x1 && stream1x1_applicable(dtype, a)) return stream1x1_run(a, st);
+  if (knobs().s1x1_small && s1x1_small_applicable(dtype, a)) return s1x1_small_run(a, st);
   // 8-channel operands take the tap-packed GEMM instead of the halo kernel
   // (which stages 32-channel chunks) unless tappack bit 1 is clear
   const bool pack_first = (knobs().tappack & 3) == 3 && a.ach == 8;
@@ -1459,6 +1462,7 @@ extern "C" int um_set_tuning(const char* key, int value) {
   else if (!strcmp(key, "halo_staged")) f = &k.halo_staged;
   else if (!strcmp(key, "border_valu")) f = &k.border_valu;
   else if (!strcmp(key, "s1x1")) f = &k.s1x1;
+  else if (!strcmp(key, "s1x1_small")) f = &k.s1x1_small;
   if (!f) return -1;
   const int old = *f;
   *f = value;

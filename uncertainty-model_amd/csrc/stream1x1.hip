@@ -181,6 +181,123 @@ __global__ void __launch_bounds__(256) stream1x1_kernel(IgArgs a, int nb, long n
   }
 }
 
+// Small-M 1x1 convolutions (round 6): the deep 8x16 .. 32x64 layers (M = 1k
+// .. 16k pixels, C <= 512 reduction channels, N up to 1536: the attention's
+// fused K/Q/V and reprojection, the decoder's first squeeze-excite 1x1, and
+// their data gradients).  On 64x64 GEMM tiles these were 16-32 sequential
+// k-steps per block with split-K epilogues (9-22 us for 0.5-1.6 GFLOP).  Here
+// a workgroup owns NG 16-channel output blocks (grid.y) and stages only their
+// weights (NG*16 rows x C, <= 64 KB) in LDS; each wave takes 16-pixel strips
+// whose KS activation fragments (the whole reduction) it loads into registers
+// at once -- one round of load latency per strip, no k-loop barrier -- then
+// runs the KS x NG MFMAs (D = W . A^T as stream1x1_kernel: each lane ends with
+// 4 consecutive output channels of one pixel) and the same epilogues (bias,
+// residual, f32 output, accumulate, BN statistics into f64 slots).
+template <int KS, int NG, bool F32, bool STATS>
+__global__ void __launch_bounds__(256) s1x1_small_kernel(IgArgs a, long nstrips) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t sW[];  // KS x (NG*16) x 32
+  __shared__ float sStat[STATS ? 4 : 1][STATS ? NG * 16 : 1][2];
+  constexpr int NR = NG * 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n0 = blockIdx.y * NR;  // this workgroup's first output channel
+  const bf16_t* __restrict__ wsrc = reinterpret_cast<const bf16_t*>(a.b);
+  for (int i = tid; i < NR * KS * 4; i += 256) {
+    const int n = i / (KS * 4), c8 = i - n * (KS * 4), c = c8 * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n0 + n < a.NC && c < a.ach) v = *reinterpret_cast<const uint4*>(wsrc + (long)(n0 + n) * a.ldb + c);
+    *reinterpret_cast<uint4*>(&sW[wimg(c8 >> 2, NR, n, c8 & 3)]) = v;
+  }
+  __syncthreads();
+  const bf16_t* __restrict__ act = reinterpret_cast<const bf16_t*>(a.a);
+  const int px = lane & 15, kq = lane >> 4;
+  float st1[STATS ? NG : 1][4], st2[STATS ? NG : 1][4];
+  if constexpr (STATS) {
+#pragma unroll
+    for (int b = 0; b < NG; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st1[b][j] = st2[b][j] = 0.f;
+  }
+  for (long t = (long)blockIdx.x * 4 + w; t < nstrips; t += (long)gridDim.x * 4) {
+    const long m = t * 16 + px;
+    bf16x8_t af[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c = ks * 32 + kq * 8;
+      af[ks] = (m < a.M && c < a.ach) ? *reinterpret_cast<const bf16x8_t*>(act + m * a.lda + c)
+                                      : bf16x8_t{};
+    }
+    f32x4_t acc[NG];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        const bf16x8_t wf = *reinterpret_cast<const bf16x8_t*>(&sW[wimg(ks, NR, q * 16 + px, kq)]);
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, af[ks], acc[q], 0, 0, 0);
+      }
+    if (m >= a.M) continue;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const int n = n0 + q * 16 + kq * 4;
+      if (n >= a.NC) break;
+      float v[4] = {acc[q][0], acc[q][1], acc[q][2], acc[q][3]};
+      if (a.bias != nullptr) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += a.bias[n + j];
+      }
+      if (a.epilogue == UM_EPI_RESIDUAL)
+        add4(reinterpret_cast<const bf16_t*>(a.residual) + m * a.ldr + n, v);
+      if constexpr (F32) {
+        float* o = reinterpret_cast<float*>(a.out) + m * a.ld_out + n;
+        if (a.accumulate) {
+          const float4 p = *reinterpret_cast<const float4*>(o);
+          v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+        }
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + m * a.ld_out + n;
+        if (a.accumulate) add4(o, v);
+        uint2 r;
+        r.x = pack_bf16x2(v[0], v[1]);
+        r.y = pack_bf16x2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(o) = r;
+      }
+      if constexpr (STATS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          st1[q][j] += v[j];
+          st2[q][j] += v[j] * v[j];
+        }
+      }
+    }
+  }
+  if constexpr (STATS) {
+#pragma unroll
+    for (int b = 0; b < NG; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x = st1[b][j], y = st2[b][j];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          x += __shfl_xor(x, o, 64);
+          y += __shfl_xor(y, o, 64);
+        }
+        if (px == 0) {
+          sStat[w][b * 16 + kq * 4 + j][0] = x;
+          sStat[w][b * 16 + kq * 4 + j][1] = y;
+        }
+      }
+    __syncthreads();
+    double* slots = reinterpret_cast<double*>(a.stats);
+    stat_slots_count(slots, a.NC, a.M);
+    stat_slots_add_row(slots, blockIdx.x, a.NC, n0, min(NR, a.NC - n0), [&](int i) {
+      return sStat[0][i >> 1][i & 1] + sStat[1][i >> 1][i & 1] + sStat[2][i >> 1][i & 1] +
+             sStat[3][i >> 1][i & 1];
+    });
+  }
+}
+
 }  // namespace
 
 namespace umamd {
@@ -207,6 +324,76 @@ bool stream1x1_applicable(int dtype, const IgArgs& a) {
   if (a.epilogue == UM_EPI_STATS)
     return a.stat_slots && a.out_f32 && a.NC <= 16 * S1STATNB && a.stats != nullptr;
   return false;
+}
+
+static int small_ks(int ach) {
+  const int k = (ach + 31) / 32;
+  return k <= 2 ? (k <= 1 ? 1 : 2) : (k <= 4 ? 4 : (k <= 8 ? 8 : (k <= 16 ? 16 : 0)));
+}
+
+// the small-M 1x1 path (s1x1_small_kernel): M < 16384 pixels (the streaming
+// kernel's lower bound), C <= 512, N a multiple of 16, the same operand and
+// epilogue conditions as stream1x1 (igemm's knob s1x1_small, 0 = off)
+bool s1x1_small_applicable(int dtype, const IgArgs& a) {
+  if (dtype != UM_BF16 || a.R != 1 || a.Rx != 1 || a.stride != 1 || a.pad != 0 ||
+      a.padx != 0 || a.cls || a.border || a.pmode != IG_PAD_ZERO || a.oh != a.ah || a.ow != a.aw)
+    return false;
+  // NC <= 512: wider outputs (the attention's fused 768/1536-channel K/Q/V)
+  // re-stage their weights once per 64 pixels and measured slower than the
+  // GEMM tiles (tools/conv_table.py, 16 -> 25 us)
+  if (a.M >= 16384 || a.M < 256 || a.ach % 8 || a.lda % 8 || a.ld_out % 8 || a.NC % 16 ||
+      a.NC > 512)
+    return false;
+  if (small_ks(a.ach) == 0) return false;
+  auto al = [](const void* p, int b) { return (reinterpret_cast<uintptr_t>(p) % b) == 0; };
+  if (!al(a.a, 16) || !al(a.b, 16) || !al(a.out, a.out_f32 ? 16 : 8) ||
+      (a.residual != nullptr && !al(a.residual, 8)))
+    return false;
+  if (a.epilogue == UM_EPI_NONE) return true;
+  if (a.epilogue == UM_EPI_RESIDUAL) return !a.out_f32 && a.ldr % 4 == 0 && a.residual != nullptr;
+  if (a.epilogue == UM_EPI_STATS) return a.stat_slots && a.out_f32 && a.stats != nullptr;
+  return false;
+}
+
+int s1x1_small_run(const IgArgs& a, hipStream_t st) {
+  const int ks = small_ks(a.ach);
+  const long nstrips = ((long)a.M + 15) / 16;
+  const int nb = a.NC / 16;
+  // 4 output blocks (64 channels) per workgroup, 2 when that leaves < 256
+  // workgroups; strips: one per wave while the grid stays <= 1024 workgroups
+  // (KS = 16 keeps two: 16 activation fragments + 4 weight blocks exceed the
+  // register file at one wave per SIMD)
+  const int ng = (ks < 16 && (long)ceil_div(nstrips, 4) * ceil_div(nb, 4) >= 256) ? 4 : 2;
+  const int gy = ceil_div(nb, ng);
+  const long gx = std::max<long>(1, std::min<long>(ceil_div(nstrips, 4), std::max<long>(1, 1024 / gy)));
+  const size_t lds = (size_t)ks * ng * 16 * 32 * sizeof(bf16_t);
+  const bool stats = a.epilogue == UM_EPI_STATS;
+#define UM_S1S(KS_, NG_, F32_, ST_)                                                               \
+  hipLaunchKernelGGL((s1x1_small_kernel<KS_, NG_, F32_, ST_>), dim3((int)gx, gy), dim3(256), lds, st, \
+                     a, nstrips)
+#define UM_S1SK(NG_, F32_, ST_)                    \
+  switch (ks) {                                    \
+    case 1: UM_S1S(1, NG_, F32_, ST_); break;      \
+    case 2: UM_S1S(2, NG_, F32_, ST_); break;      \
+    case 4: UM_S1S(4, NG_, F32_, ST_); break;      \
+    case 8: UM_S1S(8, NG_, F32_, ST_); break;      \
+    default: UM_S1S(16, NG_, F32_, ST_); break;    \
+  }
+#define UM_S1SN(F32_, ST_)              \
+  if (ng == 4) { UM_S1SK(4, F32_, ST_) } \
+  else { UM_S1SK(2, F32_, ST_) }
+  if (stats) {
+    UM_S1SN(true, true)
+  } else if (a.out_f32) {
+    UM_S1SN(true, false)
+  } else {
+    UM_S1SN(false, false)
+  }
+#undef UM_S1SN
+#undef UM_S1SK
+#undef UM_S1S
+  UM_LAUNCH_CHECK();
+  return UM_OK;
 }
 
 int stream1x1_run(const IgArgs& a, hipStream_t st) {
