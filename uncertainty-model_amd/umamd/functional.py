@@ -1354,8 +1354,16 @@ class AttentionFn(torch.autograd.Function):
              ptr(r))
         dwqkv = _conv_wgrad(x, dqkv, 3 * C, 3 * C, C, 1, 1, 0, L.PAD_ZERO)
         dbqkv = _colsum_grad(dqkv, 3 * C)
-        dx = dout.clone() if dout.dtype == dt else dout.to(dt)
-        _conv_dgrad(dqkv, wT, (N, H, W, C), 3 * C, 1, 1, 0, L.PAD_ZERO, dx=dx, accumulate=True)
+        if dout.dtype == dt:
+            # dx = dout (the residual path) + the K/Q/V convs' input gradient:
+            # wT [C][3C] is the weight of a 3C -> C 1x1 conv, so this is one
+            # forward GEMM with the residual epilogue (no copy of dout first)
+            dx = _conv_fwd(dqkv, wT, None, C, 1, 1, 0, L.PAD_ZERO, epi=L.EPI_RESIDUAL,
+                           residual=dout)
+        else:
+            dx = dout.to(dt)
+            _conv_dgrad(dqkv, wT, (N, H, W, C), 3 * C, 1, 1, 0, L.PAD_ZERO, dx=dx,
+                        accumulate=True)
         return (dx, dwqkv[:C], dbqkv[:C], dwqkv[C:2 * C], dbqkv[C:2 * C], dwqkv[2 * C:],
                 dbqkv[2 * C:], dwr, dbr, None)
 
