@@ -648,21 +648,49 @@ __global__ void __launch_bounds__(256) se_mlp_fwd_kernel(
     }
     __syncthreads();
   }
-  // z = relu(W1 p): one wave per output row, lanes over the C inputs
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int r = wave; r < R; r += 4) {
+  // z = relu(W1 p): LP lanes per output row (all R rows in one pass for R <=
+  // 256 / LP), each lane 4 inputs per 16-byte load with every load of its
+  // slice issued before the sums -- one round of load latency instead of
+  // R / 4 dependent wave rounds
+  int LP = 64;
+  while (LP > 1 && LP * R > 256) LP >>= 1;
+  const int vec = (C % 4 == 0) ? 4 : 1;
+  for (int r0 = 0; r0 < R; r0 += 256 / LP) {
+    const int r = r0 + (int)threadIdx.x / LP, j = threadIdx.x % LP;
     float t = 0.f;
-    for (int c = lane; c < C; c += 64) t += w1[r * C + c] * p[c];
-    t = fmaxf(wave_sum(t), 0.f);
-    if (lane == 0) {
+    if (r < R) {
+      const float* wr = w1 + (long)r * C;
+      if (vec == 4) {
+#pragma unroll 4
+        for (int c = j * 4; c < C; c += LP * 4) {
+          const float4 a = *reinterpret_cast<const float4*>(wr + c);
+          t += a.x * p[c] + a.y * p[c + 1] + a.z * p[c + 2] + a.w * p[c + 3];
+        }
+      } else {
+        for (int c = j; c < C; c += LP) t += wr[c] * p[c];
+      }
+    }
+    for (int o = LP >> 1; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (r < R && j == 0) {
+      t = fmaxf(t, 0.f);
       z[r] = t;
       z1[n * R + r] = t;
     }
   }
   __syncthreads();
+  // s = sigmoid(W2 z): thread per output channel, its W2 row (R contiguous
+  // floats) in 16-byte loads
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float* wc = w2 + (long)c * R;
     float t = 0.f;
-    for (int r = 0; r < R; ++r) t += w2[c * R + r] * z[r];
+    if (R % 4 == 0) {
+      for (int r = 0; r < R; r += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(wc + r);
+        t += a.x * z[r] + a.y * z[r + 1] + a.z * z[r + 2] + a.w * z[r + 3];
+      }
+    } else {
+      for (int r = 0; r < R; ++r) t += wc[r] * z[r];
+    }
     s[n * C + c] = sigmoidf_(t);
   }
 }
