@@ -950,8 +950,25 @@ extern "C" {
 long um_conv_dgrad_ws_pad(int dtype, int N, int H, int W, int C, int R, int K, int stride, int pad,
                           int pad_mode) {
   const long base = um_conv_dgrad_ws(dtype, N, H, W, C, R, K, stride);
-  if (!pad_dgrad_applies(dtype, N, C, R, pad, pad_mode, stride, H, W, H, W)) return base;
-  return std::max(base, pad_dgrad_bytes(dtype, N, H, W, C, R, K, pad, nullptr));
+  if (pad_dgrad_applies(dtype, N, C, R, pad, pad_mode, stride, H, W, H, W))
+    return std::max(base, pad_dgrad_bytes(dtype, N, H, W, C, R, K, pad, nullptr));
+  // split form of a reflect data gradient: the border-list GEMM of the fold
+  // splits its k-loop too (a few thousand rows x 9 taps: unsplit, 96-256
+  // workgroups ran 24-53 us behind a 30-87 us main pass), unless the fold is
+  // the VALU pass (um_conv2d_dgrad)
+  static const int border_split = (int)umamd::tuning_env("border_split", 1);
+  if (border_split && pad_mode == UM_PAD_REFLECT && pad > 0 && stride == 1 &&
+      split_form(dtype, N, H, W, C, R)) {
+    const int bv = umamd::igemm_border_valu();
+    if (!((bv == 2 || (bv == 1 && K <= 8)) && C % 8 == 0 && K % 8 == 0)) {
+      umamd::IgArgs a{};
+      a.oh = H; a.ow = W; a.fold_pad = pad;
+      const long mb = (long)N * umamd::igemm_border_list(a);
+      // after the main pass's own workspace (its plan stays as sized by base)
+      return base + umamd::igemm_border_ws_bytes(dtype, (int)mb, C, R * R, K);
+    }
+  }
+  return base;
 }
 
 int um_conv_stats_parts(int M, int K) {
@@ -1277,7 +1294,10 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
     a.epilogue = UM_EPI_NONE; a.accumulate = accumulate; a.epi_scale = 1.f;
     a.residual = nullptr; a.ldr = 0; a.stats = nullptr;
     // the (zero-pad) transposed conv over every pixel (all fast paths apply) ...
-    int rc = umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
+    // (its workspace: the first `base` bytes; the border GEMM's split
+    // partials follow them, um_conv_dgrad_ws_pad)
+    const long base = um_conv_dgrad_ws(dtype, N, H, W, C, R, K, stride);
+    int rc = umamd::igemm_run(dtype, a, (float*)ws, ws ? std::min(ws_bytes, base) : 0, st);
     if (rc != UM_OK || fold1 || pad_mode != UM_PAD_REFLECT || pad == 0) return rc;
     // ... then the reflect fold: the pixels rows/columns 1..pad and H-1-pad..H-2
     // also receive the gradient of the padded taps that mirrored them.  A
@@ -1301,7 +1321,9 @@ int um_conv2d_dgrad(int dtype, int N, int H, int W, int C, int ldx, void* dx, in
       UM_LAUNCH_CHECK();
       return UM_OK;
     }
-    return umamd::igemm_run(dtype, a, (float*)ws, ws_bytes, st);
+    const long rest = ws != nullptr ? ws_bytes - base : 0;
+    return umamd::igemm_run(dtype, a, rest > 0 ? (float*)((char*)ws + base) : nullptr,
+                            rest > 0 ? rest : 0, st);
   }
   // stride 2 (zero padding): four parity classes (ay, ax) of dx pixels, each
   // a stride-1 gather over dy with the weight taps of matching parity:

@@ -78,6 +78,7 @@ int igemm_stats_rows(int M, int NC);
 
 // workspace bytes the split-K heuristic wants for this shape (0: no split)
 long igemm_ws_bytes(int dtype, int M, int NC, int taps, int ach);
+long igemm_border_ws_bytes(int dtype, int M, int NC, int taps, int ach);
 // launch; ws may be null (then no split)
 int igemm_run(int dtype, const IgArgs& a, float* ws, long ws_bytes, hipStream_t st);
 

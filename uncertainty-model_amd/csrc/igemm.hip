@@ -838,6 +838,9 @@ __device__ __forceinline__ void splitk_epi_rows(const IgArgs& a, const float* __
   const long m1 = min((long)a.M, m0 + a.stats_rows);
   const long zs = (long)a.M * a.NC;
   const bool act = n < a.NC;
+  // 4 consecutive outputs as one 16-byte (f32) / 8-byte (bf16) access
+  const bool vec4 = (a.ld_out & 3) == 0 &&
+                    (reinterpret_cast<uintptr_t>(a.out) & (a.out_f32 || sizeof(T) == 4 ? 15 : 7)) == 0;
   float sm[4] = {0, 0, 0, 0}, sq[4] = {0, 0, 0, 0};
   if (act) {
     float bv[4] = {0, 0, 0, 0};
@@ -863,16 +866,52 @@ __device__ __forceinline__ void splitk_epi_rows(const IgArgs& a, const float* __
         if (a.epilogue == UM_EPI_RESIDUAL)
           v[e] += to_f32(reinterpret_cast<const T*>(a.residual)[m * a.ldr + n + e]);
         if (a.epilogue == UM_EPI_SIGMOID_SCALE) v[e] = a.epi_scale * sigmoidf_(v[e]);
-        const long off = out_row<MODE>(a, (int)m) + n + e;
+      }
+      // the row's output offset once (the border mode maps it through the
+      // reflect list), then the 4 columns as one vector access when aligned
+      const long off = out_row<MODE>(a, (int)m) + n;
+      if (vec4) {
         if (a.out_f32) {
-          float* o = reinterpret_cast<float*>(a.out) + off;
-          if (a.accumulate) v[e] += *o;
-          *o = v[e];
+          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(a.out) + off);
+          if (a.accumulate) {
+            const float4 p = *o;
+            v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+          }
+          *o = make_float4(v[0], v[1], v[2], v[3]);
+        } else if constexpr (sizeof(T) == 2) {
+          uint2* o = reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.out) + off);
+          if (a.accumulate) {
+            const uint2 p = *o;
+            v[0] += __uint_as_float(p.x << 16);
+            v[1] += __uint_as_float(p.x & 0xffff0000u);
+            v[2] += __uint_as_float(p.y << 16);
+            v[3] += __uint_as_float(p.y & 0xffff0000u);
+          }
+          *o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         } else {
-          T* o = reinterpret_cast<T*>(a.out) + off;
-          if (a.accumulate) v[e] += to_f32(*o);
-          *o = from_f32<T>(v[e]);
+          float4* o = reinterpret_cast<float4*>(reinterpret_cast<T*>(a.out) + off);
+          if (a.accumulate) {
+            const float4 p = *o;
+            v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+          }
+          *o = make_float4(v[0], v[1], v[2], v[3]);
         }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (a.out_f32) {
+            float* o = reinterpret_cast<float*>(a.out) + off + e;
+            if (a.accumulate) v[e] += *o;
+            *o = v[e];
+          } else {
+            T* o = reinterpret_cast<T*>(a.out) + off + e;
+            if (a.accumulate) v[e] += to_f32(*o);
+            *o = from_f32<T>(v[e]);
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
         sm[e] += v[e];
         sq[e] += v[e] * v[e];
       }
@@ -1220,6 +1259,16 @@ int igemm_border_list(IgArgs& a) {
 
 long igemm_ws_bytes(int dtype, int M, int NC, int taps, int ach) {
   const Plan p = make_plan(dtype, M, NC, taps, ach, -1, false);
+  return p.splits > 1 ? (long)p.splits * M * NC * 4 : 0;
+}
+
+// split-K workspace of the reflect fold's border-list GEMM (igemm_run's
+// a.border plan: 64x64 register tiles, 32-deep k-steps)
+long igemm_border_ws_bytes(int dtype, int M, int NC, int taps, int ach) {
+  (void)dtype;
+  Plan p{};
+  p.bk = 32; p.bm = 64; p.bn = 64; p.wm = 2; p.wn = 2;
+  split_plan(p, M, NC, taps, ach, -1, false);
   return p.splits > 1 ? (long)p.splits * M * NC * 4 : 0;
 }
 
