@@ -828,14 +828,18 @@ __global__ void __launch_bounds__(NW * 64) igemm_glds_cls4_kernel(IgArgs a0, IgA
 // sum the split-K partials and apply the epilogue.  Block = a.stats_rows rows x
 // 64 columns: thread (g, lane) owns columns 4g..4g+3 and rows lane, lane+16, ...
 constexpr int EPI_COLS = 64;
+// rows: the block's row count -- a.stats_rows when the epilogue takes BN
+// statistics (one partial row per statistics row block), else EPI_ROWS (more,
+// smaller blocks: one row per thread, the partial loads of all rows in flight)
+constexpr int EPI_ROWS = 16;
 template <typename T, int MODE>
 __device__ __forceinline__ void splitk_epi_rows(const IgArgs& a, const float* __restrict__ ws,
-                                                int splits, int bx) {
+                                                int splits, int bx, int rows) {
   __shared__ float red[16][16][8];
   const int g = threadIdx.x & 15, lane = threadIdx.x >> 4;
   const int n = blockIdx.y * EPI_COLS + g * 4;  // NC % 4 == 0 (host-checked)
-  const long m0 = (long)bx * a.stats_rows;
-  const long m1 = min((long)a.M, m0 + a.stats_rows);
+  const long m0 = (long)bx * rows;
+  const long m1 = min((long)a.M, m0 + rows);
   const long zs = (long)a.M * a.NC;
   const bool act = n < a.NC;
   // 4 consecutive outputs as one 16-byte (f32) / 8-byte (bf16) access
@@ -946,8 +950,8 @@ __device__ __forceinline__ void splitk_epi_rows(const IgArgs& a, const float* __
 
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) splitk_epilogue_kernel(IgArgs a, const float* __restrict__ ws,
-                                                               int splits) {
-  splitk_epi_rows<T, MODE>(a, ws, splits, blockIdx.x);
+                                                               int splits, int rows) {
+  splitk_epi_rows<T, MODE>(a, ws, splits, blockIdx.x, rows);
 }
 
 // the split-K sums of igemm_glds_cls4_kernel: class c owns row blocks
@@ -959,10 +963,10 @@ __global__ void __launch_bounds__(256) splitk_epilogue_cls4_kernel(IgArgs a0, Ig
                                                                     const float* __restrict__ ws,
                                                                     long4 wsoff) {
   const int b = blockIdx.x;
-  if (b < rstart.y) splitk_epi_rows<T, 1>(a0, ws + wsoff.x, splits.x, b - rstart.x);
-  else if (b < rstart.z) splitk_epi_rows<T, 1>(a1, ws + wsoff.y, splits.y, b - rstart.y);
-  else if (b < rstart.w) splitk_epi_rows<T, 1>(a2, ws + wsoff.z, splits.z, b - rstart.z);
-  else splitk_epi_rows<T, 1>(a3, ws + wsoff.w, splits.w, b - rstart.w);
+  if (b < rstart.y) splitk_epi_rows<T, 1>(a0, ws + wsoff.x, splits.x, b - rstart.x, a0.stats_rows);
+  else if (b < rstart.z) splitk_epi_rows<T, 1>(a1, ws + wsoff.y, splits.y, b - rstart.y, a1.stats_rows);
+  else if (b < rstart.w) splitk_epi_rows<T, 1>(a2, ws + wsoff.z, splits.z, b - rstart.z, a2.stats_rows);
+  else splitk_epi_rows<T, 1>(a3, ws + wsoff.w, splits.w, b - rstart.w, a3.stats_rows);
 }
 
 struct Plan {
@@ -1169,10 +1173,12 @@ int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
       else
         hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, 4, false, MODE, 3>), grid, dim3(256), 0, st, g, ws,
                            p.steps, p.per, ntn);
-      if (p.splits > 1)
+      if (p.splits > 1) {
+        const int er = a.epilogue == UM_EPI_STATS ? a.stats_rows : EPI_ROWS;
         hipLaunchKernelGGL((splitk_epilogue_kernel<T, MODE>),
-                           dim3(ceil_div(a.M, a.stats_rows), ceil_div(a.NC, EPI_COLS)), dim3(256), 0,
-                           st, a, (const float*)ws, p.splits);
+                           dim3(ceil_div(a.M, er), ceil_div(a.NC, EPI_COLS)), dim3(256), 0, st, a,
+                           (const float*)ws, p.splits, er);
+      }
       UM_LAUNCH_CHECK();
       return UM_OK;
     }
@@ -1180,9 +1186,10 @@ int launch_cls(const IgArgs& a, const Plan& p, float* ws, hipStream_t st) {
   if (p.splits > 1) {
     hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, true, MODE>),
                        dim3(ntm * ntn, 1, p.splits), dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
+    const int er = a.epilogue == UM_EPI_STATS ? a.stats_rows : EPI_ROWS;
     hipLaunchKernelGGL((splitk_epilogue_kernel<T, MODE>),
-                       dim3(ceil_div(a.M, a.stats_rows), ceil_div(a.NC, EPI_COLS)), dim3(256), 0, st,
-                       a, (const float*)ws, p.splits);
+                       dim3(ceil_div(a.M, er), ceil_div(a.NC, EPI_COLS)), dim3(256), 0, st, a,
+                       (const float*)ws, p.splits, er);
   } else {
     hipLaunchKernelGGL((igemm_kernel<T, BK, BM, BN, WM, WN, false, MODE>), dim3(ntm * ntn, 1, 1),
                        dim3(256), 0, st, a, ws, p.steps, p.per, ntn);
