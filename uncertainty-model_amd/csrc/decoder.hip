@@ -154,9 +154,18 @@ __device__ __forceinline__ void cat_vals(const CatSrc& s, int n, int y, int x, i
       v[e] = sub == 0 ? q[4 * e] : sub == 1 ? q[4 * e + 1] : sub == 2 ? q[4 * e + 2] : q[4 * e + 3];
   }
   if (s.scale) {
+    const float* g = s.scale + n * s.C + cc;
+    if ((s.C & 3) == 0 && cc + 8 <= s.C && (reinterpret_cast<uintptr_t>(s.scale) & 15) == 0) {
+      // the gate row's 8 values as two 16-byte loads
+      const float4 g0 = *reinterpret_cast<const float4*>(g);
+      const float4 g1 = *reinterpret_cast<const float4*>(g + 4);
+      v[0] *= g0.x; v[1] *= g0.y; v[2] *= g0.z; v[3] *= g0.w;
+      v[4] *= g1.x; v[5] *= g1.y; v[6] *= g1.z; v[7] *= g1.w;
+    } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      if (cc + e < s.C) v[e] *= s.scale[n * s.C + cc + e];
+      for (int e = 0; e < 8; ++e)
+        if (cc + e < s.C) v[e] *= g[e];
+    }
   }
 }
 
