@@ -530,6 +530,35 @@ def test_conv_fwd_up2_slots(case, yact):
     assert float(slots[-1]) == N * H * W
 
 
+# the decoder's second concat: the upsample conv's output pixel-shuffled
+# (PixelShuffle(2), source [N][h][w][4C] -> [N][2h][2w][C]) next to a gated
+# copy source, bf16 and f32, odd source sizes, against torch pixel_shuffle +
+# cat; and the adjoint of the shuffled source
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('h,w,C', [(4, 8, 16), (5, 7, 32), (3, 33, 8), (16, 32, 64)])
+def test_pshuf_concat(dtype, h, w, C):
+    from umamd import functional as U
+    from umamd._lib import CAT_COPY, CAT_PSHUF
+    N, C2 = 2, 24
+    torch.manual_seed(h + w + C)
+    up = torch.randn(N, 4 * C, h, w)
+    cp = torch.randn(N, C2, 2 * h, 2 * w)
+    gate = torch.rand(N, C2)
+    upq, cpq = up.to(dtype).float(), cp.to(dtype).float()
+    ref = torch.cat([F.pixel_shuffle(upq, 2), cpq * gate[:, :, None, None]], 1)
+    ud = _nhwc(upq).to(dtype).requires_grad_(True)
+    cd = _nhwc(cpq).to(dtype)
+    y, _ = U.concat([U.CatSource(ud, CAT_PSHUF, C), U.CatSource(cd, CAT_COPY, C2, gate.to(DEV))],
+                    N, 2 * h, 2 * w, dtype)
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-6
+    assert _rel(_nchw(y[..., :C + C2].float()), ref) < tol
+    assert torch.equal(_nchw(y[..., :C].float()).cpu(), F.pixel_shuffle(upq, 2))
+    go = torch.randn(N, 2 * h, 2 * w, y.shape[-1], device=DEV)
+    (y.float() * go).sum().backward()
+    gref = F.pixel_unshuffle(go[..., :C].permute(0, 3, 1, 2).cpu(), 2)
+    assert _rel(_nchw(ud.grad.float()), gref) < tol
+
+
 # x2 bilinear (align_corners=True) upsample of a concat source: forward and
 # the adjoint (branch-free 6x6 window for low-res sides >= 4, general path
 # below), with and without an SE gate, against torch
